@@ -1,0 +1,124 @@
+/*
+ * libsesa -- MI355X-native chunked source-separation hot path (C ABI).
+ *
+ * Drop-in boundary for the reference's separation hot path
+ * (test4373/SESA-Audio-Separation).  Plain pointers and sizes, no torch
+ * types.  All tensors are DEVICE pointers owned by the caller; `stream` is a hipStream_t
+ * (NULL = default stream).  Every entry point is asynchronous on `stream`, never synchronises
+ * the host, never allocates inside a launch function (safe under hipGraph capture), and
+ * returns 0 on success or a negative SESA_ERR_* code with a thread-local message available
+ * from sesa_last_error().
+ *
+ * Compute is fp32 in / fp32 out.  The MDX23C network runs its contractions on MFMA in one of
+ * two precisions (sesa_mdx23c_config.precision):
+ *   SESA_PREC_BF16X3 -- hi/lo bf16 split, 3 MFMA passes, fp32 accumulate (parity mode:
+ *                       ~1.4e-6 RMS vs the fp32 reference on the vocals config)
+ *   SESA_PREC_BF16   -- single bf16 pass (throughput mode; ~6e-4 RMS, outside the 1e-4 gate)
+ */
+#ifndef SESA_H_
+#define SESA_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SESA_OK 0
+#define SESA_ERR_INVALID (-1)   /* bad argument / unsupported configuration              */
+#define SESA_ERR_HIP (-2)       /* HIP runtime error                                      */
+#define SESA_ERR_STATE (-3)     /* object used in the wrong state (e.g. params missing)    */
+#define SESA_ERR_NOMEM (-4)     /* device allocation failed (create/finalize only)         */
+
+#define SESA_PREC_BF16X3 0
+#define SESA_PREC_BF16 1
+
+int sesa_version(void);
+const char* sesa_last_error(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Spectral front/back end.
+ * Replaces models/mdx23c_tfc_tdf_v3.py:14-30 (STFT.__call__ -> torch.stft, center=True,
+ * reflect pad, periodic Hann, onesided, un-normalised, cropped to dim_f bins).
+ *   x   [n_sig, len]                 fp32
+ *   out [n_sig, 2 (re,im), dim_f, frames]  frames = 1 + len / hop
+ * (for n_sig = B*c this is exactly the reference's [B, 2c, dim_f, frames] output).
+ * Supported: n_fft == 8192, len % hop == 0, len > n_fft/2.
+ */
+int sesa_stft_f32(const float* x, int n_sig, int len, int n_fft, int hop, int dim_f, float* out,
+                  void* stream);
+
+/* Replaces models/mdx23c_tfc_tdf_v3.py:32-44 (STFT.inverse: zero-pad bins dim_f..n_fft/2,
+ * torch.istft center=True without `length`).
+ *   spec [n_sig, 2 (re,im), dim_f, frames] fp32
+ *   out  [n_sig, hop * (frames - 1)]       fp32
+ * `frame_ws` is caller-owned scratch of sesa_istft_workspace_size(...) bytes.
+ */
+size_t sesa_istft_workspace_size(int n_sig, int frames, int n_fft);
+int sesa_istft_f32(const float* spec, int n_sig, int dim_f, int frames, int n_fft, int hop,
+                   float* out, void* frame_ws, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Chunker / windowed overlap-add (inference_pytorch.py:55-186 == utils.py:330-477 generic).
+ *
+ * sesa_chunk_gather_f32 -- inference_pytorch.py:102-103 + :125-138: builds the batch
+ *   out[j] = pad_C( reflect_pad_border(mix)[:, starts[j] : starts[j]+C] ) for j < n_chunks,
+ *   where the border reflect pad is applied iff `border` > 0 (caller passes 0 when the
+ *   reference would not pad) and a short chunk is padded with reflect if its length > C/2
+ *   else with zeros.
+ *   mix [n_ch, L] (unpadded), starts (host int64 array, padded coordinates), out [n_chunks, n_ch, C]
+ */
+int sesa_chunk_gather_f32(const float* mix, int n_ch, int64_t L, int64_t border,
+                          const int64_t* starts, int n_chunks, int chunk, float* out, void* stream);
+
+/* sesa_ola_accumulate_f32 -- inference_pytorch.py:151-159.  For chunk j (in order):
+ *   result[:, s_j : s_j+n_j] += y[j, :, :n_j] * window[:n_j];  counter[s_j : s_j+n_j] += window[:n_j]
+ * with fp32 multiply-then-add rounding and chunk-order summation exactly as the reference.
+ *   y [n_chunks, n_out_ch, C] (n_out_ch = n_instr * 2), window [C] (device, the batch's window
+ *   after the first/last fade fix-ups), result [n_out_ch, L_pad], counter [L_pad].
+ *   starts / seg_lens are host arrays (the chunk plan is host-side control).
+ */
+int sesa_ola_accumulate_f32(const float* y, int n_chunks, int n_out_ch, int chunk,
+                            const int64_t* starts, const int64_t* seg_lens, const float* window,
+                            float* result, float* counter, int64_t L_pad, void* stream);
+
+/* sesa_ola_finalize_f32 -- inference_pytorch.py:174-180: out = nan_to_num(result / counter,
+ * nan=0) cropped to [border, L_pad - border).  out [n_out_ch, L_pad - 2*border]. */
+int sesa_ola_finalize_f32(const float* result, const float* counter, int n_out_ch, int64_t L_pad,
+                          int64_t border, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * MDX23C TFC-TDF-v3 network (models/mdx23c_tfc_tdf_v3.py:141-242, TFC_TDF_net).
+ * Only norm == InstanceNorm and act == gelu are supported (the released configs).
+ */
+typedef struct sesa_mdx23c_config {
+  int chunk_size, dim_f, dim_t, hop_length, n_fft, audio_channels;   /* audio.*            */
+  int num_subbands, num_scales, num_blocks_per_scale, num_channels;  /* model.*            */
+  int growth, bottleneck_factor, scale_t, scale_f;
+  int num_instruments;                                               /* prefer_target_instrument */
+  int precision;                                                     /* SESA_PREC_*        */
+} sesa_mdx23c_config;
+
+typedef struct sesa_mdx23c sesa_mdx23c;
+
+/* Build the network plan on the current HIP device. */
+int sesa_mdx23c_create(const sesa_mdx23c_config* cfg, sesa_mdx23c** out);
+/* Number of parameters and the i-th (name, numel) in the reference named_parameters() order. */
+int sesa_mdx23c_num_params(const sesa_mdx23c* m);
+int sesa_mdx23c_param_info(const sesa_mdx23c* m, int i, const char** name, int64_t* numel);
+/* Copy one parameter (HOST fp32, reference state_dict layout) by its reference name
+ * (load_state_dict semantics; unknown names return SESA_ERR_INVALID). */
+int sesa_mdx23c_set_param(sesa_mdx23c* m, const char* name, const float* host, int64_t numel);
+/* Pack weights into the MFMA layouts on the device (after every parameter was set). */
+int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream);
+size_t sesa_mdx23c_workspace_size(const sesa_mdx23c* m, int batch);
+/* x [batch, audio_channels, chunk_size] -> out [batch, num_instruments, audio_channels, chunk_size] */
+int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, float* out, void* workspace,
+                        size_t workspace_bytes, void* stream);
+int sesa_mdx23c_destroy(sesa_mdx23c* m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SESA_H_ */

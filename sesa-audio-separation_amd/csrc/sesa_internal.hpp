@@ -1,0 +1,15 @@
+// Internal launchers shared between translation units of libsesa.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace sesa {
+
+int get_spectral_tables(const float2** tw4096, const float2** twN, const float** window);
+
+// layout 0 = reference layout, 1 = MDX23C channels-last sub-band image (see sesa_spectral.hip).
+int stft_launch(const float* x, int n_sig, int len, int hop, int dim_f, int layout, int nsub, float* out,
+                hipStream_t st);
+int istft_launch(const float* spec, int n_sig, int dim_f, int frames, int hop, int layout, int nsub, int ni,
+                 float* out, float* frame_ws, hipStream_t st);
+
+}  // namespace sesa

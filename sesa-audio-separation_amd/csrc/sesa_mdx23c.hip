@@ -1,0 +1,572 @@
+// MDX23C TFC-TDF-v3 network: parameter registry, weight packing and the forward pass (gfx950).
+//
+// Reference: models/mdx23c_tfc_tdf_v3.py:141-242 (TFC_TDF_net), :100-138 (TFC_TDF), :74-97
+// (Upscale / Downscale), :14-44 (STFT).  Parameter names/shapes follow the reference
+// named_parameters() order (so checkpoints load by state_dict key, load_state_dict semantics).
+//
+// Forward (all on one stream, no host sync, no allocation):
+//   STFT (sub-band channels-last image) -> first_conv -> encoder [TFC_TDF, Downscale] x n
+//   -> bottleneck TFC_TDF -> decoder [Upscale, cat, TFC_TDF] x n -> (x * first_conv_out,
+//   cat mix) final 1x1 -> GELU -> 1x1 -> iSTFT.
+// Every InstanceNorm+GELU is fused into the prologue of its consumer and every norm statistic
+// into the epilogue of its producer (sesa_tapgemm.hip), so each block is exactly
+//   shortcut 1x1, conv3x3, linear, linear(+res), conv3x3(+res)   -- five launches.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "sesa_common.hpp"
+#include "sesa_internal.hpp"
+#include "sesa_tapgemm.hpp"
+
+namespace sesa {
+namespace {
+
+uint16_t f2bf(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+float bf2f(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+struct Param {
+  std::string name;
+  std::vector<int64_t> shape;
+  int64_t numel = 0;
+  std::vector<float> host;
+  bool set = false;
+};
+
+struct ConvW {
+  int kind = 0, C_in = 0, C_out = 0, n_cols = 0, bn = 64, param = -1;
+  int64_t w_off = 0;  // uint16 offset into the packed weight blob
+};
+struct TdfW {
+  int M = 0, K = 0, param = -1;
+  int64_t w_off = 0;
+};
+struct Norm {
+  int gamma = -1, beta = -1;   // param indices
+  int64_t off_g = 0, off_b = 0;  // float offsets into the affine blob
+};
+struct Block {
+  Norm tfc1, tdf0, tdf3, tfc2;
+  ConvW conv1, conv2, shortcut;
+  TdfW lin1, lin2;
+  int in_c = 0, c = 0;
+};
+struct Stack {
+  std::vector<Block> blocks;
+};
+struct Level {
+  int T, F, c;
+};
+
+}  // namespace
+}  // namespace sesa
+
+struct sesa_mdx23c {
+  sesa_mdx23c_config cfg;
+  int dim_c = 0, F0 = 0, T0 = 0, ni = 0;
+  std::vector<sesa::Param> params;
+  std::map<std::string, int> by_name;
+  std::vector<sesa::Level> lv;
+  sesa::ConvW first_conv, final0, final2;
+  std::vector<sesa::Stack> enc, dec;
+  std::vector<sesa::Norm> down_norm, up_norm;
+  std::vector<sesa::ConvW> down, up;
+  sesa::Stack bottleneck;
+  uint16_t* d_w = nullptr;
+  float* d_affine = nullptr;
+  bool finalized = false;
+  int device = 0;
+};
+
+namespace sesa {
+namespace {
+
+int add_param(sesa_mdx23c* m, const std::string& name, std::vector<int64_t> shape) {
+  Param p;
+  p.name = name;
+  p.shape = shape;
+  p.numel = 1;
+  for (auto s : shape) p.numel *= s;
+  m->by_name[name] = (int)m->params.size();
+  m->params.push_back(std::move(p));
+  return (int)m->params.size() - 1;
+}
+
+Norm add_norm(sesa_mdx23c* m, const std::string& prefix, int c) {
+  Norm n;
+  n.gamma = add_param(m, prefix + ".weight", {c});
+  n.beta = add_param(m, prefix + ".bias", {c});
+  return n;
+}
+
+ConvW add_conv(sesa_mdx23c* m, const std::string& name, int kind, int c_out, int c_in, int kh, int kw) {
+  ConvW w;
+  w.kind = kind;
+  w.C_in = c_in;
+  w.C_out = c_out;
+  if (kind == DECONV2X2S2) {
+    w.param = add_param(m, name, {c_in, c_out, kh, kw});  // ConvTranspose2d weight [in, out, kh, kw]
+    w.n_cols = 4 * c_out;
+  } else {
+    w.param = add_param(m, name, {c_out, c_in, kh, kw});
+    w.n_cols = c_out;
+  }
+  w.bn = (kind == CONV1X1 && w.n_cols <= 32) ? 32 : 64;
+  return w;
+}
+
+// TFC_TDF.__init__ (mdx23c_tfc_tdf_v3.py:100-129)
+Stack add_stack(sesa_mdx23c* m, const std::string& prefix, int in_c, int c, int f, int l, int bn) {
+  Stack s;
+  for (int i = 0; i < l; ++i) {
+    const std::string p = prefix + ".blocks." + std::to_string(i);
+    Block b;
+    b.in_c = in_c;
+    b.c = c;
+    b.tfc1 = add_norm(m, p + ".tfc1.0", in_c);
+    b.conv1 = add_conv(m, p + ".tfc1.2.weight", CONV3X3, c, in_c, 3, 3);
+    b.tdf0 = add_norm(m, p + ".tdf.0", c);
+    b.lin1.param = add_param(m, p + ".tdf.2.weight", {f / bn, f});
+    b.lin1.M = f / bn;
+    b.lin1.K = f;
+    b.tdf3 = add_norm(m, p + ".tdf.3", c);
+    b.lin2.param = add_param(m, p + ".tdf.5.weight", {f, f / bn});
+    b.lin2.M = f;
+    b.lin2.K = f / bn;
+    b.tfc2 = add_norm(m, p + ".tfc2.0", c);
+    b.conv2 = add_conv(m, p + ".tfc2.2.weight", CONV3X3, c, c, 3, 3);
+    b.shortcut = add_conv(m, p + ".shortcut.weight", CONV1X1, c, in_c, 1, 1);
+    s.blocks.push_back(b);
+    in_c = c;
+  }
+  return s;
+}
+
+// ---- weight packing (layouts consumed by sesa_tapgemm.hip) ----
+void pack_conv(const Param& P, ConvW& w, std::vector<uint16_t>& blob) {
+  const bool tr = w.kind == DECONV2X2S2;
+  const int KH = (int)P.shape[2], KW = (int)P.shape[3];
+  const int taps = tr ? 1 : KH * KW;
+  const int BN = w.bn;
+  const int N = w.n_cols;
+  const int nblk = (N + BN - 1) / BN;
+  const int nch = w.C_in / kConvBK;
+  w.w_off = (int64_t)blob.size();
+  const int64_t img = (int64_t)taps * BN * 16;  // uint16 per image
+  blob.resize(blob.size() + (size_t)nblk * nch * 2 * img, 0);
+  uint16_t* base = blob.data() + w.w_off;
+  const float* W = P.host.data();
+  for (int nb = 0; nb < nblk; ++nb)
+    for (int kc = 0; kc < nch; ++kc) {
+      uint16_t* hi = base + ((int64_t)nb * nch + kc) * 2 * img;
+      uint16_t* lo = hi + img;
+      for (int tap = 0; tap < taps; ++tap)
+        for (int n = 0; n < BN; ++n)
+          for (int kk = 0; kk < kConvBK; ++kk) {
+            const int ncol = nb * BN + n, ci = kc * kConvBK + kk;
+            float v = 0.f;
+            if (ncol < N) {
+              if (!tr) {
+                const int dy = tap / KW, dx = tap % KW;
+                v = W[(((int64_t)ncol * w.C_in + ci) * KH + dy) * KW + dx];
+              } else {
+                const int t2 = ncol / w.C_out, co = ncol % w.C_out;
+                v = W[(((int64_t)ci * w.C_out + co) * 2 + (t2 >> 1)) * 2 + (t2 & 1)];
+              }
+            }
+            const int p = tap * BN + n;
+            const int64_t o = (int64_t)p * 16 + ((((kk >> 3) ^ ((p >> 3) & 1))) << 3) + (kk & 7);
+            const uint16_t h = f2bf(v);
+            hi[o] = h;
+            lo[o] = f2bf(v - bf2f(h));
+          }
+    }
+}
+
+void pack_tdf(const Param& P, TdfW& w, std::vector<uint16_t>& blob) {
+  const int M = w.M, K = w.K;
+  const int nmb = (M + kTdfBM - 1) / kTdfBM;
+  const int nch = (K + kTdfBK - 1) / kTdfBK;
+  w.w_off = (int64_t)blob.size();
+  const int64_t img = (int64_t)kTdfBM * kTdfBK;
+  blob.resize(blob.size() + (size_t)nmb * nch * 2 * img, 0);
+  uint16_t* base = blob.data() + w.w_off;
+  const float* W = P.host.data();
+  for (int mb = 0; mb < nmb; ++mb)
+    for (int kc = 0; kc < nch; ++kc) {
+      uint16_t* hi = base + ((int64_t)mb * nch + kc) * 2 * img;
+      uint16_t* lo = hi + img;
+      for (int row = 0; row < kTdfBM; ++row)
+        for (int kk = 0; kk < kTdfBK; ++kk) {
+          const int m = mb * kTdfBM + row, k = kc * kTdfBK + kk;
+          const float v = (m < M && k < K) ? W[(int64_t)m * K + k] : 0.f;
+          const int64_t o = (int64_t)row * kTdfBK + (((kk >> 3) ^ ((row >> 2) & 3)) << 3) + (kk & 7);
+          const uint16_t h = f2bf(v);
+          hi[o] = h;
+          lo[o] = f2bf(v - bf2f(h));
+        }
+    }
+}
+
+void pack_norm(sesa_mdx23c* m, Norm& n, std::vector<float>& aff) {
+  n.off_g = (int64_t)aff.size();
+  aff.insert(aff.end(), m->params[n.gamma].host.begin(), m->params[n.gamma].host.end());
+  n.off_b = (int64_t)aff.size();
+  aff.insert(aff.end(), m->params[n.beta].host.begin(), m->params[n.beta].host.end());
+}
+
+// ---- forward ----
+struct Tensor {
+  float* p = nullptr;
+  double* st = nullptr;
+  int C = 0;
+};
+
+struct Fwd {
+  sesa_mdx23c* m;
+  hipStream_t st;
+  bool dry;
+  int B;
+  int x3;
+  char* ws;
+  size_t off = 0;        // float region bump offset (bytes)
+  size_t stats_off = 0;  // stats region bump offset (bytes), relative to stats_base
+  char* stats_base = nullptr;
+  size_t stats_cap = 0;
+  int rc = SESA_OK;
+
+  float* buf(int64_t nfloat) {
+    float* p = dry ? nullptr : reinterpret_cast<float*>(ws + off);
+    off += ((size_t)nfloat * 4 + 255) & ~(size_t)255;
+    return p;
+  }
+  double* stats(int C) {
+    double* p = dry ? nullptr : reinterpret_cast<double*>(stats_base + stats_off);
+    stats_off += (((size_t)B * C * 2 * 8) + 255) & ~(size_t)255;
+    return p;
+  }
+  const float* aff(int64_t off_f) const { return m->d_affine + off_f; }
+
+  GemmIn input(Tensor a, Tensor b, int mode_a, int mode_b, const Norm* nrm, int T, int F) const {
+    GemmIn in{};
+    in.src[0] = Src{a.p, a.st, nullptr, a.C, mode_a};
+    in.src[1] = b.p ? Src{b.p, b.st, nullptr, b.C, mode_b} : Src{a.p, a.st, nullptr, a.C, mode_a};
+    in.C_split = a.C;
+    in.C_in = a.C + (b.p ? b.C : 0);
+    in.gamma = nrm ? aff(nrm->off_g) : nullptr;
+    in.beta = nrm ? aff(nrm->off_b) : nullptr;
+    in.inv_count = 1.0 / ((double)T * (double)F);
+    return in;
+  }
+
+  void conv(const ConvW& w, const GemmIn& in, int T_in, int F_in, int T_out, int F_out, float* out,
+            const float* residual, double* out_stats, int gelu) {
+    if (dry || rc) return;
+    ConvArgs a{};
+    a.in = in;
+    a.out = GemmOut{out, residual, out_stats, w.C_out, gelu};
+    a.w = m->d_w + w.w_off;
+    a.T_in = T_in;
+    a.F_in = F_in;
+    a.T_out = T_out;
+    a.F_out = F_out;
+    a.n_cols = w.n_cols;
+    a.n_chunks = w.C_in / kConvBK;
+    rc = launch_conv(w.kind, w.bn, x3, a, B, st);
+  }
+
+  void tdf(const TdfW& w, const GemmIn& in, int T, float* out, const float* residual, double* out_stats, int C) {
+    if (dry || rc) return;
+    TdfArgs a{};
+    a.in = in;
+    a.out = GemmOut{out, residual, out_stats, C, 0};
+    a.w = m->d_w + w.w_off;
+    a.T = T;
+    a.K = w.K;
+    a.M = w.M;
+    a.n_chunks = (w.K + kTdfBK - 1) / kTdfBK;
+    rc = launch_tdf(x3, a, B, st);
+  }
+
+  // TFC_TDF.forward (mdx23c_tfc_tdf_v3.py:131-138)
+  Tensor stack(const Stack& s, Tensor x0, Tensor x1, const Level& L) {
+    const int bnf = m->cfg.bottleneck_factor;
+    for (size_t i = 0; i < s.blocks.size(); ++i) {
+      const Block& bk = s.blocks[i];
+      const int c = bk.c;
+      const int64_t plane = (int64_t)B * L.T * L.F * c;
+      float* S = buf(plane);
+      float* H = buf(plane);
+      float* U = buf((int64_t)B * L.T * (L.F / bnf) * c);
+      double* st_h1 = stats(c);
+      double* st_u = stats(c);
+      double* st_h2 = stats(c);
+      double* st_out = stats(c);
+      // s = shortcut(x)
+      conv(bk.shortcut, input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F), L.T, L.F, L.T, L.F, S, nullptr, nullptr, 0);
+      // x = tfc1(x)
+      conv(bk.conv1, input(x0, x1, SRC_NORM_GELU, SRC_NORM_GELU, &bk.tfc1, L.T, L.F), L.T, L.F, L.T, L.F, H, nullptr,
+           st_h1, 0);
+      // x = x + tdf(x)
+      tdf(bk.lin1, input(Tensor{H, st_h1, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf0, L.T, L.F), L.T, U, nullptr, st_u,
+          c);
+      tdf(bk.lin2, input(Tensor{U, st_u, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf3, L.T, L.F / bnf), L.T, H, H, st_h2,
+          c);
+      // x = tfc2(x) + s
+      conv(bk.conv2, input(Tensor{H, st_h2, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tfc2, L.T, L.F), L.T, L.F, L.T, L.F, S,
+           S, st_out, 0);
+      x0 = Tensor{S, st_out, c};
+      x1 = Tensor{};
+    }
+    return x0;
+  }
+
+  // TFC_TDF_net.forward (mdx23c_tfc_tdf_v3.py:205-242)
+  void run(const float* x, float* out) {
+    const sesa_mdx23c_config& c = m->cfg;
+    const int n = c.num_scales;
+    const int T = m->T0, F = m->F0, dc = m->dim_c;
+    Tensor mix{buf((int64_t)B * T * F * dc), nullptr, dc};
+    if (!dry && !rc) rc = stft_launch(x, B * 2, c.chunk_size, c.hop_length, c.dim_f, 1, c.num_subbands, mix.p, st);
+    Tensor fco{buf((int64_t)B * T * F * c.num_channels), stats(c.num_channels), c.num_channels};
+    conv(m->first_conv, input(mix, Tensor{}, SRC_RAW, 0, nullptr, T, F), T, F, T, F, fco.p, nullptr, fco.st, 0);
+    Tensor xt = fco;
+    std::vector<Tensor> skips;
+    for (int l = 0; l < n; ++l) {
+      const Level& L = m->lv[l];
+      const Level& L1 = m->lv[l + 1];
+      Tensor y = stack(m->enc[l], xt, Tensor{}, L);
+      skips.push_back(y);
+      Tensor d{buf((int64_t)B * L1.T * L1.F * L1.c), stats(L1.c), L1.c};
+      conv(m->down[l], input(y, Tensor{}, SRC_NORM_GELU, 0, &m->down_norm[l], L.T, L.F), L.T, L.F, L1.T, L1.F, d.p,
+           nullptr, d.st, 0);
+      xt = d;
+    }
+    xt = stack(m->bottleneck, xt, Tensor{}, m->lv[n]);
+    for (int i = 0; i < n; ++i) {
+      const int l = n - 1 - i;
+      const Level& L = m->lv[l];
+      const Level& L1 = m->lv[l + 1];
+      Tensor upt{buf((int64_t)B * L.T * L.F * L.c), stats(L.c), L.c};
+      // Upscale: GEMM over the level-(l+1) positions, N = 4*c_l, scattered to 2x2 outputs
+      conv(m->up[i], input(xt, Tensor{}, SRC_NORM_GELU, 0, &m->up_norm[i], L1.T, L1.F), L1.T, L1.F, L1.T, L1.F, upt.p,
+           nullptr, upt.st, 0);
+      xt = stack(m->dec[i], upt, skips[l], L);
+    }
+    // x = x * first_conv_out; x = final_conv(cat([mix, x]))
+    float* f1 = buf((int64_t)B * T * F * c.num_channels);
+    {
+      GemmIn in = input(mix, xt, SRC_RAW, SRC_MUL, nullptr, T, F);
+      in.src[1].mul = fco.p;
+      conv(m->final0, in, T, F, T, F, f1, nullptr, nullptr, 1);
+    }
+    const int cf = m->ni * dc;
+    float* fin = buf((int64_t)B * T * F * cf);
+    conv(m->final2, input(Tensor{f1, nullptr, c.num_channels}, Tensor{}, SRC_RAW, 0, nullptr, T, F), T, F, T, F, fin,
+         nullptr, nullptr, 0);
+    float* frames = buf((int64_t)B * m->ni * 2 * T * c.n_fft);
+    if (!dry && !rc)
+      rc = istft_launch(fin, B * m->ni * 2, c.dim_f, T, c.hop_length, 1, c.num_subbands, m->ni, out, frames, st);
+  }
+};
+
+}  // namespace
+}  // namespace sesa
+
+using namespace sesa;
+
+extern "C" int sesa_mdx23c_create(const sesa_mdx23c_config* cfg, sesa_mdx23c** out) {
+  clear_error();
+  SESA_REQUIRE(cfg && out, SESA_ERR_INVALID, "sesa_mdx23c_create: null argument");
+  const sesa_mdx23c_config& c = *cfg;
+  SESA_REQUIRE(c.n_fft == 8192, SESA_ERR_INVALID, "mdx23c: only n_fft=8192 is supported");
+  SESA_REQUIRE(c.audio_channels == 2, SESA_ERR_INVALID, "mdx23c: only stereo audio is supported");
+  SESA_REQUIRE(c.scale_t == 2 && c.scale_f == 2, SESA_ERR_INVALID, "mdx23c: only scale [2,2] is supported");
+  SESA_REQUIRE(c.chunk_size == c.hop_length * (c.dim_t - 1), SESA_ERR_INVALID,
+               "mdx23c: chunk_size must equal hop_length*(dim_t-1) (got %d vs %d*%d)", c.chunk_size, c.hop_length,
+               c.dim_t - 1);
+  SESA_REQUIRE(c.num_subbands > 0 && c.dim_f % c.num_subbands == 0 && c.dim_f <= c.n_fft / 2, SESA_ERR_INVALID,
+               "mdx23c: bad dim_f / num_subbands");
+  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16, SESA_ERR_INVALID,
+               "mdx23c: bad precision %d", c.precision);
+  const int F0 = c.dim_f / c.num_subbands;
+  const int n = c.num_scales;
+  SESA_REQUIRE(n >= 1 && c.num_blocks_per_scale >= 1 && c.bottleneck_factor >= 1, SESA_ERR_INVALID,
+               "mdx23c: bad scales/blocks");
+  const int Fb = F0 >> n, Tb = c.dim_t >> n;
+  SESA_REQUIRE(Fb >= 32 && Fb % 32 == 0 && (F0 % (1 << n)) == 0 && Tb >= 1 && (c.dim_t % (1 << n)) == 0,
+               SESA_ERR_INVALID, "mdx23c: dim_f/num_subbands/2^num_scales must be a multiple of 32 (got %d)", Fb);
+  SESA_REQUIRE(c.num_channels % 16 == 0 && c.growth % 16 == 0, SESA_ERR_INVALID,
+               "mdx23c: num_channels and growth must be multiples of 16");
+  SESA_REQUIRE(c.num_instruments >= 1, SESA_ERR_INVALID, "mdx23c: num_instruments >= 1");
+
+  sesa_mdx23c* m = new sesa_mdx23c();
+  m->cfg = c;
+  m->dim_c = c.num_subbands * c.audio_channels * 2;
+  m->F0 = F0;
+  m->T0 = c.dim_t;
+  m->ni = c.num_instruments;
+  (void)hipGetDevice(&m->device);
+  const int l = c.num_blocks_per_scale, g = c.growth, bn = c.bottleneck_factor;
+  int ch = c.num_channels, f = F0, t = c.dim_t;
+  m->first_conv = add_conv(m, "first_conv.weight", CONV1X1, ch, m->dim_c, 1, 1);
+  for (int i = 0; i < n; ++i) {
+    m->lv.push_back(Level{t, f, ch});
+    m->enc.push_back(add_stack(m, "encoder_blocks." + std::to_string(i) + ".tfc_tdf", ch, ch, f, l, bn));
+    m->down_norm.push_back(add_norm(m, "encoder_blocks." + std::to_string(i) + ".downscale.conv.0", ch));
+    m->down.push_back(
+        add_conv(m, "encoder_blocks." + std::to_string(i) + ".downscale.conv.2.weight", CONV2X2S2, ch + g, ch, 2, 2));
+    f /= 2;
+    t /= 2;
+    ch += g;
+  }
+  m->lv.push_back(Level{t, f, ch});
+  m->bottleneck = add_stack(m, "bottleneck_block", ch, ch, f, l, bn);
+  for (int i = 0; i < n; ++i) {
+    m->up_norm.push_back(add_norm(m, "decoder_blocks." + std::to_string(i) + ".upscale.conv.0", ch));
+    m->up.push_back(
+        add_conv(m, "decoder_blocks." + std::to_string(i) + ".upscale.conv.2.weight", DECONV2X2S2, ch - g, ch, 2, 2));
+    f *= 2;
+    t *= 2;
+    ch -= g;
+    m->dec.push_back(add_stack(m, "decoder_blocks." + std::to_string(i) + ".tfc_tdf", 2 * ch, ch, f, l, bn));
+  }
+  m->final0 = add_conv(m, "final_conv.0.weight", CONV1X1, ch, ch + m->dim_c, 1, 1);
+  m->final2 = add_conv(m, "final_conv.2.weight", CONV1X1, m->ni * m->dim_c, ch, 1, 1);
+  *out = m;
+  return SESA_OK;
+}
+
+extern "C" int sesa_mdx23c_num_params(const sesa_mdx23c* m) { return m ? (int)m->params.size() : 0; }
+
+extern "C" int sesa_mdx23c_param_info(const sesa_mdx23c* m, int i, const char** name, int64_t* numel) {
+  clear_error();
+  SESA_REQUIRE(m && i >= 0 && i < (int)m->params.size(), SESA_ERR_INVALID, "param_info: index out of range");
+  if (name) *name = m->params[i].name.c_str();
+  if (numel) *numel = m->params[i].numel;
+  return SESA_OK;
+}
+
+extern "C" int sesa_mdx23c_set_param(sesa_mdx23c* m, const char* name, const float* host, int64_t numel) {
+  clear_error();
+  SESA_REQUIRE(m && name && host, SESA_ERR_INVALID, "set_param: null argument");
+  auto it = m->by_name.find(name);
+  SESA_REQUIRE(it != m->by_name.end(), SESA_ERR_INVALID, "set_param: unknown parameter '%s'", name);
+  Param& p = m->params[it->second];
+  SESA_REQUIRE(p.numel == numel, SESA_ERR_INVALID, "set_param: '%s' expects %lld elements, got %lld", name,
+               (long long)p.numel, (long long)numel);
+  p.host.assign(host, host + numel);
+  p.set = true;
+  m->finalized = false;
+  return SESA_OK;
+}
+
+extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
+  clear_error();
+  SESA_REQUIRE(m, SESA_ERR_INVALID, "finalize: null model");
+  for (auto& p : m->params)
+    SESA_REQUIRE(p.set, SESA_ERR_STATE, "finalize: parameter '%s' was never set", p.name.c_str());
+  std::vector<uint16_t> blob;
+  std::vector<float> aff;
+  auto pc = [&](ConvW& w) { pack_conv(m->params[w.param], w, blob); };
+  auto pstack = [&](Stack& s) {
+    for (auto& b : s.blocks) {
+      pc(b.conv1);
+      pc(b.conv2);
+      pc(b.shortcut);
+      pack_tdf(m->params[b.lin1.param], b.lin1, blob);
+      pack_tdf(m->params[b.lin2.param], b.lin2, blob);
+      pack_norm(m, b.tfc1, aff);
+      pack_norm(m, b.tdf0, aff);
+      pack_norm(m, b.tdf3, aff);
+      pack_norm(m, b.tfc2, aff);
+    }
+  };
+  pc(m->first_conv);
+  for (size_t i = 0; i < m->enc.size(); ++i) {
+    pstack(m->enc[i]);
+    pc(m->down[i]);
+    pack_norm(m, m->down_norm[i], aff);
+  }
+  pstack(m->bottleneck);
+  for (size_t i = 0; i < m->dec.size(); ++i) {
+    pc(m->up[i]);
+    pack_norm(m, m->up_norm[i], aff);
+    pstack(m->dec[i]);
+  }
+  pc(m->final0);
+  pc(m->final2);
+  if (m->d_w) (void)hipFree(m->d_w);
+  if (m->d_affine) (void)hipFree(m->d_affine);
+  m->d_w = nullptr;
+  m->d_affine = nullptr;
+  SESA_REQUIRE(hipMalloc(&m->d_w, blob.size() * 2) == hipSuccess, SESA_ERR_NOMEM, "finalize: hipMalloc weights");
+  SESA_REQUIRE(hipMalloc(&m->d_affine, aff.size() * 4) == hipSuccess, SESA_ERR_NOMEM, "finalize: hipMalloc affine");
+  SESA_CHECK_HIP(hipMemcpyAsync(m->d_w, blob.data(), blob.size() * 2, hipMemcpyHostToDevice, as_stream(stream)));
+  SESA_CHECK_HIP(hipMemcpyAsync(m->d_affine, aff.data(), aff.size() * 4, hipMemcpyHostToDevice, as_stream(stream)));
+  SESA_CHECK_HIP(hipStreamSynchronize(as_stream(stream)));  // host blobs die at return
+  const float2 *a, *b;
+  const float* w;
+  int rc = get_spectral_tables(&a, &b, &w);
+  if (rc) return rc;
+  m->finalized = true;
+  return SESA_OK;
+}
+
+namespace {
+void plan_sizes(sesa_mdx23c* m, int batch, size_t* float_bytes, size_t* stats_bytes) {
+  Fwd f{m, nullptr, true, batch, m->cfg.precision == SESA_PREC_BF16X3 ? 1 : 0, nullptr};
+  f.run(nullptr, nullptr);
+  *float_bytes = f.off;
+  *stats_bytes = f.stats_off;
+}
+}  // namespace
+
+extern "C" size_t sesa_mdx23c_workspace_size(const sesa_mdx23c* m, int batch) {
+  if (!m || batch <= 0) return 0;
+  size_t fb, sb;
+  plan_sizes(const_cast<sesa_mdx23c*>(m), batch, &fb, &sb);
+  return fb + sb;
+}
+
+extern "C" int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, float* out, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  clear_error();
+  SESA_REQUIRE(m && x && out && workspace && batch > 0, SESA_ERR_INVALID, "forward: bad arguments");
+  SESA_REQUIRE(m->finalized, SESA_ERR_STATE, "forward: call sesa_mdx23c_finalize first");
+  size_t fb, sb;
+  plan_sizes(m, batch, &fb, &sb);
+  SESA_REQUIRE(workspace_bytes >= fb + sb, SESA_ERR_INVALID, "forward: workspace %zu < required %zu",
+               workspace_bytes, fb + sb);
+  hipStream_t st = as_stream(stream);
+  char* ws = reinterpret_cast<char*>(workspace);
+  SESA_CHECK_HIP(hipMemsetAsync(ws + fb, 0, sb, st));  // norm statistics accumulate atomically
+  Fwd f{m, st, false, batch, m->cfg.precision == SESA_PREC_BF16X3 ? 1 : 0, ws};
+  f.stats_base = ws + fb;
+  f.stats_cap = sb;
+  f.run(x, out);
+  return f.rc;
+}
+
+extern "C" int sesa_mdx23c_destroy(sesa_mdx23c* m) {
+  if (!m) return SESA_OK;
+  if (m->d_w) (void)hipFree(m->d_w);
+  if (m->d_affine) (void)hipFree(m->d_affine);
+  delete m;
+  return SESA_OK;
+}

@@ -1,0 +1,477 @@
+// MFMA contraction kernels for the MDX23C TFC-TDF network (gfx950, wave64).
+//
+// Layout: every activation is NHWC fp32 [B][T][F][C] (channels innermost), so both GEMM operands
+// of a convolution are K-contiguous (K = input channel) and MFMA fragments are single 16-byte
+// LDS reads.  Precision: fp32 activations in HBM; operands are split in-register into bf16
+// hi + lo and contracted with 3 MFMA passes (hi*hi + hi*lo + lo*hi, fp32 accumulate) -- the
+// parity mode -- or with one bf16 pass (X3 = false).
+//
+// tap_gemm_kernel -- implicit-GEMM convolution over (T, F) with KHxKW taps and stride S
+//   (nn.Conv2d 3x3 p1 / 1x1, Downscale 2x2 s2, and the ConvTranspose2d 2x2 s2 of Upscale as a
+//   1x1 GEMM with N = 4*C_out and a scattering epilogue), mdx23c_tfc_tdf_v3.py:74-138, 161, 183-187.
+//   Workgroup tile: TM rows x 32 columns of output positions x BN output channels; 4 waves.
+//   Per 16-channel K chunk the halo tile is loaded ONCE from HBM/L2, the consumer's
+//   InstanceNorm-affine + exact GELU (or the x*first_conv_out product) is applied in the
+//   prologue, split to bf16 hi/lo and stored to LDS; all KH*KW taps then read shifted windows.
+//   Epilogue: optional residual add (x + s, :137) and output GELU, fp32 store, and per-channel
+//   sum / sum-of-squares for the NEXT InstanceNorm (double atomics), so no norm kernel and no
+//   extra pass over the activation exists anywhere.
+// tdf_kernel -- the TDF nn.Linear over the frequency axis (:113-120), per (b, t):
+//   out[f', c] = sum_f W[f', f] * act(x)[f, c] (+ residual), same prologue / epilogue fusion.
+//
+// MFMA: v_mfma_f32_32x32x16_bf16.  Lane l holds A[m = l&31][k = 8(l>>5)+j] and
+// B[k = 8(l>>5)+j][n = l&31]; D: column n = l&31, row (r&3) + 8(r>>2) + 4(l>>5).
+// LDS images store 16-byte halves swizzled by (row>>3)&1 (conv) / (row>>2)&3 (TDF) so the
+// ds_read_b128 lane groups are bank-conflict free.
+#include <hip/hip_runtime.h>
+
+#include "sesa_common.hpp"
+#include "sesa_tapgemm.hpp"
+
+namespace sesa {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxCin = 1536;
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t pack2(__bf16 a, __bf16 b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+
+// Per-channel affine (scale, shift) of the consumer's InstanceNorm, from the producer's sums.
+__device__ void build_affine(const GemmIn& in, int b, float* sc, float* sh) {
+  for (int c = threadIdx.x; c < in.C_in; c += kThreads) {
+    const int s = c < in.C_split ? 0 : 1;
+    const Src& src = in.src[s];
+    const int cl = c - (s ? in.C_split : 0);
+    float scale = 1.f, shift = 0.f;
+    if (src.mode == SRC_NORM_GELU) {
+      const double* st = src.stats + ((int64_t)b * src.C + cl) * 2;
+      const double mean = st[0] * in.inv_count;
+      double var = st[1] * in.inv_count - mean * mean;
+      if (var < 0) var = 0;
+      const float rstd = (float)(1.0 / sqrt(var + 1e-5));
+      const float g = in.gamma ? in.gamma[c] : 1.f;
+      const float be = in.beta ? in.beta[c] : 0.f;
+      scale = g * rstd;
+      shift = be - (float)mean * scale;
+    }
+    sc[c] = scale;
+    sh[c] = shift;
+  }
+}
+
+__device__ __forceinline__ void transform4(float (&v)[4], int mode, const float* sc, const float* sh, int c,
+                                           const float* mulp) {
+  if (mode == SRC_NORM_GELU) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = gelu_erf(v[q] * sc[c + q] + sh[c + q]);
+  } else if (mode == SRC_MUL) {
+    const float4 m = *reinterpret_cast<const float4*>(mulp);
+    v[0] *= m.x; v[1] *= m.y; v[2] *= m.z; v[3] *= m.w;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool X3, bool UPS>
+__global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int MI = TM / WM;                 // 32-position MFMA row blocks per wave
+  constexpr int NI = BN / WN / 32;            // 32-channel MFMA column blocks per wave
+  constexpr int HT = (TM - 1) * S + KH;       // halo rows
+  constexpr int HW = (kTF - 1) * S + KW;      // halo cols
+  constexpr int NPOS = HT * HW;
+  constexpr int TAPS = KH * KW;
+  constexpr int A_BYTES = NPOS * 32;          // one (hi or lo) image: 16 bf16 per position
+  constexpr int W_BYTES = TAPS * BN * 32;
+  static_assert(MI >= 1 && NI >= 1, "tile");
+
+  __shared__ __attribute__((aligned(16))) char smem[2 * A_BYTES + 2 * W_BYTES + 2 * kMaxCin * 4];
+  char* A_hi = smem;
+  char* A_lo = smem + A_BYTES;
+  char* W_hi = smem + 2 * A_BYTES;
+  char* W_lo = W_hi + W_BYTES;
+  float* sc = reinterpret_cast<float*>(W_lo + W_BYTES);
+  float* sh = sc + kMaxCin;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int l32 = lane & 31, h = lane >> 5;
+
+  const int tiles_f = a.F_out / kTF;
+  const int t0 = (blockIdx.x / tiles_f) * TM;
+  const int f0 = (blockIdx.x % tiles_f) * kTF;
+  const int nb = blockIdx.y;
+  const int b = blockIdx.z;
+  const int t_in0 = t0 * S - PAD, f_in0 = f0 * S - PAD;
+
+  build_affine(a.in, b, sc, sh);
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const uint16_t* wblk = a.w + (int64_t)nb * a.n_chunks * (2 * W_BYTES / 2);
+
+  for (int kc = 0; kc < a.n_chunks; ++kc) {
+    __syncthreads();  // previous chunk's fragment reads are done (and sc/sh are built)
+    // ---- stage W (pre-packed, pre-swizzled image: straight copy) ----
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(wblk + (int64_t)kc * (2 * W_BYTES / 2));
+      uint4* dst = reinterpret_cast<uint4*>(W_hi);
+      constexpr int N16 = (X3 ? 2 : 1) * W_BYTES / 16;
+      for (int e = tid; e < N16; e += kThreads) dst[e] = src[e];
+    }
+    // ---- stage A: halo x 16 channels, transformed + split ----
+    {
+      const int k0 = kc * kConvBK;
+      const int s = k0 < a.in.C_split ? 0 : 1;
+      const Src& src = a.in.src[s];
+      const int cl0 = k0 - (s ? a.in.C_split : 0);
+      for (int e = tid; e < NPOS * 4; e += kThreads) {
+        const int p = e >> 2, g = e & 3;
+        const int hr = p / HW, hc = p - hr * HW;
+        const int ti = t_in0 + hr, fi = f_in0 + hc;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in) {
+          const int64_t idx = (((int64_t)b * a.T_in + ti) * a.F_in + fi) * src.C + cl0 + 4 * g;
+          const float4 x = *reinterpret_cast<const float4*>(src.ptr + idx);
+          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+          transform4(v, src.mode, sc, sh, k0 + 4 * g, src.mode == SRC_MUL ? src.mul + idx : nullptr);
+        }
+        __bf16 hi[4], lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) split_bf16(v[q], hi[q], lo[q]);
+        const int off = p * 32 + ((((g >> 1) ^ ((p >> 3) & 1))) << 4) + ((g & 1) << 3);
+        *reinterpret_cast<uint2*>(A_hi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
+        if (X3) *reinterpret_cast<uint2*>(A_lo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
+      }
+    }
+    __syncthreads();
+    // ---- MFMA over the taps ----
+#pragma unroll
+    for (int tap = 0; tap < TAPS; ++tap) {
+      const int dy = tap / KW, dx = tap % KW;
+      bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * MI + i;
+        const int p = (row * S + dy) * HW + l32 * S + dx;
+        const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+        ah[i] = *reinterpret_cast<const bf16x8*>(A_hi + off);
+        if (X3) al[i] = *reinterpret_cast<const bf16x8*>(A_lo + off);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int p = tap * BN + (wn * NI + j) * 32 + l32;
+        const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+        bh[j] = *reinterpret_cast<const bf16x8*>(W_hi + off);
+        if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(W_lo + off);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          if (X3) {
+            acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
+            acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
+          }
+          acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+        }
+    }
+  }
+
+  // ---- epilogue ----
+  float ssum[NI], ssq[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
+  const int C_out = a.out.C_out;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int ncol = nb * BN + (wn * NI + j) * 32 + l32;  // GEMM column
+    int co = ncol, dy = 0, dx = 0;
+    if (UPS) {
+      const int tap = ncol / C_out;
+      co = ncol - tap * C_out;
+      dy = tap >> 1;
+      dx = tap & 1;
+    }
+    const bool col_ok = UPS ? (ncol < a.n_cols) : (co < C_out);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int t = t0 + wm * MI + i;
+      if (t >= a.T_out || !col_ok) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = f0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        int64_t idx;
+        if (UPS) {
+          const int T2 = a.T_out * 2, F2 = a.F_out * 2;
+          idx = (((int64_t)b * T2 + 2 * t + dy) * F2 + 2 * f + dx) * C_out + co;
+        } else {
+          idx = (((int64_t)b * a.T_out + t) * a.F_out + f) * C_out + co;
+        }
+        float v = acc[i][j][r];
+        if (a.out.residual) v += a.out.residual[idx];
+        if (a.out.gelu) v = gelu_erf(v);
+        a.out.ptr[idx] = v;
+        ssum[j] += v;
+        ssq[j] += v * v;
+      }
+    }
+  }
+  if (a.out.stats) {
+    // reduce over the two lane halves, then over the WM waves sharing these columns (LDS)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      ssum[j] += __shfl_xor(ssum[j], 32);
+      ssq[j] += __shfl_xor(ssq[j], 32);
+      if (h == 0) {
+        const int n = (wn * NI + j) * 32 + l32;
+        red[(wm * BN + n) * 2 + 0] = ssum[j];
+        red[(wm * BN + n) * 2 + 1] = ssq[j];
+      }
+    }
+    __syncthreads();
+    for (int n = tid; n < BN; n += kThreads) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s0 += red[(w * BN + n) * 2 + 0];
+        s1 += red[(w * BN + n) * 2 + 1];
+      }
+      const int ncol = nb * BN + n;
+      const int co = UPS ? ncol % C_out : ncol;
+      if ((UPS ? ncol < a.n_cols : co < C_out)) {
+        double* st = a.out.stats + ((int64_t)b * C_out + co) * 2;
+        atomicAdd(st + 0, (double)s0);
+        atomicAdd(st + 1, (double)s1);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// TDF linear: per (b, t), D[m = f_out][n = c] = sum_k W[m][k] * act(x[b][t][k][c]).
+template <int BN, bool X3>
+__global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
+  constexpr int BM = kTdfBM;
+  constexpr int WM = 2, WN = 2;
+  constexpr int MI = BM / WM / 32, NI = BN / WN / 32;
+  constexpr int ROWB = kTdfBK * 2;            // 64 B per image row (32 bf16)
+  constexpr int AW_BYTES = BM * ROWB;
+  constexpr int B_BYTES = BN * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * AW_BYTES + 2 * B_BYTES + 2 * kMaxCin * 4];
+  char* Whi = smem;
+  char* Wlo = smem + AW_BYTES;
+  char* Bhi = smem + 2 * AW_BYTES;
+  char* Blo = Bhi + B_BYTES;
+  float* sc = reinterpret_cast<float*>(Blo + B_BYTES);
+  float* sh = sc + kMaxCin;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int mb = blockIdx.x, c0 = blockIdx.y * BN;
+  const int bt = blockIdx.z;
+  const int b = bt / a.T, t = bt - b * a.T;
+  const int C = a.in.src[0].C;  // TDF input is a single source
+  const Src& src = a.in.src[0];
+
+  build_affine(a.in, b, sc, sh);
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const float* xrow = src.ptr + ((int64_t)b * a.T + t) * a.K * C;
+  const uint16_t* wblk = a.w + (int64_t)mb * a.n_chunks * (2 * AW_BYTES / 2);
+
+  for (int kc = 0; kc < a.n_chunks; ++kc) {
+    __syncthreads();
+    {
+      const uint4* s4 = reinterpret_cast<const uint4*>(wblk + (int64_t)kc * (2 * AW_BYTES / 2));
+      uint4* d4 = reinterpret_cast<uint4*>(Whi);
+      constexpr int N16 = (X3 ? 2 : 1) * AW_BYTES / 16;
+      for (int e = tid; e < N16; e += kThreads) d4[e] = s4[e];
+    }
+    {
+      const int k0 = kc * kTdfBK;
+      for (int e = tid; e < BN * 4; e += kThreads) {
+        const int n = e % BN, g = e / BN;  // lanes walk channels: 256 B coalesced per k
+        const int c = c0 + n;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = k0 + 8 * g + j;
+          float x = 0.f;
+          if (c < C && k < a.K) {
+            x = xrow[(int64_t)k * C + c];
+            if (src.mode == SRC_NORM_GELU) x = gelu_erf(x * sc[c] + sh[c]);
+          }
+          v[j] = x;
+        }
+        __bf16 hi[8], lo[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) split_bf16(v[j], hi[j], lo[j]);
+        const int off = n * ROWB + ((g ^ ((n >> 2) & 3)) << 4);
+        *reinterpret_cast<uint4*>(Bhi + off) =
+            make_uint4(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]), pack2(hi[4], hi[5]), pack2(hi[6], hi[7]));
+        if (X3)
+          *reinterpret_cast<uint4*>(Blo + off) =
+              make_uint4(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]), pack2(lo[4], lo[5]), pack2(lo[6], lo[7]));
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
+      const int q = ks * 2 + h;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = (wm * MI + i) * 32 + l32;
+        const int off = row * ROWB + ((q ^ ((row >> 2) & 3)) << 4);
+        ah[i] = *reinterpret_cast<const bf16x8*>(Whi + off);
+        if (X3) al[i] = *reinterpret_cast<const bf16x8*>(Wlo + off);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int n = (wn * NI + j) * 32 + l32;
+        const int off = n * ROWB + ((q ^ ((n >> 2) & 3)) << 4);
+        bh[j] = *reinterpret_cast<const bf16x8*>(Bhi + off);
+        if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(Blo + off);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          if (X3) {
+            acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
+            acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
+          }
+          acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+        }
+    }
+  }
+
+  float ssum[NI], ssq[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
+  const int Cout = a.out.C_out;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int c = c0 + (wn * NI + j) * 32 + l32;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb * BM + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= a.M || c >= Cout) continue;
+        const int64_t idx = (((int64_t)b * a.T + t) * a.M + m) * Cout + c;
+        float v = acc[i][j][r];
+        if (a.out.residual) v += a.out.residual[idx];
+        a.out.ptr[idx] = v;
+        ssum[j] += v;
+        ssq[j] += v * v;
+      }
+    }
+  }
+  if (a.out.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      ssum[j] += __shfl_xor(ssum[j], 32);
+      ssq[j] += __shfl_xor(ssq[j], 32);
+      if (h == 0) {
+        const int n = (wn * NI + j) * 32 + l32;
+        red[(wm * BN + n) * 2 + 0] = ssum[j];
+        red[(wm * BN + n) * 2 + 1] = ssq[j];
+      }
+    }
+    __syncthreads();
+    for (int n = tid; n < BN; n += kThreads) {
+      const int c = c0 + n;
+      if (c >= Cout) continue;
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s0 += red[(w * BN + n) * 2 + 0];
+        s1 += red[(w * BN + n) * 2 + 1];
+      }
+      double* st = a.out.stats + ((int64_t)b * Cout + c) * 2;
+      atomicAdd(st + 0, (double)s0);
+      atomicAdd(st + 1, (double)s1);
+    }
+  }
+}
+
+template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool UPS>
+int launch_conv_t(int x3, const ConvArgs& a, int batch, hipStream_t st) {
+  dim3 grid((unsigned)(((a.T_out + TM - 1) / TM) * (a.F_out / kTF)), (unsigned)((a.n_cols + BN - 1) / BN),
+            (unsigned)batch);
+  if (x3)
+    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, true, UPS>), grid, dim3(kThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, false, UPS>), grid, dim3(kThreads), 0, st, a);
+  SESA_CHECK_LAUNCH();
+  return SESA_OK;
+}
+
+}  // namespace
+
+// Tile choices per kind (BN = 64 unless the GEMM N is <= 32).
+int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStream_t st) {
+  SESA_REQUIRE(a.F_out % kTF == 0, SESA_ERR_INVALID, "conv: F_out %d not a multiple of %d", a.F_out, kTF);
+  SESA_REQUIRE(a.in.C_in % kConvBK == 0 && a.in.C_split % kConvBK == 0 && a.in.C_in <= kMaxCin, SESA_ERR_INVALID,
+               "conv: C_in %d / split %d must be multiples of %d (<= %d)", a.in.C_in, a.in.C_split, kConvBK,
+               kMaxCin);
+  switch (kind) {
+    case CONV3X3:
+      return launch_conv_t<3, 3, 1, 1, 8, 64, 4, false>(x3, a, batch, st);
+    case CONV1X1:
+      if (bn == 32) return launch_conv_t<1, 1, 1, 0, 8, 32, 4, false>(x3, a, batch, st);
+      return launch_conv_t<1, 1, 1, 0, 8, 64, 4, false>(x3, a, batch, st);
+    case CONV2X2S2:
+      return launch_conv_t<2, 2, 2, 0, 4, 64, 4, false>(x3, a, batch, st);
+    case DECONV2X2S2:
+      return launch_conv_t<1, 1, 1, 0, 8, 64, 4, true>(x3, a, batch, st);
+  }
+  set_error("conv: unknown kind %d", kind);
+  return SESA_ERR_INVALID;
+}
+
+int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st) {
+  SESA_REQUIRE(a.in.C_in <= kMaxCin, SESA_ERR_INVALID, "tdf: C %d > %d", a.in.C_in, kMaxCin);
+  const int C = a.out.C_out;
+  const int bn = C <= 64 ? 64 : 128;
+  dim3 grid((unsigned)((a.M + kTdfBM - 1) / kTdfBM), (unsigned)((C + bn - 1) / bn), (unsigned)(batch * a.T));
+  if (bn == 64) {
+    if (x3) hipLaunchKernelGGL((tdf_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((tdf_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
+  } else {
+    if (x3) hipLaunchKernelGGL((tdf_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((tdf_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
+  }
+  SESA_CHECK_LAUNCH();
+  return SESA_OK;
+}
+
+}  // namespace sesa

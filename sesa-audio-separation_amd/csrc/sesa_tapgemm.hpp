@@ -1,0 +1,71 @@
+// Argument blocks for the MFMA contraction kernels of the MDX23C network (see sesa_tapgemm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace sesa {
+
+enum SrcMode : int {
+  SRC_RAW = 0,        // x
+  SRC_NORM_GELU = 1,  // GELU(InstanceNorm_affine(x))   (get_norm + get_act, mdx23c_tfc_tdf_v3.py:47-71)
+  SRC_MUL = 2,        // x * mul                         (x * first_conv_out, :230)
+};
+
+// One input source of a (possibly channel-concatenated) NHWC fp32 activation
+// [B][T][F][C] -- torch.cat([a, b], 1) is expressed as two sources (:225, :232).
+struct Src {
+  const float* ptr;
+  const double* stats;  // [B][C][2] (sum, sumsq) over T*F, for SRC_NORM_GELU
+  const float* mul;     // same layout as ptr, for SRC_MUL
+  int C;
+  int mode;
+};
+
+struct GemmIn {
+  Src src[2];
+  int C_split;          // channels [0, C_split) from src[0], the rest from src[1]
+  int C_in;
+  const float* gamma;   // InstanceNorm affine over the concatenated channels (nullable)
+  const float* beta;
+  double inv_count;     // 1 / (T_in * F_in)
+};
+
+struct GemmOut {
+  float* ptr;                // NHWC [B][T_out][F_out][C_out]
+  const float* residual;     // nullable, same layout (may alias ptr)
+  double* stats;             // nullable, [B][C_out][2] accumulated with atomics
+  int C_out;
+  int gelu;                  // apply exact GELU to the stored value (final_conv[1], :185)
+};
+
+struct ConvArgs {
+  GemmIn in;
+  GemmOut out;
+  const uint16_t* w;         // packed bf16 hi/lo weight image (host packing in sesa_mdx23c.hip)
+  int T_in, F_in, T_out, F_out;
+  int n_cols;                // GEMM N (C_out, or 4*C_out for the transposed 2x2 conv)
+  int n_chunks;              // C_in / 16
+};
+
+struct TdfArgs {
+  GemmIn in;
+  GemmOut out;
+  const uint16_t* w;         // packed [M/BM][K/32][BM][32] hi, lo
+  int T, K, M;               // F_in = K, F_out = M
+  int n_chunks;              // ceil(K / 32)
+};
+
+// conv kinds
+enum ConvKind : int { CONV3X3 = 0, CONV1X1 = 1, CONV2X2S2 = 2, DECONV2X2S2 = 3 };
+
+int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStream_t st);
+int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st);
+
+// Tile geometry shared by the host packer and the kernels.
+constexpr int kTF = 32;       // output columns per tile (one MFMA 32-row block = one tile row)
+constexpr int kConvBK = 16;   // input channels per K chunk of the tap GEMM
+constexpr int kTdfBM = 128;   // TDF output rows (frequency) per tile
+constexpr int kTdfBN = 128;   // TDF output channels per tile
+constexpr int kTdfBK = 32;    // TDF K (frequency) per chunk
+
+}  // namespace sesa

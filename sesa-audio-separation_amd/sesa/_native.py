@@ -1,0 +1,78 @@
+"""ctypes binding of libsesa (include/sesa.h).  The product path has NO fallback: if the HIP
+library is missing or no HIP device is usable, importing/using these entry points raises."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SESA_LIB", os.path.join(_HERE, "_native", "libsesa.so"))
+
+c_int, c_int64, c_size_t, c_void_p, c_char_p = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
+P_f32 = ctypes.c_void_p
+P_i64 = ctypes.POINTER(ctypes.c_int64)
+
+SESA_PREC_BF16X3 = 0
+SESA_PREC_BF16 = 1
+
+
+class SesaMdx23cConfig(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "chunk_size", "dim_f", "dim_t", "hop_length", "n_fft", "audio_channels",
+        "num_subbands", "num_scales", "num_blocks_per_scale", "num_channels",
+        "growth", "bottleneck_factor", "scale_t", "scale_f", "num_instruments", "precision")]
+
+
+# name -> (restype, argtypes); every symbol declared in include/sesa.h
+SIGNATURES = {
+    "sesa_version": (c_int, []),
+    "sesa_last_error": (c_char_p, []),
+    "sesa_stft_f32": (c_int, [P_f32, c_int, c_int, c_int, c_int, c_int, P_f32, c_void_p]),
+    "sesa_istft_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "sesa_istft_f32": (c_int, [P_f32, c_int, c_int, c_int, c_int, c_int, P_f32, c_void_p, c_void_p]),
+    "sesa_chunk_gather_f32": (c_int, [P_f32, c_int, c_int64, c_int64, P_i64, c_int, c_int, P_f32, c_void_p]),
+    "sesa_ola_accumulate_f32": (c_int, [P_f32, c_int, c_int, c_int, P_i64, P_i64, P_f32, P_f32, P_f32, c_int64,
+                                        c_void_p]),
+    "sesa_ola_finalize_f32": (c_int, [P_f32, P_f32, c_int, c_int64, c_int64, P_f32, c_void_p]),
+    "sesa_mdx23c_create": (c_int, [ctypes.POINTER(SesaMdx23cConfig), ctypes.POINTER(c_void_p)]),
+    "sesa_mdx23c_num_params": (c_int, [c_void_p]),
+    "sesa_mdx23c_param_info": (c_int, [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64)]),
+    "sesa_mdx23c_set_param": (c_int, [c_void_p, c_char_p, P_f32, c_int64]),
+    "sesa_mdx23c_finalize": (c_int, [c_void_p, c_void_p]),
+    "sesa_mdx23c_workspace_size": (c_size_t, [c_void_p, c_int]),
+    "sesa_mdx23c_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
+    "sesa_mdx23c_destroy": (c_int, [c_void_p]),
+}
+
+
+class SesaError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libsesa.so (once).  Raises ImportError if the HIP library was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libsesa not built: {LIB_PATH} missing (run __graft_entry__.build() or "
+                              f"`make -C sesa-audio-separation_amd/csrc`)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().sesa_last_error()
+        raise SesaError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc
+
+
+def i64_array(values):
+    arr = (ctypes.c_int64 * len(values))(*[int(v) for v in values])
+    return arr

@@ -1,0 +1,65 @@
+"""Inference backend: drop-in for ``pytorch_backend.py`` (PyTorchBackend :19-332,
+create_inference_session :492-536).
+
+The reference backend wraps an nn.Module with device flags, fp16 autocast and torch.compile /
+jit / channels_last modes.  Here the model is a native libsesa network; the optimisation modes
+are accepted for CLI compatibility and map onto what exists on MI355X:
+
+* ``enable_amp``  -> throughput precision (single-pass bf16 MFMA) instead of the default
+  3-pass bf16x3 parity precision.  (The reference's AMP is fp16 autocast, :308-311.)
+* ``optimize_mode`` ('channels_last' | 'compile' | 'jit' | 'default') -> no effect: the native
+  forward already runs channels-last with fused prologues/epilogues, and there is no tracing
+  compiler in the path.
+* ``enable_tf32`` / ``enable_cudnn_benchmark`` -> no effect (no TF32 on gfx950, no cuDNN).
+
+Unlike the reference there is NO CPU fallback: a device that is not a HIP GPU is an error.
+"""
+import torch
+
+from ._native import SesaError
+
+
+class HipBackend:
+    """PyTorchBackend-compatible callable: ``backend(x[B,2,C]) -> model(x)``."""
+
+    def __init__(self, device="cuda:0", optimize_mode="channels_last", exec_batch=8):
+        if isinstance(device, torch.device):
+            device = str(device)
+        if not str(device).startswith("cuda"):
+            raise SesaError(f"HipBackend: device {device!r} is not a HIP device; the MI355X path has no CPU fallback")
+        if not torch.cuda.is_available():
+            raise SesaError("HipBackend: no HIP device visible")
+        self.device = device
+        self.optimize_mode = optimize_mode
+        self.model = None
+        self.compiled_model = None
+        self.use_amp = False
+        self.exec_batch = exec_batch
+
+    def optimize_model(self, model, example_input=None, use_amp=False, use_channels_last=True):
+        self.model = model.eval()
+        self.use_amp = bool(use_amp)
+        if hasattr(model, "set_precision"):
+            model.set_precision("bf16" if self.use_amp else "bf16x3")
+        self.compiled_model = self.model
+        return self.compiled_model
+
+    def __call__(self, x):
+        if self.compiled_model is None:
+            raise RuntimeError("No model has been optimized yet")
+        if not x.is_cuda:
+            x = x.to(self.device)
+        with torch.no_grad():
+            return self.compiled_model(x)
+
+
+PyTorchBackend = HipBackend
+
+
+def create_inference_session(model, device="cuda:0", optimize_mode="default", enable_amp=False, enable_tf32=True,
+                             enable_cudnn_benchmark=True, exec_batch=8):
+    """pytorch_backend.create_inference_session (:492-536).  NOTE: the default of ``enable_amp``
+    is False here (parity precision); the reference CLI also passes False unless --enable_amp."""
+    be = HipBackend(device=device, optimize_mode=optimize_mode, exec_batch=exec_batch)
+    be.optimize_model(model, use_amp=enable_amp)
+    return be

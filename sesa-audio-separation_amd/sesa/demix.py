@@ -1,0 +1,142 @@
+"""Device-resident chunker + windowed overlap-add.
+
+Drop-in for ``inference_pytorch.demix_pytorch_optimized`` (/root/reference/inference_pytorch.py:55-186)
+and the generic mode of ``utils.demix`` (utils.py:330-477).  Same parameters, same return value
+(``{instrument: np.ndarray[2, L] f32}``), same ``[SESA_PROGRESS]N`` stdout lines, same window and
+counter quirks -- but the mix is uploaded once, chunks are gathered on the device, the model runs
+``exec_batch`` chunks per launch, and result/counter accumulate in HBM; the only D2H copy is the
+final stems.
+
+The *logical* batch (``config.inference.batch_size``) still decides the window fix-ups exactly as
+in the reference (:145-155); the *execution* batch is independent of it (InstanceNorm is
+per-instance, so grouping chunks differently does not change any chunk's output).
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+from .config import prefer_target_instrument
+
+
+def windowing_array(chunk_size, fade_size):
+    """utils._getWindowingArray (utils.py:295-327): torch.linspace fades, float32."""
+    w = torch.ones(chunk_size)
+    w[-fade_size:] = torch.linspace(1, 0, fade_size)
+    w[:fade_size] = torch.linspace(0, 1, fade_size)
+    return w
+
+
+def chunk_plan(L, chunk_size, num_overlap, batch_size):
+    """Loop control of inference_pytorch.py:115-163.  Returns (padded, border, L_pad, batches,
+    progress) with batches = [(chunks[(start, seg_len)], no_fade_in, no_fade_out)] and progress =
+    the list of (chunk_index_after_which_printed, percent) lines the reference prints."""
+    step = chunk_size // num_overlap
+    border = chunk_size - step
+    padded = L > 2 * border and border > 0
+    L_pad = L + 2 * border if padded else L
+    batches, cur, progress = [], [], []
+    i, last, idx = 0, -1, 0
+    while i < L_pad:
+        seg = min(chunk_size, L_pad - i)
+        cur.append((i, seg))
+        i += step
+        if len(cur) >= batch_size or i >= L_pad:
+            no_in = i - step == 0
+            batches.append((list(cur), no_in, (not no_in) and i >= L_pad))
+            cur = []
+        pct = int((i / L_pad) * 100)
+        if pct > last:
+            last = pct
+            progress.append((idx, pct))
+        idx += 1
+    return padded, border, L_pad, batches, progress
+
+
+class _Windows:
+    def __init__(self, chunk_size, device):
+        fade = chunk_size // 10
+        base = windowing_array(chunk_size, fade)
+        w_in = base.clone()
+        w_in[:fade] = 1
+        w_out = base.clone()
+        w_out[-fade:] = 1
+        self.normal = base.to(device)
+        self.no_in = w_in.to(device)
+        self.no_out = w_out.to(device)
+
+    def pick(self, no_in, no_out):
+        return self.no_in if no_in else (self.no_out if no_out else self.normal)
+
+
+def demix_device(config, model, mix, device, exec_batch=None, progress=True, chunk_range=None,
+                 instruments=None):
+    """Core device loop.  ``mix`` is a host array [2, L] or a device tensor.  Returns the
+    device tensor est [n_instr, 2, L] (after nan_to_num and border crop).
+
+    ``chunk_range`` = (first, last) restricts the work to a contiguous range of global chunk
+    indices (multi-GPU chunk sharding, sesa/parallel.py); the caller then receives the raw
+    (result, counter, plan) partial sums instead of the finalized estimate.
+    """
+    C = int(config.audio.chunk_size)
+    ov = int(config.inference.num_overlap)
+    bs = int(config.inference.batch_size)
+    if instruments is None:
+        instruments = prefer_target_instrument(config)
+    ni = len(instruments)
+    if isinstance(mix, torch.Tensor):
+        mix_d = mix.to(device=device, dtype=torch.float32).contiguous()
+    else:
+        mix_d = torch.from_numpy(np.ascontiguousarray(mix, dtype=np.float32)).to(device, non_blocking=False)
+    n_ch, L = mix_d.shape
+    padded, border, L_pad, batches, prog = chunk_plan(L, C, ov, bs)
+    E = exec_batch or getattr(model, "exec_batch", None) or 8
+    win = _Windows(C, device)
+    result = torch.zeros(ni * n_ch, L_pad, device=device, dtype=torch.float32)
+    counter = torch.zeros(L_pad, device=device, dtype=torch.float32)
+    # flatten chunks with their logical-batch window
+    flat = []
+    for chunks, no_in, no_out in batches:
+        for (s, n) in chunks:
+            flat.append((s, n, no_in, no_out))
+    lo, hi = (0, len(flat)) if chunk_range is None else chunk_range
+    prog_at = dict(prog)
+    xbuf = None
+    pos = lo
+    while pos < hi:
+        group = flat[pos:min(hi, pos + E)]
+        starts = [g[0] for g in group]
+        if xbuf is None or xbuf.shape[0] != len(group):
+            xbuf = torch.empty(len(group), n_ch, C, device=device, dtype=torch.float32)
+        ops.chunk_gather(mix_d, border if padded else 0, starts, C, out=xbuf)
+        y = model(xbuf)
+        y = y.reshape(len(group), ni * n_ch, C)
+        # OLA per run of equal windows (== per logical batch), in chunk order
+        j = 0
+        while j < len(group):
+            k = j
+            while k < len(group) and group[k][2:] == group[j][2:]:
+                k += 1
+            w = win.pick(*group[j][2:])
+            ops.ola_accumulate(y[j:k], [g[0] for g in group[j:k]], [g[1] for g in group[j:k]], w, result, counter)
+            j = k
+        if progress:
+            for ci in range(pos, pos + len(group)):
+                if ci in prog_at:
+                    print(f"[SESA_PROGRESS]{prog_at[ci]}", flush=True)
+        pos += len(group)
+    if chunk_range is not None:
+        return result, counter, (padded, border, L_pad)
+    est = ops.ola_finalize(result, counter, border if padded else 0)
+    return est.reshape(ni, n_ch, L)
+
+
+def demix_pytorch_optimized(config, backend, mix, device, pbar=False):
+    """inference_pytorch.demix_pytorch_optimized (:55-186): same signature and return value."""
+    dev = torch.device(device) if not isinstance(device, torch.device) else device
+    instruments = prefer_target_instrument(config)
+    est = demix_device(config, backend, mix, dev, progress=True)
+    print("[SESA_PROGRESS]100", flush=True)
+    est = est.cpu().numpy()
+    return {k: v for k, v in zip(instruments, est)}

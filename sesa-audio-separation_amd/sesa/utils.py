@@ -1,0 +1,94 @@
+"""Reference ``utils.py`` surface on the MI355X path.
+
+* ``load_config`` / ``get_model_from_config`` -- utils.py:26-161 (same model_type strings; the
+  types without a native implementation raise NotImplementedError naming what exists).
+* ``normalize_audio`` / ``denormalize_audio`` -- utils.py:199-238.
+* ``demix`` -- utils.py:330-477 (generic mode on the device loop of sesa/demix.py).
+* ``apply_tta`` -- utils.py:241-292.
+* ``prefer_target_instrument`` -- utils.py:480-499.
+* ``load_start_checkpoint`` -- utils.py:585-613 / inference_pytorch.py:326-369 (safe loader).
+"""
+import numpy as np
+import torch
+
+from .config import ConfigDict, load_config, prefer_target_instrument  # noqa: F401
+from .demix import demix_device, windowing_array as _getWindowingArray  # noqa: F401
+
+# model_type strings accepted by the reference registry (utils.py:89-157)
+REFERENCE_MODEL_TYPES = (
+    "mdx23c", "htdemucs", "segm_models", "torchseg", "mel_band_roformer", "bs_roformer", "swin_upernet", "bandit",
+    "bandit_v2", "scnet_unofficial", "scnet", "apollo", "bs_mamba2", "experimental_mdx23c_stht",
+    "mel_band_roformer_experimental", "bs_roformer_experimental", "bs_roformer_custom", "scnet_tran", "scnet_masked",
+    "conformer", "mel_band_conformer")
+NATIVE_MODEL_TYPES = ("mdx23c",)
+
+
+def get_model_from_config(model_type: str, config_path: str):
+    """utils.get_model_from_config: model_type string -> (model, config)."""
+    config = load_config(model_type, config_path)
+    if model_type == "mdx23c":
+        from .models.mdx23c import TFC_TDF_net
+        model = TFC_TDF_net(config)
+    elif model_type in REFERENCE_MODEL_TYPES:
+        raise NotImplementedError(f"model_type '{model_type}' has no MI355X-native implementation yet "
+                                  f"(native: {', '.join(NATIVE_MODEL_TYPES)})")
+    else:
+        raise ValueError(f"Unknown model type: {model_type}")
+    return model, config
+
+
+def normalize_audio(audio: np.ndarray):
+    mono = audio.mean(0)
+    mean, std = mono.mean(), mono.std()
+    return (audio - mean) / std, {"mean": mean, "std": std}
+
+
+def denormalize_audio(audio: np.ndarray, norm_params):
+    return audio * norm_params["std"] + norm_params["mean"]
+
+
+def _as_backend(model, device):
+    if hasattr(model, "compiled_model"):
+        return model
+    from .backend import create_inference_session
+    return create_inference_session(model, device=str(device))
+
+
+def demix(config, model, mix, device, model_type: str = "generic", pbar: bool = False):
+    """utils.demix generic mode.  (The 'htdemucs' demucs mode has no native model yet.)"""
+    if model_type == "htdemucs":
+        raise NotImplementedError("demucs-mode demix needs the htdemucs model, not implemented natively yet")
+    dev = torch.device(device) if not isinstance(device, torch.device) else device
+    est = demix_device(config, _as_backend(model, dev), mix, dev, progress=False).cpu().numpy()
+    return {k: v for k, v in zip(prefer_target_instrument(config), est)}
+
+
+def apply_tta(config, model, mix, waveforms_orig, device, model_type):
+    """utils.apply_tta (:241-292): channel swap + polarity flip, averaged with the original."""
+    track_proc_list = [mix[::-1].copy(), -1.0 * mix.copy()]
+    for i, augmented_mix in enumerate(track_proc_list):
+        waveforms = demix(config, model, augmented_mix, device, model_type=model_type)
+        for el in waveforms:
+            if i == 0:
+                waveforms_orig[el] += waveforms[el][::-1].copy()
+            else:
+                waveforms_orig[el] -= waveforms[el]
+    for el in waveforms_orig:
+        waveforms_orig[el] /= len(track_proc_list) + 1
+    return waveforms_orig
+
+
+def load_checkpoint_state(path, map_location="cpu"):
+    """Checkpoint -> state_dict (inference_pytorch.py:326-366), with the SAFE loader only
+    (weights_only=True): checkpoints that need arbitrary unpickling are refused."""
+    ckpt = torch.load(path, map_location=map_location, weights_only=True)
+    if isinstance(ckpt, dict):
+        for key in ("state_dict", "model", "state"):
+            if key in ckpt:
+                return ckpt[key]
+    return ckpt
+
+
+def load_start_checkpoint(args, model, type_="inference"):
+    """utils.load_start_checkpoint (strict load)."""
+    model.load_state_dict(load_checkpoint_state(args.start_check_point), strict=True)

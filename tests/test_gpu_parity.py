@@ -1,0 +1,164 @@
+"""Parity of the HIP path (through the libsesa C ABI) against the reference's golden vectors and
+the CPU oracle.  Needs a real MI355X: every test is marked ``gpu``.
+
+Tolerances (written per test):
+* integer/byte-like work (chunk gather, OLA accumulate/finalize given identical model output):
+  bit-exact against the oracle restatement.
+* STFT/iSTFT: fp32 FFT rounding, max |err| <= 2e-6 * max|X| (STFT) / 1e-6 abs (iSTFT).
+* network / stems: per-sample RMS <= 1e-4 (north_star gate) in the default bf16x3 precision.
+"""
+import contextlib
+import glob
+import io
+import os
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from conftest import CONFIGS, GOLDEN, rms
+
+pytestmark = pytest.mark.gpu
+
+RMS_GATE = 1e-4
+
+
+def _cfg(name):
+    from sesa.config import load_config
+    return load_config("mdx23c", os.path.join(CONFIGS, name))
+
+
+def _raw_cfg(name):
+    with open(os.path.join(CONFIGS, name)) as f:
+        return yaml.safe_load(f)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+def _model(cfg_name, affine, precision="bf16x3"):
+    from sesa.utils import get_model_from_config
+    from sesa.weights import synth_state_dict
+    m, c = get_model_from_config("mdx23c", os.path.join(CONFIGS, cfg_name))
+    m.load_state_dict(synth_state_dict(m, affine=affine), strict=True)
+    m.set_precision(precision)
+    return m, c
+
+
+def test_native_library_loaded():
+    from sesa import _native
+    assert _native.lib().sesa_version() >= 100
+
+
+def test_stft_matches_reference(golden, dev):
+    from sesa import ops
+    g = golden("stft_istft.npz")
+    x = torch.from_numpy(g["x"]).to(dev)                         # [1,2,16384]
+    X = ops.stft(x, 8192, 1024, 4096)                             # [1,2,2,4096,17]
+    X = X.reshape(1, 4, 4096, 17).cpu().numpy()
+    ref = g["X"]
+    assert np.abs(X - ref).max() <= 2e-6 * np.abs(ref).max()
+
+
+def test_istft_matches_reference(golden, dev):
+    from sesa import ops
+    g = golden("stft_istft.npz")
+    spec = torch.from_numpy(g["spec"]).to(dev).reshape(1, 2, 2, 2, 4096, 17)
+    y = ops.istft(spec, 8192, 1024).reshape(g["y"].shape).cpu().numpy()
+    assert np.abs(y - g["y"]).max() <= 1e-6
+
+
+@pytest.mark.parametrize("L,border", [(40000, 0), (110250, 48384), (20000, 0)])
+def test_chunk_gather_bit_exact(dev, L, border):
+    from oracle import demix as od
+    from sesa import ops
+    rng = np.random.default_rng(5)
+    mix = rng.standard_normal((2, L)).astype(np.float32)
+    C, step = 64512, 16128
+    L_pad = L + 2 * border
+    mix_pad = np.pad(mix, ((0, 0), (border, border)), mode="reflect") if border else mix
+    starts = list(range(0, L_pad, step))
+    out = ops.chunk_gather(torch.from_numpy(mix).to(dev), border, starts, C).cpu().numpy()
+    for j, s in enumerate(starts):
+        np.testing.assert_array_equal(out[j], od.extract_chunk(mix_pad, s, C))
+
+
+class _StandIn:
+    """Deterministic stand-in model y = [x, -0.5x] (SURVEY §4 known-answer test)."""
+
+    def __call__(self, x):
+        return torch.stack([x, -0.5 * x], 1)
+
+
+@pytest.mark.parametrize("L,bs", [(40000, 1), (40000, 2), (110250, 1), (110250, 3), (20000, 1), (300000, 2)])
+def test_ola_bit_exact_vs_oracle(dev, L, bs):
+    from oracle import demix as od
+    from sesa.demix import demix_device
+    c = _cfg("config_mdx23c_small.yaml")
+    c.inference.batch_size = bs
+    rng = np.random.default_rng(9)
+    mix = (0.1 * rng.standard_normal((2, L))).astype(np.float32)
+    with contextlib.redirect_stdout(io.StringIO()):
+        est = demix_device(c, _StandIn(), mix, dev, exec_batch=3).cpu().numpy()
+    ref = od.demix(c, lambda x: _StandIn()(x), mix, batch_size=bs)
+    np.testing.assert_array_equal(est[0], ref["vocals"])
+    np.testing.assert_array_equal(est[1], ref["other"])
+
+
+@pytest.mark.parametrize("fixture,cfg_name", [("mdx23c_small.npz", "config_mdx23c_small.yaml"),
+                                              ("mdx23c_small_vocals.npz", "config_mdx23c_small_vocals.yaml")])
+def test_forward_small_matches_reference(golden, dev, fixture, cfg_name):
+    g = golden(fixture)
+    m, _ = _model(cfg_name, str(g["affine"]))
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    assert y.shape == g["y"].shape
+    err = rms(y, g["y"])
+    print(f"{fixture}: rms={err:.3e} ref_rms={rms(g['y'], 0 * g['y']):.3e}")
+    assert err <= RMS_GATE
+
+
+def test_forward_full_chunk_matches_reference(golden, dev):
+    """The benchmark configuration (MDX23C vocals, 261120-sample chunk), bf16x3 precision."""
+    g = golden("mdx23c_full_chunk.npz")
+    m, _ = _model("config_vocals_mdx23c.yaml", "unit")
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"full chunk bf16x3: rms={err:.3e} max={np.abs(y - g['y']).max():.3e}")
+    assert err <= RMS_GATE
+    # batch invariance: the same chunk inside a batch of 3 gives the same output
+    xb = torch.from_numpy(np.concatenate([g["x"], 0.5 * g["x"], g["x"]])).to(dev)
+    yb = m(xb).cpu().numpy()
+    assert rms(yb[0], y[0]) < 1e-7 and rms(yb[2], y[0]) < 1e-7
+
+
+def test_forward_full_chunk_bf16_reports_deviation(golden, dev):
+    """Throughput precision: measured, not gated (expected ~6e-4, outside the 1e-4 gate)."""
+    g = golden("mdx23c_full_chunk.npz")
+    m, _ = _model("config_vocals_mdx23c.yaml", "unit", precision="bf16")
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"full chunk bf16: rms={err:.3e}")
+    assert np.isfinite(y).all() and err < 5e-3
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "demix_small_*.npz"))),
+                         ids=lambda p: os.path.basename(p))
+def test_demix_matches_reference(dev, path):
+    from sesa.backend import create_inference_session
+    from sesa.demix import demix_pytorch_optimized
+    g = np.load(path)
+    m, c = _model("config_mdx23c_small.yaml", "random")
+    c.inference.batch_size = int(g["batch_size"])
+    be = create_inference_session(m, device="cuda:0", exec_batch=4)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        out = demix_pytorch_optimized(c, be, g["mix"], "cuda:0")
+    prog = [ln for ln in buf.getvalue().splitlines() if ln.startswith("[SESA_PROGRESS]")]
+    assert prog == list(g["progress"])
+    for k in ("vocals", "other"):
+        assert out[k].shape == g[k].shape
+        assert rms(out[k], g[k]) <= RMS_GATE, k

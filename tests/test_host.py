@@ -1,0 +1,92 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every symbol include/sesa.h
+declares, the parameter registry matches the reference state_dict keys, and the host-side
+chunk plan / progress protocol matches the reference.  No compute calls (no GPU here)."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import CONFIGS, GOLDEN, REPO
+
+
+def header_symbols():
+    with open(os.path.join(REPO, "include", "sesa.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"\b(sesa_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from sesa import _native
+    L = _native.lib()
+    syms = header_symbols()
+    assert len(syms) >= 16
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_native.SIGNATURES), set(syms) ^ set(_native.SIGNATURES)
+
+
+def test_error_path_without_device():
+    """Argument validation happens before any device work and reports through sesa_last_error."""
+    from sesa import _native
+    L = _native.lib()
+    rc = L.sesa_stft_f32(None, 1, 16384, 4096, 1024, 2048, None, None)
+    assert rc == -1 and b"null" in L.sesa_last_error()
+
+
+@pytest.mark.parametrize("cfg_name,tag", [("config_vocals_mdx23c.yaml", "vocals"),
+                                          ("config_mdx23c_small.yaml", "small")])
+def test_native_param_registry_matches_reference(cfg_name, tag):
+    from sesa.utils import get_model_from_config
+    m, _ = get_model_from_config("mdx23c", os.path.join(CONFIGS, cfg_name))
+    with open(os.path.join(GOLDEN, f"params_{tag}.json")) as f:
+        ref = [(n, tuple(s)) for n, s in json.load(f)]
+    assert [(n, tuple(t.shape)) for n, t in m.named_parameters()] == ref
+
+
+def test_load_state_dict_semantics():
+    from sesa.utils import get_model_from_config
+    m, _ = get_model_from_config("mdx23c", os.path.join(CONFIGS, "config_mdx23c_small.yaml"))
+    sd = m.state_dict()
+    sd["bogus"] = sd["first_conv.weight"]
+    with pytest.raises(RuntimeError):
+        m.load_state_dict(sd, strict=True)
+    res = m.load_state_dict(sd, strict=False)  # inference_pytorch.py:368
+    assert res.unexpected_keys == ["bogus"]
+
+
+def test_unknown_and_unported_model_types():
+    from sesa.utils import get_model_from_config
+    with pytest.raises(ValueError):
+        get_model_from_config("nope", os.path.join(CONFIGS, "config_mdx23c_small.yaml"))
+    with pytest.raises(NotImplementedError):
+        get_model_from_config("bs_roformer", os.path.join(CONFIGS, "config_mdx23c_small.yaml"))
+
+
+@pytest.mark.parametrize("name", sorted(os.listdir(GOLDEN)))
+def test_progress_protocol_matches_reference(name):
+    if not name.startswith("demix_small_"):
+        pytest.skip("not a demix fixture")
+    from sesa.demix import chunk_plan
+    g = np.load(os.path.join(GOLDEN, name))
+    _, _, _, _, prog = chunk_plan(int(g["L"]), 64512, 4, int(g["batch_size"]))
+    lines = [f"[SESA_PROGRESS]{p}" for _, p in prog] + ["[SESA_PROGRESS]100"]
+    assert lines == list(g["progress"])
+
+
+def test_chunk_plan_matches_oracle():
+    from oracle.demix import chunk_plan as ref_plan
+    from sesa.demix import chunk_plan
+    for L in (20000, 40000, 96768, 96769, 110250, 441000, 10584000):
+        for bs in (1, 2, 3, 8):
+            a = chunk_plan(L, 261120 if L > 200000 else 64512, 4, bs)
+            b = ref_plan(L, 261120 if L > 200000 else 64512, 4, bs)
+            assert a[:4] == b
+
+
+def test_host_backend_refuses_cpu():
+    from sesa._native import SesaError
+    from sesa.backend import HipBackend
+    with pytest.raises(SesaError):
+        HipBackend(device="cpu")
