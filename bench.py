@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Benchmark: separated-audio seconds per wall second (x real-time) for MDX23C-TFC-TDF-v3 on
+MI355X (BASELINE.json metric; workload = configs[1]: 4-min 44.1 kHz stereo track, chunked).
+
+One "step" = one full pass of the hot path over the track: chunk gather -> native MDX23C forward
+(exec_batch chunks per launch) -> device windowed overlap-add -> finalize, with the mix already
+resident in HBM.  With --gpus N (launched by torch.distributed.run) the track's chunks are sharded
+contiguously over the N ranks and the span partial sums are joined by one RCCL all_gather
+(sesa/parallel.py); value = track seconds processed / max-over-ranks wall time ("strong" scaling:
+one track, fixed total work).
+
+Also reported (rank 0):
+* roofline -- the dominant kernel class (3x3 tap-GEMM convolutions, ~83 % of the FLOPs), timed
+  live in the timed region with hipEvents on the launch stream (libsesa sesa_profile_*):
+  achieved = algorithmic FLOPs / kernel time; peak = dense bf16 MFMA 2.5 PF/s divided by the MFMA
+  passes per algorithmic FLOP (3 in bf16x3 parity precision); traffic = HBM bytes per launch from
+  the committed rocprofv3 PMC summary (profiles/pmc_conv3x3.json) when present.
+* cpu_baseline -- the CPU oracle (PyTorch-CPU fp32 restatement of the reference path, pinned to
+  the reference's golden vectors) on a bounded sample of the same workload (N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "sesa-audio-separation_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+SR = 44100
+CFG = os.path.join(REPO, "sesa-audio-separation_amd", "sesa", "configs", "config_vocals_mdx23c.yaml")
+FLOP_PER_CHUNK = 2.4341e12  # SURVEY §6 (FlopCounterMode on the reference)
+BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cfg, n_chunks_track, track_seconds, sample_chunks):
+    """Oracle (PyTorch-CPU fp32) forward on `sample_chunks` chunks; extrapolated to the track."""
+    from oracle import mdx23c as om
+    from oracle.weights import synth_state_dict
+    threads = torch.get_num_threads()
+    params = om.to_torch_params(synth_state_dict(om.param_shapes(cfg)))
+    rng = np.random.default_rng(0)
+    x = torch.from_numpy((0.1 * rng.standard_normal((1, 2, int(cfg["audio"]["chunk_size"])))).astype(np.float32))
+    t0 = time.time()
+    with torch.inference_mode():
+        for _ in range(sample_chunks):
+            om.forward(params, cfg, x)
+    per_chunk = (time.time() - t0) / sample_chunks
+    return {"value": round(track_seconds / (per_chunk * n_chunks_track), 4), "unit": "separated-audio sec/sec",
+            "cores": threads, "kind": "port",
+            "sample": f"{sample_chunks} of {n_chunks_track} chunks of the same 4-min track, full-width MDX23C "
+                      f"vocals config, oracle/mdx23c.py PyTorch-CPU fp32, {per_chunk:.2f} s/chunk, "
+                      f"extrapolated per chunk (OLA <1% of CPU time, SURVEY §6)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"])
+    ap.add_argument("--exec-batch", type=int, default=16)
+    ap.add_argument("--track-seconds", type=float, default=240.0)
+    ap.add_argument("--cpu-sample-chunks", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from sesa import _native
+    from sesa.demix import chunk_plan
+    from sesa.parallel import demix_sharded
+    from sesa.utils import get_model_from_config
+    from sesa.weights import synth_state_dict
+
+    model, cfg = get_model_from_config("mdx23c", CFG)
+    model.load_state_dict(synth_state_dict(model), strict=True)   # random-init weights (no checkpoint offline)
+    model.set_precision(args.precision)
+    n = int(round(args.track_seconds * SR))
+    rng = np.random.default_rng(0)
+    mix = (0.1 * rng.standard_normal((2, n))).astype(np.float32)
+    mix_d = torch.from_numpy(mix).to(dev)
+    n_chunks = sum(len(b[0]) for b in chunk_plan(n, cfg.audio.chunk_size, cfg.inference.num_overlap,
+                                                    cfg.inference.batch_size)[3])
+
+    def step():
+        return demix_sharded(cfg, model, mix_d, dev, rank=rank, world=world, exec_batch=args.exec_batch)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    _native.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        est = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _native.profile_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(est).all().item()
+
+    ms, launches, work = _native.profile_read("conv3x3")
+    passes = 3 if args.precision == "bf16x3" else 1
+    achieved = work / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    peak = BF16_DENSE_TFLOPS / passes
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_conv3x3.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "kernel": "tap_gemm_kernel<3x3> (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)",
+            "launches": launches, "avg_launch_ms": round(ms / max(launches, 1), 4),
+            "flop_per_launch": round(work / max(launches, 1)),
+            "peak_note": f"2.5 PF/s dense bf16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"}
+    path_tflops = n_chunks * FLOP_PER_CHUNK * args.steps / elapsed / 1e12
+
+    value = args.track_seconds * args.steps / elapsed
+    if rank == 0:
+        line = {
+            "metric": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X",
+            "value": round(value, 3), "unit": "separated-audio sec/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic: 0.1*N(0,1) stereo mix (seed 0), name-keyed random-init weights",
+            "config": {"workload": f"mdx23c_tfc_tdf_v3 vocals config, {args.track_seconds:.0f} s 44.1 kHz stereo "
+                                   f"track chunked (C=261120, overlap 4, {n_chunks} chunks), mix resident in HBM",
+                       "chunks": n_chunks, "exec_batch": args.exec_batch,
+                       "parallelism": f"chunk-shard x{world} + RCCL all_gather" if world > 1 else "1 GPU",
+                       "path_tflops_algorithmic": round(path_tflops, 2)},
+            "roofline": roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            with open(CFG) as f:
+                import yaml
+                raw = yaml.safe_load(f)
+            line["cpu_baseline"] = cpu_baseline(raw, n_chunks, args.track_seconds, args.cpu_sample_chunks)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

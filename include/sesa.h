@@ -118,6 +118,24 @@ int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, float* out, v
                         size_t workspace_bytes, void* stream);
 int sesa_mdx23c_destroy(sesa_mdx23c* m);
 
+/* ---------------------------------------------------------------------------------------
+ * Kernel timing (measurement support for bench.py; not part of the reference surface).
+ * While enabled, every launch issued by libsesa is bracketed by a hipEvent pair on its own
+ * stream and tagged with its kernel class and ALGORITHMIC work (reference FLOPs for the
+ * contractions -- not the 3x MFMA work of the bf16x3 split -- or HBM bytes for streaming
+ * kernels).  sesa_profile_read synchronises on the recorded events.
+ */
+#define SESA_KCLASS_CONV3X3 0
+#define SESA_KCLASS_CONV1X1 1
+#define SESA_KCLASS_DOWN 2
+#define SESA_KCLASS_UP 3
+#define SESA_KCLASS_TDF 4
+#define SESA_KCLASS_STFT 5
+#define SESA_KCLASS_ISTFT 6
+#define SESA_KCLASS_COUNT 7
+int sesa_profile_enable(int enable);   /* 1: start recording (clears previous records), 0: stop */
+int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,3 +13,10 @@ int istft_launch(const float* spec, int n_sig, int dim_f, int frames, int hop, i
                  float* out, float* frame_ws, hipStream_t st);
 
 }  // namespace sesa
+
+namespace sesa {
+// launch timing hooks (sesa_profile.hip): token = profile_begin(st); <launch>; profile_end(token, ...)
+bool profiling();
+void* profile_begin(hipStream_t st);
+void profile_end(void* token, hipStream_t st, int kclass, double work);
+}  // namespace sesa

@@ -287,7 +287,13 @@ struct Fwd {
     a.F_out = F_out;
     a.n_cols = w.n_cols;
     a.n_chunks = w.C_in / kConvBK;
+    const int taps = w.kind == CONV3X3 ? 9 : (w.kind == CONV2X2S2 ? 4 : 1);
+    const int kclass = w.kind == CONV3X3 ? SESA_KCLASS_CONV3X3
+                       : w.kind == CONV1X1 ? SESA_KCLASS_CONV1X1
+                       : w.kind == CONV2X2S2 ? SESA_KCLASS_DOWN : SESA_KCLASS_UP;
+    void* tok = profile_begin(st);
     rc = launch_conv(w.kind, w.bn, x3, a, B, st);
+    profile_end(tok, st, kclass, 2.0 * B * T_out * F_out * (double)w.n_cols * w.C_in * taps);
   }
 
   void tdf(const TdfW& w, const GemmIn& in, int T, float* out, const float* residual, double* out_stats, int C) {
@@ -300,7 +306,9 @@ struct Fwd {
     a.K = w.K;
     a.M = w.M;
     a.n_chunks = (w.K + kTdfBK - 1) / kTdfBK;
+    void* tok = profile_begin(st);
     rc = launch_tdf(x3, a, B, st);
+    profile_end(tok, st, SESA_KCLASS_TDF, 2.0 * B * T * (double)w.M * w.K * C);
   }
 
   // TFC_TDF.forward (mdx23c_tfc_tdf_v3.py:131-138)
@@ -342,7 +350,11 @@ struct Fwd {
     const int n = c.num_scales;
     const int T = m->T0, F = m->F0, dc = m->dim_c;
     Tensor mix{buf((int64_t)B * T * F * dc), nullptr, dc};
-    if (!dry && !rc) rc = stft_launch(x, B * 2, c.chunk_size, c.hop_length, c.dim_f, 1, c.num_subbands, mix.p, st);
+    if (!dry && !rc) {
+      void* tok = profile_begin(st);
+      rc = stft_launch(x, B * 2, c.chunk_size, c.hop_length, c.dim_f, 1, c.num_subbands, mix.p, st);
+      profile_end(tok, st, SESA_KCLASS_STFT, 4.0 * B * (2.0 * c.chunk_size + (double)T * F * dc));
+    }
     Tensor fco{buf((int64_t)B * T * F * c.num_channels), stats(c.num_channels), c.num_channels};
     conv(m->first_conv, input(mix, Tensor{}, SRC_RAW, 0, nullptr, T, F), T, F, T, F, fco.p, nullptr, fco.st, 0);
     Tensor xt = fco;
@@ -380,8 +392,12 @@ struct Fwd {
     conv(m->final2, input(Tensor{f1, nullptr, c.num_channels}, Tensor{}, SRC_RAW, 0, nullptr, T, F), T, F, T, F, fin,
          nullptr, nullptr, 0);
     float* frames = buf((int64_t)B * m->ni * 2 * T * c.n_fft);
-    if (!dry && !rc)
+    if (!dry && !rc) {
+      void* tok = profile_begin(st);
       rc = istft_launch(fin, B * m->ni * 2, c.dim_f, T, c.hop_length, 1, c.num_subbands, m->ni, out, frames, st);
+      profile_end(tok, st, SESA_KCLASS_ISTFT,
+                  4.0 * B * ((double)T * F * cf + m->ni * 2.0 * (2.0 * T * c.n_fft + c.chunk_size)));
+    }
   }
 };
 

@@ -82,7 +82,10 @@ __global__ void ola_accumulate_kernel(const float* __restrict__ y, int n_chunks,
       for (int j = 0; j < n_chunks; ++j) {
         const int64_t off = n - tab.start[j];
         if (off < 0 || off >= tab.seg[j]) continue;
-        r = __fadd_rn(r, __fmul_rn(y[((int64_t)j * n_out_ch + c) * chunk + off], window[off]));
+        // the reference rounds y*w to fp32 before the += : keep the product out of an FMA
+        float prod = y[((int64_t)j * n_out_ch + c) * chunk + off] * window[off];
+        asm volatile("" : "+v"(prod));
+        r = r + prod;
       }
       result[(int64_t)c * L_pad + n] = r;
     }

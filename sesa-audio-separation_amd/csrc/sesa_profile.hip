@@ -1,0 +1,88 @@
+// Optional per-launch hipEvent timing (sesa_profile_*), used by bench.py to time the dominant
+// kernel class live inside the timed region.
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <vector>
+
+#include "sesa_common.hpp"
+#include "sesa_internal.hpp"
+
+namespace sesa {
+namespace {
+struct Rec {
+  int kclass;
+  double work;
+  hipEvent_t e0, e1;
+};
+std::mutex g_mu;
+bool g_on = false;
+std::vector<Rec> g_recs;
+std::vector<hipEvent_t> g_pool;
+
+hipEvent_t get_event() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+}  // namespace
+
+bool profiling() { return g_on; }
+
+void* profile_begin(hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_on) return nullptr;
+  hipEvent_t e = get_event();
+  (void)hipEventRecord(e, st);
+  return e;
+}
+
+void profile_end(void* token, hipStream_t st, int kclass, double work) {
+  if (!token) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  hipEvent_t e1 = get_event();
+  (void)hipEventRecord(e1, st);
+  g_recs.push_back(Rec{kclass, work, (hipEvent_t)token, e1});
+}
+
+}  // namespace sesa
+
+using namespace sesa;
+
+extern "C" int sesa_profile_enable(int enable) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (enable) {
+    for (auto& r : g_recs) {
+      g_pool.push_back(r.e0);
+      g_pool.push_back(r.e1);
+    }
+    g_recs.clear();
+  }
+  g_on = enable != 0;
+  return SESA_OK;
+}
+
+extern "C" int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work) {
+  clear_error();
+  std::lock_guard<std::mutex> lk(g_mu);
+  double ms = 0, work = 0;
+  int64_t n = 0;
+  for (auto& r : g_recs) {
+    if (r.kclass != kclass) continue;
+    SESA_CHECK_HIP(hipEventSynchronize(r.e1));
+    float t = 0;
+    SESA_CHECK_HIP(hipEventElapsedTime(&t, r.e0, r.e1));
+    ms += t;
+    work += r.work;
+    ++n;
+  }
+  if (total_ms) *total_ms = ms;
+  if (launches) *launches = n;
+  if (total_work) *total_work = work;
+  return SESA_OK;
+}

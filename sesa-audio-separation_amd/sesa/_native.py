@@ -40,7 +40,23 @@ SIGNATURES = {
     "sesa_mdx23c_workspace_size": (c_size_t, [c_void_p, c_int]),
     "sesa_mdx23c_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
     "sesa_mdx23c_destroy": (c_int, [c_void_p]),
+    "sesa_profile_enable": (c_int, [c_int]),
+    "sesa_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
+                                  ctypes.POINTER(ctypes.c_double)]),
 }
+
+KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6}
+
+
+def profile_enable(on):
+    check(lib().sesa_profile_enable(1 if on else 0), "sesa_profile_enable")
+
+
+def profile_read(kclass):
+    ms, n, work = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+    check(lib().sesa_profile_read(KCLASS[kclass] if isinstance(kclass, str) else kclass, ctypes.byref(ms),
+                                  ctypes.byref(n), ctypes.byref(work)), "sesa_profile_read")
+    return ms.value, n.value, work.value
 
 
 class SesaError(RuntimeError):
