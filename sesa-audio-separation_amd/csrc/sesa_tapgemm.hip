@@ -25,6 +25,8 @@
 // ds_read_b128 lane groups are bank-conflict free.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "sesa_common.hpp"
 #include "sesa_tapgemm.hpp"
 
@@ -34,6 +36,23 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxCin = 1536;
 
+// Compile-time unrolled loop: f(std::integral_constant<int, I>) for I in [0, N).  Array indices become
+// frontend constants, so SROA keeps staging arrays in registers (a pragma-unrolled loop left the
+// 9-entry weight staging array in scratch).
+template <int I, int N>
+struct Unroll {
+  template <class F>
+  __device__ __forceinline__ static void run(F&& f) {
+    f(std::integral_constant<int, I>{});
+    Unroll<I + 1, N>::run(f);
+  }
+};
+template <int N>
+struct Unroll<N, N> {
+  template <class F>
+  __device__ __forceinline__ static void run(F&&) {}
+};
+
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -42,11 +61,22 @@ __device__ __forceinline__ uint32_t pack2(__bf16 a, __bf16 b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
 }
 
+// Select source 0/1 without runtime-indexing the kernel-argument struct (which would go to scratch).
+__device__ __forceinline__ Src pick_src(const GemmIn& in, int s) {
+  Src r;
+  r.ptr = s ? in.src[1].ptr : in.src[0].ptr;
+  r.stats = s ? in.src[1].stats : in.src[0].stats;
+  r.mul = s ? in.src[1].mul : in.src[0].mul;
+  r.C = s ? in.src[1].C : in.src[0].C;
+  r.mode = s ? in.src[1].mode : in.src[0].mode;
+  return r;
+}
+
 // Per-channel affine (scale, shift) of the consumer's InstanceNorm, from the producer's sums.
 __device__ void build_affine(const GemmIn& in, int b, float* sc, float* sh) {
   for (int c = threadIdx.x; c < in.C_in; c += kThreads) {
     const int s = c < in.C_split ? 0 : 1;
-    const Src& src = in.src[s];
+    const Src src = pick_src(in, s);
     const int cl = c - (s ? in.C_split : 0);
     float scale = 1.f, shift = 0.f;
     if (src.mode == SRC_NORM_GELU) {
@@ -123,41 +153,115 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 
   const uint16_t* wblk = a.w + (int64_t)nb * a.n_chunks * (2 * W_BYTES / 2);
 
+  // Register-staged software pipeline: the global loads of chunk k+1 are issued before the MFMAs
+  // of chunk k and land while they run; transform + LDS write happen between two barriers.
+  constexpr int A_ITEMS = (NPOS * 4 + kThreads - 1) / kThreads;
+  constexpr int W16 = (X3 ? 2 : 1) * W_BYTES / 16;
+  constexpr int W_ITEMS = (W16 + kThreads - 1) / kThreads;
+  static_assert(A_ITEMS <= 32, "valid mask");
+  f32x4 areg[A_ITEMS];  // native vectors: HIP's float4/uint4 structs copy via memcpy and defeat SROA
+  u32x4 wreg[W_ITEMS];
+  uint32_t avalid = 0;
+
+  // prologue: chunk 0 into registers
+  {
+    const int kc = 0;
+
+    const u32x4* wsrc = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * (2 * W_BYTES / 2));
+    Unroll<0, W_ITEMS>::run([&](auto I) {
+      const int e = tid + I * kThreads;
+      wreg[I] = wsrc[e < W16 ? e : W16 - 1];  // unconditional (clamped) so wreg stays in VGPRs
+    });
+    const int k0 = kc * kConvBK;
+    const int s = k0 < a.in.C_split ? 0 : 1;
+    const Src src = pick_src(a.in, s);
+    const int cl0 = k0 - (s ? a.in.C_split : 0);
+    avalid = 0;
+    Unroll<0, A_ITEMS>::run([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int e = tid + i * kThreads;
+      const int p = e >> 2, g = e & 3;
+      const int hr = p / HW, hc = p - hr * HW;
+      const int ti = t_in0 + hr, fi = f_in0 + hc;
+      const bool ok = (e < NPOS * 4) && ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in;
+      if (ok) {
+        const int64_t idx = (((int64_t)b * a.T_in + ti) * a.F_in + fi) * src.C + cl0 + 4 * g;
+        areg[i] = *reinterpret_cast<const f32x4*>(src.ptr + idx);
+        avalid |= 1u << i;
+      } else {
+        areg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    });
+  }
   for (int kc = 0; kc < a.n_chunks; ++kc) {
     __syncthreads();  // previous chunk's fragment reads are done (and sc/sh are built)
-    // ---- stage W (pre-packed, pre-swizzled image: straight copy) ----
     {
-      const uint4* src = reinterpret_cast<const uint4*>(wblk + (int64_t)kc * (2 * W_BYTES / 2));
-      uint4* dst = reinterpret_cast<uint4*>(W_hi);
-      constexpr int N16 = (X3 ? 2 : 1) * W_BYTES / 16;
-      for (int e = tid; e < N16; e += kThreads) dst[e] = src[e];
-    }
-    // ---- stage A: halo x 16 channels, transformed + split ----
-    {
-      const int k0 = kc * kConvBK;
-      const int s = k0 < a.in.C_split ? 0 : 1;
-      const Src& src = a.in.src[s];
-      const int cl0 = k0 - (s ? a.in.C_split : 0);
-      for (int e = tid; e < NPOS * 4; e += kThreads) {
-        const int p = e >> 2, g = e & 3;
-        const int hr = p / HW, hc = p - hr * HW;
-        const int ti = t_in0 + hr, fi = f_in0 + hc;
-        float v[4] = {0.f, 0.f, 0.f, 0.f};
-        if (ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in) {
-          const int64_t idx = (((int64_t)b * a.T_in + ti) * a.F_in + fi) * src.C + cl0 + 4 * g;
-          const float4 x = *reinterpret_cast<const float4*>(src.ptr + idx);
-          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-          transform4(v, src.mode, sc, sh, k0 + 4 * g, src.mode == SRC_MUL ? src.mul + idx : nullptr);
+
+    u32x4* wdst = reinterpret_cast<u32x4*>(W_hi);
+    Unroll<0, W_ITEMS>::run([&](auto I) {
+      const int e = tid + I * kThreads;
+      if (W16 % kThreads == 0 || e < W16) wdst[e] = wreg[I];
+    });
+    const int k0 = kc * kConvBK;
+    const int s = k0 < a.in.C_split ? 0 : 1;
+    const Src src = pick_src(a.in, s);
+    const int cl0 = k0 - (s ? a.in.C_split : 0);
+    Unroll<0, A_ITEMS>::run([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int e = tid + i * kThreads;
+      if (NPOS * 4 % kThreads != 0 && e >= NPOS * 4) return;
+      const int p = e >> 2, g = e & 3;
+      float v[4] = {areg[i][0], areg[i][1], areg[i][2], areg[i][3]};
+      if (avalid & (1u << i)) {
+        const float* mulp = nullptr;
+        if (src.mode == SRC_MUL) {
+          const int hr = p / HW, hc = p - hr * HW;
+          const int64_t idx = (((int64_t)b * a.T_in + t_in0 + hr) * a.F_in + f_in0 + hc) * src.C + cl0 + 4 * g;
+          mulp = src.mul + idx;
         }
-        __bf16 hi[4], lo[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) split_bf16(v[q], hi[q], lo[q]);
-        const int off = p * 32 + ((((g >> 1) ^ ((p >> 3) & 1))) << 4) + ((g & 1) << 3);
-        *reinterpret_cast<uint2*>(A_hi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
-        if (X3) *reinterpret_cast<uint2*>(A_lo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
+        transform4(v, src.mode, sc, sh, k0 + 4 * g, mulp);
       }
+      __bf16 hi[4], lo[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) split_bf16(v[q], hi[q], lo[q]);
+      const int off = p * 32 + ((((g >> 1) ^ ((p >> 3) & 1))) << 4) + ((g & 1) << 3);
+      *reinterpret_cast<uint2*>(A_hi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
+      if (X3) *reinterpret_cast<uint2*>(A_lo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
+    });
     }
     __syncthreads();
+    if (kc + 1 < a.n_chunks) {
+      const int kcn = kc + 1;
+      {
+        const int kc = kcn;
+
+    const u32x4* wsrc = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * (2 * W_BYTES / 2));
+    Unroll<0, W_ITEMS>::run([&](auto I) {
+      const int e = tid + I * kThreads;
+      wreg[I] = wsrc[e < W16 ? e : W16 - 1];  // unconditional (clamped) so wreg stays in VGPRs
+    });
+    const int k0 = kc * kConvBK;
+    const int s = k0 < a.in.C_split ? 0 : 1;
+    const Src src = pick_src(a.in, s);
+    const int cl0 = k0 - (s ? a.in.C_split : 0);
+    avalid = 0;
+    Unroll<0, A_ITEMS>::run([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int e = tid + i * kThreads;
+      const int p = e >> 2, g = e & 3;
+      const int hr = p / HW, hc = p - hr * HW;
+      const int ti = t_in0 + hr, fi = f_in0 + hc;
+      const bool ok = (e < NPOS * 4) && ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in;
+      if (ok) {
+        const int64_t idx = (((int64_t)b * a.T_in + ti) * a.F_in + fi) * src.C + cl0 + 4 * g;
+        areg[i] = *reinterpret_cast<const f32x4*>(src.ptr + idx);
+        avalid |= 1u << i;
+      } else {
+        areg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    });
+      }
+    }
     // ---- MFMA over the taps ----
 #pragma unroll
     for (int tap = 0; tap < TAPS; ++tap) {
@@ -289,7 +393,7 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
   const int bt = blockIdx.z;
   const int b = bt / a.T, t = bt - b * a.T;
   const int C = a.in.src[0].C;  // TDF input is a single source
-  const Src& src = a.in.src[0];
+  const Src src = pick_src(a.in, 0);
 
   build_affine(a.in, b, sc, sh);
 
@@ -304,42 +408,65 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
   const float* xrow = src.ptr + ((int64_t)b * a.T + t) * a.K * C;
   const uint16_t* wblk = a.w + (int64_t)mb * a.n_chunks * (2 * AW_BYTES / 2);
 
+  constexpr int N16 = (X3 ? 2 : 1) * AW_BYTES / 16;
+  constexpr int W_ITEMS = (N16 + kThreads - 1) / kThreads;
+  constexpr int B_ITEMS = (BN * 4 + kThreads - 1) / kThreads;
+  u32x4 wreg[W_ITEMS];
+  float breg[B_ITEMS][8];
+
+  // prefetch chunk kc into registers (issued before the previous chunk's MFMAs)
+  auto load_chunk = [&](int kc) {
+    const u32x4* s4 = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * (2 * AW_BYTES / 2));
+    Unroll<0, W_ITEMS>::run([&](auto I) {
+      const int e = tid + I * kThreads;
+      wreg[I] = s4[e < N16 ? e : N16 - 1];
+    });
+    const int k0 = kc * kTdfBK;
+    Unroll<0, B_ITEMS>::run([&](auto I) {
+      const int e = tid + I * kThreads;
+      const int n = e % BN, g = e / BN;  // lanes walk channels: 256 B coalesced per k
+      const int c = c0 + n;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = k0 + 8 * g + j;
+        breg[I][j] = (e < BN * 4 && c < C && k < a.K) ? xrow[(int64_t)k * C + c] : 0.f;
+      }
+    });
+  };
+
+  load_chunk(0);
   for (int kc = 0; kc < a.n_chunks; ++kc) {
     __syncthreads();
     {
-      const uint4* s4 = reinterpret_cast<const uint4*>(wblk + (int64_t)kc * (2 * AW_BYTES / 2));
-      uint4* d4 = reinterpret_cast<uint4*>(Whi);
-      constexpr int N16 = (X3 ? 2 : 1) * AW_BYTES / 16;
-      for (int e = tid; e < N16; e += kThreads) d4[e] = s4[e];
-    }
-    {
+      u32x4* d4 = reinterpret_cast<u32x4*>(Whi);
+      Unroll<0, W_ITEMS>::run([&](auto I) {
+        const int e = tid + I * kThreads;
+        if (N16 % kThreads == 0 || e < N16) d4[e] = wreg[I];
+      });
       const int k0 = kc * kTdfBK;
-      for (int e = tid; e < BN * 4; e += kThreads) {
-        const int n = e % BN, g = e / BN;  // lanes walk channels: 256 B coalesced per k
+      Unroll<0, B_ITEMS>::run([&](auto I) {
+        const int e = tid + I * kThreads;
+        if (BN * 4 % kThreads != 0 && e >= BN * 4) return;
+        const int n = e % BN, g = e / BN;
         const int c = c0 + n;
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = k0 + 8 * g + j;
-          float x = 0.f;
-          if (c < C && k < a.K) {
-            x = xrow[(int64_t)k * C + c];
-            if (src.mode == SRC_NORM_GELU) x = gelu_erf(x * sc[c] + sh[c]);
-          }
-          v[j] = x;
-        }
         __bf16 hi[8], lo[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) split_bf16(v[j], hi[j], lo[j]);
+        for (int j = 0; j < 8; ++j) {
+          float x = breg[I][j];
+          const int k = k0 + 8 * g + j;
+          if (src.mode == SRC_NORM_GELU && c < C && k < a.K) x = gelu_erf(x * sc[c] + sh[c]);
+          split_bf16(x, hi[j], lo[j]);
+        }
         const int off = n * ROWB + ((g ^ ((n >> 2) & 3)) << 4);
         *reinterpret_cast<uint4*>(Bhi + off) =
             make_uint4(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]), pack2(hi[4], hi[5]), pack2(hi[6], hi[7]));
         if (X3)
           *reinterpret_cast<uint4*>(Blo + off) =
               make_uint4(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]), pack2(lo[4], lo[5]), pack2(lo[6], lo[7]));
-      }
+      });
     }
     __syncthreads();
+    if (kc + 1 < a.n_chunks) load_chunk(kc + 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
