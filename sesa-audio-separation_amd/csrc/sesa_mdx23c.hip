@@ -158,7 +158,9 @@ Stack add_stack(sesa_mdx23c* m, const std::string& prefix, int in_c, int c, int 
 }
 
 // ---- weight packing (layouts consumed by sesa_tapgemm.hip) ----
-void pack_conv(const Param& P, ConvW& w, std::vector<uint16_t>& blob) {
+// Packs one conv (and, for a 3x3 with a fused 1x1 shortcut `xs`, the shortcut's one-tap chunks
+// after each output block's main chunks: [nb][main kc][hi,lo][tap][BN][16] then [xs kc][hi,lo][BN][16]).
+void pack_conv(const Param& P, ConvW& w, std::vector<uint16_t>& blob, const Param* xs = nullptr, int xs_cin = 0) {
   const bool tr = w.kind == DECONV2X2S2;
   const int KH = (int)P.shape[2], KW = (int)P.shape[3];
   const int taps = tr ? 1 : KH * KW;
@@ -168,12 +170,21 @@ void pack_conv(const Param& P, ConvW& w, std::vector<uint16_t>& blob) {
   const int nch = w.C_in / kConvBK;
   w.w_off = (int64_t)blob.size();
   const int64_t img = (int64_t)taps * BN * 16;  // uint16 per image
-  blob.resize(blob.size() + (size_t)nblk * nch * 2 * img, 0);
+  const int xch = xs ? xs_cin / kConvBK : 0;
+  const int64_t img1 = (int64_t)BN * 16;
+  const int64_t per_nb = (int64_t)nch * 2 * img + (int64_t)xch * 2 * img1;
+  blob.resize(blob.size() + (size_t)nblk * per_nb, 0);
   uint16_t* base = blob.data() + w.w_off;
   const float* W = P.host.data();
-  for (int nb = 0; nb < nblk; ++nb)
+  auto put = [&](uint16_t* hi, uint16_t* lo, int p, int kk, float v) {
+    const int64_t o = (int64_t)p * 16 + ((((kk >> 3) ^ ((p >> 3) & 1))) << 3) + (kk & 7);
+    const uint16_t h = f2bf(v);
+    hi[o] = h;
+    lo[o] = f2bf(v - bf2f(h));
+  };
+  for (int nb = 0; nb < nblk; ++nb) {
     for (int kc = 0; kc < nch; ++kc) {
-      uint16_t* hi = base + ((int64_t)nb * nch + kc) * 2 * img;
+      uint16_t* hi = base + nb * per_nb + (int64_t)kc * 2 * img;
       uint16_t* lo = hi + img;
       for (int tap = 0; tap < taps; ++tap)
         for (int n = 0; n < BN; ++n)
@@ -189,21 +200,29 @@ void pack_conv(const Param& P, ConvW& w, std::vector<uint16_t>& blob) {
                 v = W[(((int64_t)ci * w.C_out + co) * 2 + (t2 >> 1)) * 2 + (t2 & 1)];
               }
             }
-            const int p = tap * BN + n;
-            const int64_t o = (int64_t)p * 16 + ((((kk >> 3) ^ ((p >> 3) & 1))) << 3) + (kk & 7);
-            const uint16_t h = f2bf(v);
-            hi[o] = h;
-            lo[o] = f2bf(v - bf2f(h));
+            put(hi, lo, tap * BN + n, kk, v);
           }
     }
+    for (int kc = 0; kc < xch; ++kc) {
+      uint16_t* hi = base + nb * per_nb + (int64_t)nch * 2 * img + (int64_t)kc * 2 * img1;
+      uint16_t* lo = hi + img1;
+      for (int n = 0; n < BN; ++n)
+        for (int kk = 0; kk < kConvBK; ++kk) {
+          const int ncol = nb * BN + n, ci = kc * kConvBK + kk;
+          const float v = ncol < N ? xs->host[(int64_t)ncol * xs_cin + ci] : 0.f;  // [c_out, c_in, 1, 1]
+          put(hi, lo, n, kk, v);
+        }
+    }
+  }
 }
 
 void pack_tdf(const Param& P, TdfW& w, std::vector<uint16_t>& blob) {
   const int M = w.M, K = w.K;
-  const int nmb = (M + kTdfBM - 1) / kTdfBM;
+  const int BM = tdf_block_rows(M);
+  const int nmb = (M + BM - 1) / BM;
   const int nch = (K + kTdfBK - 1) / kTdfBK;
   w.w_off = (int64_t)blob.size();
-  const int64_t img = (int64_t)kTdfBM * kTdfBK;
+  const int64_t img = (int64_t)BM * kTdfBK;
   blob.resize(blob.size() + (size_t)nmb * nch * 2 * img, 0);
   uint16_t* base = blob.data() + w.w_off;
   const float* W = P.host.data();
@@ -211,9 +230,9 @@ void pack_tdf(const Param& P, TdfW& w, std::vector<uint16_t>& blob) {
     for (int kc = 0; kc < nch; ++kc) {
       uint16_t* hi = base + ((int64_t)mb * nch + kc) * 2 * img;
       uint16_t* lo = hi + img;
-      for (int row = 0; row < kTdfBM; ++row)
+      for (int row = 0; row < BM; ++row)
         for (int kk = 0; kk < kTdfBK; ++kk) {
-          const int m = mb * kTdfBM + row, k = kc * kTdfBK + kk;
+          const int m = mb * BM + row, k = kc * kTdfBK + kk;
           const float v = (m < M && k < K) ? W[(int64_t)m * K + k] : 0.f;
           const int64_t o = (int64_t)row * kTdfBK + (((kk >> 3) ^ ((row >> 2) & 3)) << 3) + (kk & 7);
           const uint16_t h = f2bf(v);
@@ -275,7 +294,7 @@ struct Fwd {
   }
 
   void conv(const ConvW& w, const GemmIn& in, int T_in, int F_in, int T_out, int F_out, float* out,
-            const float* residual, double* out_stats, int gelu) {
+            const float* residual, double* out_stats, int gelu, const GemmIn* xin = nullptr) {
     if (dry || rc) return;
     ConvArgs a{};
     a.in = in;
@@ -287,16 +306,23 @@ struct Fwd {
     a.F_out = F_out;
     a.n_cols = w.n_cols;
     a.n_chunks = w.C_in / kConvBK;
+    if (xin) {
+      a.xin = *xin;
+      a.x_chunks = xin->C_in / kConvBK;
+    }
     const int taps = w.kind == CONV3X3 ? 9 : (w.kind == CONV2X2S2 ? 4 : 1);
     const int kclass = w.kind == CONV3X3 ? SESA_KCLASS_CONV3X3
                        : w.kind == CONV1X1 ? SESA_KCLASS_CONV1X1
                        : w.kind == CONV2X2S2 ? SESA_KCLASS_DOWN : SESA_KCLASS_UP;
     void* tok = profile_begin(st);
     rc = launch_conv(w.kind, w.bn, x3, a, B, st);
-    profile_end(tok, st, kclass, 2.0 * B * T_out * F_out * (double)w.n_cols * w.C_in * taps);
+    profile_end(tok, st, kclass,
+                2.0 * B * T_out * F_out * (double)w.n_cols * (w.C_in * taps + (xin ? xin->C_in : 0)));
   }
 
-  void tdf(const TdfW& w, const GemmIn& in, int T, float* out, const float* residual, double* out_stats, int C) {
+  // transposed_io 0: first Linear (NHWC in, U^T [B][T][C][F/bn] out); 1: second Linear (U^T in, NHWC out)
+  void tdf(const TdfW& w, const GemmIn& in, int T, float* out, const float* residual, double* out_stats, int C,
+           int transposed_io) {
     if (dry || rc) return;
     TdfArgs a{};
     a.in = in;
@@ -307,7 +333,7 @@ struct Fwd {
     a.M = w.M;
     a.n_chunks = (w.K + kTdfBK - 1) / kTdfBK;
     void* tok = profile_begin(st);
-    rc = launch_tdf(x3, a, B, st);
+    rc = launch_tdf(x3, a, B, st, transposed_io);
     profile_end(tok, st, SESA_KCLASS_TDF, 2.0 * B * T * (double)w.M * w.K * C);
   }
 
@@ -318,26 +344,25 @@ struct Fwd {
       const Block& bk = s.blocks[i];
       const int c = bk.c;
       const int64_t plane = (int64_t)B * L.T * L.F * c;
-      float* S = buf(plane);
+      float* S = buf(plane);  // block output
       float* H = buf(plane);
-      float* U = buf((int64_t)B * L.T * (L.F / bnf) * c);
+      float* U = buf((int64_t)B * L.T * (L.F / bnf) * c);  // U^T [B][T][c][F/bn]
       double* st_h1 = stats(c);
       double* st_u = stats(c);
       double* st_h2 = stats(c);
       double* st_out = stats(c);
-      // s = shortcut(x)
-      conv(bk.shortcut, input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F), L.T, L.F, L.T, L.F, S, nullptr, nullptr, 0);
       // x = tfc1(x)
       conv(bk.conv1, input(x0, x1, SRC_NORM_GELU, SRC_NORM_GELU, &bk.tfc1, L.T, L.F), L.T, L.F, L.T, L.F, H, nullptr,
            st_h1, 0);
       // x = x + tdf(x)
       tdf(bk.lin1, input(Tensor{H, st_h1, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf0, L.T, L.F), L.T, U, nullptr, st_u,
-          c);
+          c, 0);
       tdf(bk.lin2, input(Tensor{U, st_u, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf3, L.T, L.F / bnf), L.T, H, H, st_h2,
-          c);
-      // x = tfc2(x) + s
+          c, 1);
+      // x = tfc2(x) + shortcut(block input): the 1x1 shortcut rides along as extra K (raw input)
+      const GemmIn xs = input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F);
       conv(bk.conv2, input(Tensor{H, st_h2, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tfc2, L.T, L.F), L.T, L.F, L.T, L.F, S,
-           S, st_out, 0);
+           nullptr, st_out, 0, &xs);
       x0 = Tensor{S, st_out, c};
       x1 = Tensor{};
     }
@@ -503,8 +528,7 @@ extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
   auto pstack = [&](Stack& s) {
     for (auto& b : s.blocks) {
       pc(b.conv1);
-      pc(b.conv2);
-      pc(b.shortcut);
+      pack_conv(m->params[b.conv2.param], b.conv2, blob, &m->params[b.shortcut.param], b.in_c);
       pack_tdf(m->params[b.lin1.param], b.lin1, blob);
       pack_tdf(m->params[b.lin2.param], b.lin2, blob);
       pack_norm(m, b.tfc1, aff);

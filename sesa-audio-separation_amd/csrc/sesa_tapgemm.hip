@@ -107,7 +107,11 @@ __device__ __forceinline__ void transform4(float (&v)[4], int mode, const float*
 }
 
 // ---------------------------------------------------------------------------------------------
-template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool X3, bool UPS>
+// K is walked in 16-channel chunks: first the n_chunks chunks of the main (normalised) input over
+// all KH*KW taps, then x_chunks chunks of an optional RAW extra input over the centre tap only --
+// the 1x1 shortcut of TFC_TDF (mdx23c_tfc_tdf_v3.py:126, :132, :137) fused into tfc2's conv as
+// extra K, so `s` never round-trips through HBM.
+template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool X3, bool UPS, bool XTRA>
 __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int MI = TM / WM;                 // 32-position MFMA row blocks per wave
@@ -116,16 +120,17 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
   constexpr int HW = (kTF - 1) * S + KW;      // halo cols
   constexpr int NPOS = HT * HW;
   constexpr int TAPS = KH * KW;
+  constexpr int CTAP = (KH / 2) * KW + KW / 2;  // centre tap (the 1x1 shortcut's alignment, PAD = 1)
   constexpr int A_BYTES = NPOS * 32;          // one (hi or lo) image: 16 bf16 per position
   constexpr int W_BYTES = TAPS * BN * 32;
+  constexpr int W1_BYTES = BN * 32;           // one-tap image of an extra (shortcut) chunk
   static_assert(MI >= 1 && NI >= 1, "tile");
 
   __shared__ __attribute__((aligned(16))) char smem[2 * A_BYTES + 2 * W_BYTES + 2 * kMaxCin * 4];
   char* A_hi = smem;
   char* A_lo = smem + A_BYTES;
   char* W_hi = smem + 2 * A_BYTES;
-  char* W_lo = W_hi + W_BYTES;
-  float* sc = reinterpret_cast<float*>(W_lo + W_BYTES);
+  float* sc = reinterpret_cast<float*>(W_hi + 2 * W_BYTES);
   float* sh = sc + kMaxCin;
 
   const int tid = threadIdx.x;
@@ -140,6 +145,7 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
   const int nb = blockIdx.y;
   const int b = blockIdx.z;
   const int t_in0 = t0 * S - PAD, f_in0 = f0 * S - PAD;
+  const int n_total = a.n_chunks + (XTRA ? a.x_chunks : 0);
 
   build_affine(a.in, b, sc, sh);
 
@@ -151,7 +157,8 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const uint16_t* wblk = a.w + (int64_t)nb * a.n_chunks * (2 * W_BYTES / 2);
+  // per-nb weight block: [n_chunks x (hi,lo) TAPS-tap images][x_chunks x (hi,lo) 1-tap images]
+  const uint16_t* wblk = a.w + (int64_t)nb * (a.n_chunks * W_BYTES + (XTRA ? a.x_chunks * W1_BYTES : 0));
 
   // Register-staged software pipeline: the global loads of chunk k+1 are issued before the MFMAs
   // of chunk k and land while they run; transform + LDS write happen between two barriers.
@@ -163,19 +170,29 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
   u32x4 wreg[W_ITEMS];
   uint32_t avalid = 0;
 
-  // prologue: chunk 0 into registers
-  {
-    const int kc = 0;
+  // source of chunk kc: (src, local channel offset, first concatenated channel, is-extra)
+  auto chunk_src = [&](int kc, Src& src, int& cl0, int& k0, bool& ext) {
+    ext = XTRA && kc >= a.n_chunks;
+    k0 = (ext ? kc - a.n_chunks : kc) * kConvBK;
+    const GemmIn& g = ext ? a.xin : a.in;
+    const int s = k0 < g.C_split ? 0 : 1;
+    src = pick_src(g, s);
+    cl0 = k0 - (s ? g.C_split : 0);
+  };
 
-    const u32x4* wsrc = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * (2 * W_BYTES / 2));
+  auto load_chunk = [&](int kc) {
+    Src src;
+    int cl0, k0;
+    bool ext;
+    chunk_src(kc, src, cl0, k0, ext);
+    const int w16 = ext ? (X3 ? 2 : 1) * W1_BYTES / 16 : W16;
+    const u32x4* wsrc = reinterpret_cast<const u32x4*>(
+        wblk + (ext ? (int64_t)a.n_chunks * W_BYTES + (int64_t)(kc - a.n_chunks) * W1_BYTES
+                    : (int64_t)kc * W_BYTES));
     Unroll<0, W_ITEMS>::run([&](auto I) {
       const int e = tid + I * kThreads;
-      wreg[I] = wsrc[e < W16 ? e : W16 - 1];  // unconditional (clamped) so wreg stays in VGPRs
+      wreg[I] = wsrc[e < w16 ? e : w16 - 1];  // unconditional (clamped) so wreg stays in VGPRs
     });
-    const int k0 = kc * kConvBK;
-    const int s = k0 < a.in.C_split ? 0 : 1;
-    const Src src = pick_src(a.in, s);
-    const int cl0 = k0 - (s ? a.in.C_split : 0);
     avalid = 0;
     Unroll<0, A_ITEMS>::run([&](auto I) {
       constexpr int i = decltype(I)::value;
@@ -192,27 +209,26 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
         areg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     });
-  }
-  for (int kc = 0; kc < a.n_chunks; ++kc) {
-    __syncthreads();  // previous chunk's fragment reads are done (and sc/sh are built)
-    {
+  };
 
+  auto store_chunk = [&](int kc) {
+    Src src;
+    int cl0, k0;
+    bool ext;
+    chunk_src(kc, src, cl0, k0, ext);
+    const int w16 = ext ? (X3 ? 2 : 1) * W1_BYTES / 16 : W16;
     u32x4* wdst = reinterpret_cast<u32x4*>(W_hi);
     Unroll<0, W_ITEMS>::run([&](auto I) {
       const int e = tid + I * kThreads;
-      if (W16 % kThreads == 0 || e < W16) wdst[e] = wreg[I];
+      if (e < w16) wdst[e] = wreg[I];
     });
-    const int k0 = kc * kConvBK;
-    const int s = k0 < a.in.C_split ? 0 : 1;
-    const Src src = pick_src(a.in, s);
-    const int cl0 = k0 - (s ? a.in.C_split : 0);
     Unroll<0, A_ITEMS>::run([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int e = tid + i * kThreads;
       if (NPOS * 4 % kThreads != 0 && e >= NPOS * 4) return;
       const int p = e >> 2, g = e & 3;
       float v[4] = {areg[i][0], areg[i][1], areg[i][2], areg[i][3]};
-      if (avalid & (1u << i)) {
+      if (!ext && (avalid & (1u << i))) {
         const float* mulp = nullptr;
         if (src.mode == SRC_MUL) {
           const int hr = p / HW, hc = p - hr * HW;
@@ -228,70 +244,49 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
       *reinterpret_cast<uint2*>(A_hi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
       if (X3) *reinterpret_cast<uint2*>(A_lo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
     });
-    }
-    __syncthreads();
-    if (kc + 1 < a.n_chunks) {
-      const int kcn = kc + 1;
-      {
-        const int kc = kcn;
+  };
 
-    const u32x4* wsrc = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * (2 * W_BYTES / 2));
-    Unroll<0, W_ITEMS>::run([&](auto I) {
-      const int e = tid + I * kThreads;
-      wreg[I] = wsrc[e < W16 ? e : W16 - 1];  // unconditional (clamped) so wreg stays in VGPRs
-    });
-    const int k0 = kc * kConvBK;
-    const int s = k0 < a.in.C_split ? 0 : 1;
-    const Src src = pick_src(a.in, s);
-    const int cl0 = k0 - (s ? a.in.C_split : 0);
-    avalid = 0;
-    Unroll<0, A_ITEMS>::run([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const int e = tid + i * kThreads;
-      const int p = e >> 2, g = e & 3;
-      const int hr = p / HW, hc = p - hr * HW;
-      const int ti = t_in0 + hr, fi = f_in0 + hc;
-      const bool ok = (e < NPOS * 4) && ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in;
-      if (ok) {
-        const int64_t idx = (((int64_t)b * a.T_in + ti) * a.F_in + fi) * src.C + cl0 + 4 * g;
-        areg[i] = *reinterpret_cast<const f32x4*>(src.ptr + idx);
-        avalid |= 1u << i;
-      } else {
-        areg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    });
-      }
+  // one tap: A window shifted by (dy, dx), W image tap `wt` of a (hi, lo) image pair `wimg` bytes apart
+  auto mfma_tap = [&](int dy, int dx, int wt, int wimg) {
+    bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * MI + i;
+      const int p = (row * S + dy) * HW + l32 * S + dx;
+      const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+      ah[i] = *reinterpret_cast<const bf16x8*>(A_hi + off);
+      if (X3) al[i] = *reinterpret_cast<const bf16x8*>(A_lo + off);
     }
-    // ---- MFMA over the taps ----
 #pragma unroll
-    for (int tap = 0; tap < TAPS; ++tap) {
-      const int dy = tap / KW, dx = tap % KW;
-      bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
+    for (int j = 0; j < NI; ++j) {
+      const int p = wt * BN + (wn * NI + j) * 32 + l32;
+      const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+      bh[j] = *reinterpret_cast<const bf16x8*>(W_hi + off);
+      if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(W_hi + wimg + off);
+    }
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int row = wm * MI + i;
-        const int p = (row * S + dy) * HW + l32 * S + dx;
-        const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
-        ah[i] = *reinterpret_cast<const bf16x8*>(A_hi + off);
-        if (X3) al[i] = *reinterpret_cast<const bf16x8*>(A_lo + off);
-      }
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int p = tap * BN + (wn * NI + j) * 32 + l32;
-        const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
-        bh[j] = *reinterpret_cast<const bf16x8*>(W_hi + off);
-        if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(W_lo + off);
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          if (X3) {
-            acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
-            acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
-          }
-          acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+        if (X3) {
+          acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
         }
+        acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+      }
+  };
+
+  load_chunk(0);
+  for (int kc = 0; kc < n_total; ++kc) {
+    __syncthreads();  // previous chunk's fragment reads are done (and sc/sh are built)
+    store_chunk(kc);
+    __syncthreads();
+    if (kc + 1 < n_total) load_chunk(kc + 1);
+    if (!XTRA || kc < a.n_chunks) {
+#pragma unroll 3
+      for (int tap = 0; tap < TAPS; ++tap) mfma_tap(tap / KW, tap % KW, tap, W_BYTES);
+    } else {
+      mfma_tap(CTAP / KW, CTAP % KW, 0, W1_BYTES);
     }
   }
 
@@ -369,11 +364,17 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // TDF linear: per (b, t), D[m = f_out][n = c] = sum_k W[m][k] * act(x[b][t][k][c]).
-template <int BN, bool X3>
+// One workgroup covers BM = 128*MI output rows (all of M for the TDF's first Linear, so every
+// input element is normalised + GELU'd once) x BN = 64 channels; 4 waves stacked along M.
+// BK_CONTIG: the input is the transposed U^T [b][t][c][k] written by the first Linear (k
+//   contiguous -> two 16-B loads per 8 k); otherwise NHWC [b][t][k][c] (lanes walk c).
+// OUT_T: write the output transposed as U^T [b][t][c][m] (16-B stores of 4 consecutive rows).
+template <int MI, bool X3, bool BK_CONTIG, bool OUT_T>
 __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
-  constexpr int BM = kTdfBM;
-  constexpr int WM = 2, WN = 2;
-  constexpr int MI = BM / WM / 32, NI = BN / WN / 32;
+  constexpr int BN = 64;
+  constexpr int WM = 4;
+  constexpr int NI = BN / 32;
+  constexpr int BM = WM * MI * 32;
   constexpr int ROWB = kTdfBK * 2;            // 64 B per image row (32 bf16)
   constexpr int AW_BYTES = BM * ROWB;
   constexpr int B_BYTES = BN * ROWB;
@@ -386,14 +387,13 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
   float* sh = sc + kMaxCin;
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
+  const int lane = tid & 63, wm = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int mb = blockIdx.x, c0 = blockIdx.y * BN;
   const int bt = blockIdx.z;
-  const int b = bt / a.T, t = bt - b * a.T;
-  const int C = a.in.src[0].C;  // TDF input is a single source
+  const int b = bt / a.T;
   const Src src = pick_src(a.in, 0);
+  const int C = src.C;
 
   build_affine(a.in, b, sc, sh);
 
@@ -405,16 +405,15 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const float* xrow = src.ptr + ((int64_t)b * a.T + t) * a.K * C;
+  const float* xin = src.ptr + (int64_t)bt * a.K * C;  // this (b, t) slice, either layout
   const uint16_t* wblk = a.w + (int64_t)mb * a.n_chunks * (2 * AW_BYTES / 2);
 
   constexpr int N16 = (X3 ? 2 : 1) * AW_BYTES / 16;
   constexpr int W_ITEMS = (N16 + kThreads - 1) / kThreads;
   constexpr int B_ITEMS = (BN * 4 + kThreads - 1) / kThreads;
   u32x4 wreg[W_ITEMS];
-  float breg[B_ITEMS][8];
+  f32x4 breg[B_ITEMS][2];
 
-  // prefetch chunk kc into registers (issued before the previous chunk's MFMAs)
   auto load_chunk = [&](int kc) {
     const u32x4* s4 = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * (2 * AW_BYTES / 2));
     Unroll<0, W_ITEMS>::run([&](auto I) {
@@ -424,12 +423,21 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
     const int k0 = kc * kTdfBK;
     Unroll<0, B_ITEMS>::run([&](auto I) {
       const int e = tid + I * kThreads;
-      const int n = e % BN, g = e / BN;  // lanes walk channels: 256 B coalesced per k
+      const int n = e % BN, g = e / BN;
       const int c = c0 + n;
+      const int k = k0 + 8 * g;
+      const bool ok = (e < BN * 4) && c < C && k < a.K;
+      if (BK_CONTIG) {
+        // k-contiguous: K is a multiple of 8, so a group of 8 is wholly in or out
+        const f32x4* p4 = reinterpret_cast<const f32x4*>(xin + (int64_t)(ok ? c : 0) * a.K + (ok ? k : 0));
+        breg[I][0] = ok ? p4[0] : f32x4{0.f, 0.f, 0.f, 0.f};
+        breg[I][1] = ok ? p4[1] : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = k0 + 8 * g + j;
-        breg[I][j] = (e < BN * 4 && c < C && k < a.K) ? xrow[(int64_t)k * C + c] : 0.f;
+        for (int j = 0; j < 8; ++j) {
+          const bool okj = ok && k + j < a.K;
+          breg[I][j >> 2][j & 3] = okj ? xin[(int64_t)(k + j) * C + c] : 0.f;
+        }
       }
     });
   };
@@ -449,12 +457,13 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
         if (BN * 4 % kThreads != 0 && e >= BN * 4) return;
         const int n = e % BN, g = e / BN;
         const int c = c0 + n;
+        const bool ok = c < C && k0 + 8 * g < a.K;
+        const float scale = ok ? sc[c] : 1.f, shift = ok ? sh[c] : 0.f;
         __bf16 hi[8], lo[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float x = breg[I][j];
-          const int k = k0 + 8 * g + j;
-          if (src.mode == SRC_NORM_GELU && c < C && k < a.K) x = gelu_erf(x * sc[c] + sh[c]);
+          float x = breg[I][j >> 2][j & 3];
+          if (src.mode == SRC_NORM_GELU && ok && k0 + 8 * g + j < a.K) x = gelu_erf(x * scale + shift);
           split_bf16(x, hi[j], lo[j]);
         }
         const int off = n * ROWB + ((g ^ ((n >> 2) & 3)) << 4);
@@ -480,7 +489,7 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int n = (wn * NI + j) * 32 + l32;
+        const int n = j * 32 + l32;
         const int off = n * ROWB + ((q ^ ((n >> 2) & 3)) << 4);
         bh[j] = *reinterpret_cast<const bf16x8*>(Bhi + off);
         if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(Blo + off);
@@ -504,19 +513,38 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
   const int Cout = a.out.C_out;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int c = c0 + (wn * NI + j) * 32 + l32;
+    const int c = c0 + j * 32 + l32;
+    if (c >= Cout) continue;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mb * BM + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m >= a.M || c >= Cout) continue;
-        const int64_t idx = (((int64_t)b * a.T + t) * a.M + m) * Cout + c;
-        float v = acc[i][j][r];
-        if (a.out.residual) v += a.out.residual[idx];
-        a.out.ptr[idx] = v;
-        ssum[j] += v;
-        ssq[j] += v * v;
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int m0 = mb * BM + (wm * MI + i) * 32 + 8 * g4 + 4 * h;  // rows m0 .. m0+3 in regs 4*g4 ..
+        if (OUT_T) {
+          // U^T [b][t][c][m]; M is a multiple of 4 here (F / bottleneck_factor, checked on the host)
+          if (m0 >= a.M) continue;
+          f32x4 v4;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = acc[i][j][4 * g4 + q];
+            v4[q] = v;
+            ssum[j] += v;
+            ssq[j] += v * v;
+          }
+          *reinterpret_cast<f32x4*>(a.out.ptr + ((int64_t)bt * Cout + c) * a.M + m0) = v4;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int m = m0 + q;
+            if (m >= a.M) continue;
+            const int64_t idx = ((int64_t)bt * a.M + m) * Cout + c;
+            float v = acc[i][j][4 * g4 + q];
+            if (a.out.residual) v += a.out.residual[idx];
+            a.out.ptr[idx] = v;
+            ssum[j] += v;
+            ssq[j] += v * v;
+          }
+        }
       }
     }
   }
@@ -528,7 +556,7 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
       ssum[j] += __shfl_xor(ssum[j], 32);
       ssq[j] += __shfl_xor(ssq[j], 32);
       if (h == 0) {
-        const int n = (wn * NI + j) * 32 + l32;
+        const int n = j * 32 + l32;
         red[(wm * BN + n) * 2 + 0] = ssum[j];
         red[(wm * BN + n) * 2 + 1] = ssq[j];
       }
@@ -550,14 +578,14 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
   }
 }
 
-template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool UPS>
+template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool UPS, bool XTRA = false>
 int launch_conv_t(int x3, const ConvArgs& a, int batch, hipStream_t st) {
   dim3 grid((unsigned)(((a.T_out + TM - 1) / TM) * (a.F_out / kTF)), (unsigned)((a.n_cols + BN - 1) / BN),
             (unsigned)batch);
   if (x3)
-    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, true, UPS>), grid, dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, true, UPS, XTRA>), grid, dim3(kThreads), 0, st, a);
   else
-    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, false, UPS>), grid, dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, false, UPS, XTRA>), grid, dim3(kThreads), 0, st, a);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }
@@ -572,6 +600,11 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
                kMaxCin);
   switch (kind) {
     case CONV3X3:
+      if (a.x_chunks > 0) {
+        SESA_REQUIRE(a.xin.C_in % kConvBK == 0 && a.xin.C_split % kConvBK == 0, SESA_ERR_INVALID,
+                     "conv: fused shortcut C_in %d must be a multiple of %d", a.xin.C_in, kConvBK);
+        return launch_conv_t<3, 3, 1, 1, 8, 64, 4, false, true>(x3, a, batch, st);
+      }
       return launch_conv_t<3, 3, 1, 1, 8, 64, 4, false>(x3, a, batch, st);
     case CONV1X1:
       if (bn == 32) return launch_conv_t<1, 1, 1, 0, 8, 32, 4, false>(x3, a, batch, st);
@@ -585,20 +618,29 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
   return SESA_ERR_INVALID;
 }
 
-int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st) {
-  SESA_REQUIRE(a.in.C_in <= kMaxCin, SESA_ERR_INVALID, "tdf: C %d > %d", a.in.C_in, kMaxCin);
-  const int C = a.out.C_out;
-  const int bn = C <= 64 ? 64 : 128;
-  dim3 grid((unsigned)((a.M + kTdfBM - 1) / kTdfBM), (unsigned)((C + bn - 1) / bn), (unsigned)(batch * a.T));
-  if (bn == 64) {
-    if (x3) hipLaunchKernelGGL((tdf_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((tdf_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
-  } else {
-    if (x3) hipLaunchKernelGGL((tdf_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((tdf_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
-  }
+template <int MI, bool BKC, bool OT>
+int launch_tdf_t(int x3, const TdfArgs& a, int batch, hipStream_t st) {
+  constexpr int BM = 4 * MI * 32;
+  dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)((a.out.C_out + 63) / 64), (unsigned)(batch * a.T));
+  if (x3) hipLaunchKernelGGL((tdf_kernel<MI, true, BKC, OT>), grid, dim3(kThreads), 0, st, a);
+  else hipLaunchKernelGGL((tdf_kernel<MI, false, BKC, OT>), grid, dim3(kThreads), 0, st, a);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
+}
+
+int tdf_block_rows(int M) { return M > 128 ? 256 : 128; }
+
+// transposed_io: 0 = first Linear (NHWC in, U^T out), 1 = second Linear (U^T in, NHWC out)
+int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io) {
+  SESA_REQUIRE(a.in.C_in <= kMaxCin, SESA_ERR_INVALID, "tdf: C %d > %d", a.in.C_in, kMaxCin);
+  if (transposed_io == 0) {
+    SESA_REQUIRE(a.M % 4 == 0, SESA_ERR_INVALID, "tdf: M %d must be a multiple of 4", a.M);
+    return tdf_block_rows(a.M) == 256 ? launch_tdf_t<2, false, true>(x3, a, batch, st)
+                                      : launch_tdf_t<1, false, true>(x3, a, batch, st);
+  }
+  SESA_REQUIRE(a.K % 8 == 0, SESA_ERR_INVALID, "tdf: K %d must be a multiple of 8", a.K);
+  return tdf_block_rows(a.M) == 256 ? launch_tdf_t<2, true, false>(x3, a, batch, st)
+                                    : launch_tdf_t<1, true, false>(x3, a, batch, st);
 }
 
 }  // namespace sesa

@@ -45,12 +45,14 @@ struct ConvArgs {
   int T_in, F_in, T_out, F_out;
   int n_cols;                // GEMM N (C_out, or 4*C_out for the transposed 2x2 conv)
   int n_chunks;              // C_in / 16
+  GemmIn xin;                // optional RAW extra input over the centre tap (fused 1x1 shortcut)
+  int x_chunks;              // xin.C_in / 16 (0 = none)
 };
 
 struct TdfArgs {
   GemmIn in;
   GemmOut out;
-  const uint16_t* w;         // packed [M/BM][K/32][BM][32] hi, lo
+  const uint16_t* w;         // packed [M/BM][K/32][BM][32] hi, lo (BM = tdf_block_rows(M))
   int T, K, M;               // F_in = K, F_out = M
   int n_chunks;              // ceil(K / 32)
 };
@@ -59,13 +61,12 @@ struct TdfArgs {
 enum ConvKind : int { CONV3X3 = 0, CONV1X1 = 1, CONV2X2S2 = 2, DECONV2X2S2 = 3 };
 
 int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStream_t st);
-int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st);
+int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io);
+int tdf_block_rows(int M);  // BM chosen for a TDF Linear with M output rows (weights packed to match)
 
 // Tile geometry shared by the host packer and the kernels.
 constexpr int kTF = 32;       // output columns per tile (one MFMA 32-row block = one tile row)
 constexpr int kConvBK = 16;   // input channels per K chunk of the tap GEMM
-constexpr int kTdfBM = 128;   // TDF output rows (frequency) per tile
-constexpr int kTdfBN = 128;   // TDF output channels per tile
 constexpr int kTdfBK = 32;    // TDF K (frequency) per chunk
 
 }  // namespace sesa

@@ -162,3 +162,16 @@ def test_demix_matches_reference(dev, path):
     for k in ("vocals", "other"):
         assert out[k].shape == g[k].shape
         assert rms(out[k], g[k]) <= RMS_GATE, k
+
+
+def test_sharded_path_single_rank_matches_demix(dev):
+    """bench.py's step (sesa/parallel.py at world 1) equals the plain device demix bit-for-bit."""
+    from sesa.demix import demix_device
+    from sesa.parallel import demix_sharded
+    m, c = _model("config_mdx23c_small.yaml", "random")
+    rng = np.random.default_rng(1)
+    mix = torch.from_numpy((0.1 * rng.standard_normal((2, 300000))).astype(np.float32)).to(dev)
+    with contextlib.redirect_stdout(io.StringIO()):
+        a = demix_device(c, m, mix, dev, exec_batch=4)
+    b = demix_sharded(c, m, mix, dev, rank=0, world=1, exec_batch=4)
+    assert torch.equal(a, b)

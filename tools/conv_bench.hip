@@ -41,11 +41,15 @@ int main(int argc, char** argv) {
   struct Shape { int T, F, Cin, Cout, kind; };
   Shape shapes[] = {{256, 1024, 128, 128, CONV3X3}, {128, 512, 256, 256, CONV3X3}, {64, 256, 384, 384, CONV3X3},
                     {32, 128, 512, 512, CONV3X3}, {16, 64, 640, 640, CONV3X3},  {256, 1024, 128, 128, CONV1X1},
-                    {256, 1024, 256, 128, CONV1X1}, {128, 512, 128, 256, CONV2X2S2}, {128, 512, 256, 128, DECONV2X2S2}};
+                    {256, 1024, 256, 128, CONV1X1}, {128, 512, 128, 256, CONV2X2S2}, {128, 512, 256, 128, DECONV2X2S2},
+                    {256, 1024, 128, 128, 100 + CONV3X3}};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (auto& s : shapes) {
+  for (auto& s0 : shapes) {
+    Shape s = s0;
+    const bool xtra = s.kind >= 100;  // conv3x3 with the block input fused as a 1x1 shortcut (extra K)
+    if (xtra) s.kind -= 100;
     const bool ups = s.kind == DECONV2X2S2;
     const int taps = s.kind == CONV3X3 ? 9 : (s.kind == CONV2X2S2 ? 4 : 1);
     const int Tin = s.T, Fin = s.F;
@@ -63,7 +67,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(st_in, hs.data(), hs.size() * 8, hipMemcpyHostToDevice));
     float* gam = dalloc<float>(s.Cin, 1.f);
     float* bet = dalloc<float>(s.Cin, 0.2f);
-    size_t wn = (size_t)((ncols + bn - 1) / bn) * (s.Cin / 16) * 2 * taps * bn * 16;
+    size_t wn = (size_t)((ncols + bn - 1) / bn) * ((s.Cin / 16) * 2 * taps * bn * 16 + (xtra ? (s.Cin / 16) * 2 * bn * 16 : 0));
     uint16_t* w = dalloc<uint16_t>(wn);
     ConvArgs a{};
     a.in.src[0] = Src{x, st_in, nullptr, s.Cin, SRC_NORM_GELU};
@@ -81,6 +85,12 @@ int main(int argc, char** argv) {
     a.F_out = ups ? Fin : Fout;
     a.n_cols = ncols;
     a.n_chunks = s.Cin / 16;
+    if (xtra) {
+      a.xin = a.in;
+      a.xin.src[0].mode = SRC_RAW;
+      a.xin.src[1].mode = SRC_RAW;
+      a.x_chunks = s.Cin / 16;
+    }
     for (int it = 0; it < 2; ++it)
       if (launch_conv(s.kind, bn, x3, a, B, 0)) { printf("launch failed: %s\n", sesa_last_error()); return 1; }
     CK(hipDeviceSynchronize());
@@ -92,8 +102,8 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ms /= iters;
-    const double flop = 2.0 * B * (double)(ups ? Tin * Fin : Tout * Fout) * ncols * s.Cin * taps;
-    printf("kind %d T%4d F%5d Cin%4d Cout%4d B%2d x3=%d: %8.3f ms  %7.1f TF alg  (%.1f%% of %s peak)\n", s.kind, s.T, s.F,
+    const double flop = 2.0 * B * (double)(ups ? Tin * Fin : Tout * Fout) * ncols * (s.Cin * taps + (xtra ? s.Cin : 0));
+    printf("kind %d%s T%4d F%5d Cin%4d Cout%4d B%2d x3=%d: %8.3f ms  %7.1f TF alg  (%.1f%% of %s peak)\n", s.kind, xtra ? "+sc" : "", s.T, s.F,
            s.Cin, s.Cout, B, x3, ms, flop / ms / 1e9, 100 * flop / ms / 1e9 / (x3 ? 833.3 : 2500.0),
            x3 ? "bf16x3" : "bf16");
     CK(hipFree(x)); CK(hipFree(y)); CK(hipFree(st_in)); CK(hipFree(st_out)); CK(hipFree(gam)); CK(hipFree(bet));
@@ -103,13 +113,17 @@ int main(int argc, char** argv) {
   struct TShape { int T, K, M, C; };
   TShape ts[] = {{256, 1024, 256, 128}, {256, 256, 1024, 128}, {128, 512, 128, 256}, {128, 128, 512, 256},
                  {32, 128, 32, 512}};
+  int tio[] = {0, 1, 0, 1, 0};
+  int ti = 0;
   for (auto& s : ts) {
+    const int io = tio[ti++];
     size_t in_n = (size_t)B * s.T * s.K * s.C, out_n = (size_t)B * s.T * s.M * s.C;
     float* x = dalloc<float>(in_n, 2.f);
     float* y = dalloc<float>(out_n);
     double* st_in = dalloc<double>((size_t)B * s.C * 2);
     double* st_out = dalloc<double>((size_t)B * s.C * 2);
-    size_t wn = (size_t)((s.M + 127) / 128) * ((s.K + 31) / 32) * 2 * 128 * 32;
+    const int BM = tdf_block_rows(s.M);
+    size_t wn = (size_t)((s.M + BM - 1) / BM) * ((s.K + 31) / 32) * 2 * BM * 32;
     uint16_t* w = dalloc<uint16_t>(wn);
     TdfArgs a{};
     a.in.src[0] = Src{x, st_in, nullptr, s.C, SRC_NORM_GELU};
@@ -123,18 +137,18 @@ int main(int argc, char** argv) {
     a.K = s.K;
     a.M = s.M;
     a.n_chunks = (s.K + 31) / 32;
-    for (int it = 0; it < 2; ++it) launch_tdf(x3, a, B, 0);
+    for (int it = 0; it < 2; ++it) launch_tdf(x3, a, B, 0, io);
     CK(hipDeviceSynchronize());
     const int iters = 5;
     CK(hipEventRecord(e0, 0));
-    for (int it = 0; it < iters; ++it) launch_tdf(x3, a, B, 0);
+    for (int it = 0; it < iters; ++it) launch_tdf(x3, a, B, 0, io);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ms /= iters;
     const double flop = 2.0 * B * (double)s.T * s.M * s.K * s.C;
-    printf("tdf T%4d K%5d M%5d C%4d B%2d x3=%d: %8.3f ms  %7.1f TF alg (%.1f%%)\n", s.T, s.K, s.M, s.C, B, x3, ms,
+    printf("tdf%d T%4d K%5d M%5d C%4d B%2d x3=%d: %8.3f ms  %7.1f TF alg (%.1f%%)\n", io, s.T, s.K, s.M, s.C, B, x3, ms,
            flop / ms / 1e9, 100 * flop / ms / 1e9 / (x3 ? 833.3 : 2500.0));
     CK(hipFree(x)); CK(hipFree(y)); CK(hipFree(st_in)); CK(hipFree(st_out)); CK(hipFree(w));
   }
