@@ -132,7 +132,8 @@ int sesa_mdx23c_destroy(sesa_mdx23c* m);
 #define SESA_KCLASS_TDF 4
 #define SESA_KCLASS_STFT 5
 #define SESA_KCLASS_ISTFT 6
-#define SESA_KCLASS_COUNT 7
+#define SESA_KCLASS_ACT 7     /* act_split: norm + GELU + bf16 split pass (work = HBM bytes) */
+#define SESA_KCLASS_COUNT 8
 int sesa_profile_enable(int enable);   /* 1: start recording (clears previous records), 0: stop */
 int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work);
 

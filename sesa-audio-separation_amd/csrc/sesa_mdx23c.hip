@@ -337,6 +337,28 @@ struct Fwd {
     profile_end(tok, st, SESA_KCLASS_TDF, 2.0 * B * T * (double)w.M * w.K * C);
   }
 
+  // One act_split pass: GELU(InstanceNorm_affine(a [++ b])) -> bf16 hi/lo planes, returned as the
+  // single pre-activated source its convolution consumes.
+  GemmIn act(Tensor a, Tensor b, const Norm* nrm, int T, int F) {
+    const int C = a.C + (b.p ? b.C : 0);
+    const int64_t n = (int64_t)B * T * F * C;
+    uint16_t* hi = reinterpret_cast<uint16_t*>(buf((n + 1) / 2));
+    uint16_t* lo = reinterpret_cast<uint16_t*>(buf((n + 1) / 2));
+    const GemmIn src = input(a, b, SRC_NORM_GELU, SRC_NORM_GELU, nrm, T, F);
+    if (!dry && !rc) {
+      void* tok = profile_begin(st);
+      rc = launch_act_split(src, (int64_t)T * F, B, hi, lo, st);
+      profile_end(tok, st, SESA_KCLASS_ACT, 8.0 * n);
+    }
+    GemmIn in{};
+    in.src[0] = Src{nullptr, nullptr, nullptr, C, SRC_PRE, hi, lo};
+    in.src[1] = in.src[0];
+    in.C_split = C;
+    in.C_in = C;
+    in.inv_count = src.inv_count;
+    return in;
+  }
+
   // TFC_TDF.forward (mdx23c_tfc_tdf_v3.py:131-138)
   Tensor stack(const Stack& s, Tensor x0, Tensor x1, const Level& L) {
     const int bnf = m->cfg.bottleneck_factor;
@@ -352,8 +374,7 @@ struct Fwd {
       double* st_h2 = stats(c);
       double* st_out = stats(c);
       // x = tfc1(x)
-      conv(bk.conv1, input(x0, x1, SRC_NORM_GELU, SRC_NORM_GELU, &bk.tfc1, L.T, L.F), L.T, L.F, L.T, L.F, H, nullptr,
-           st_h1, 0);
+      conv(bk.conv1, act(x0, x1, &bk.tfc1, L.T, L.F), L.T, L.F, L.T, L.F, H, nullptr, st_h1, 0);
       // x = x + tdf(x)
       tdf(bk.lin1, input(Tensor{H, st_h1, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf0, L.T, L.F), L.T, U, nullptr, st_u,
           c, 0);
@@ -361,8 +382,8 @@ struct Fwd {
           c, 1);
       // x = tfc2(x) + shortcut(block input): the 1x1 shortcut rides along as extra K (raw input)
       const GemmIn xs = input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F);
-      conv(bk.conv2, input(Tensor{H, st_h2, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tfc2, L.T, L.F), L.T, L.F, L.T, L.F, S,
-           nullptr, st_out, 0, &xs);
+      conv(bk.conv2, act(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F), L.T, L.F, L.T, L.F, S, nullptr, st_out, 0,
+           &xs);
       x0 = Tensor{S, st_out, c};
       x1 = Tensor{};
     }
@@ -390,8 +411,7 @@ struct Fwd {
       Tensor y = stack(m->enc[l], xt, Tensor{}, L);
       skips.push_back(y);
       Tensor d{buf((int64_t)B * L1.T * L1.F * L1.c), stats(L1.c), L1.c};
-      conv(m->down[l], input(y, Tensor{}, SRC_NORM_GELU, 0, &m->down_norm[l], L.T, L.F), L.T, L.F, L1.T, L1.F, d.p,
-           nullptr, d.st, 0);
+      conv(m->down[l], act(y, Tensor{}, &m->down_norm[l], L.T, L.F), L.T, L.F, L1.T, L1.F, d.p, nullptr, d.st, 0);
       xt = d;
     }
     xt = stack(m->bottleneck, xt, Tensor{}, m->lv[n]);
@@ -401,8 +421,7 @@ struct Fwd {
       const Level& L1 = m->lv[l + 1];
       Tensor upt{buf((int64_t)B * L.T * L.F * L.c), stats(L.c), L.c};
       // Upscale: GEMM over the level-(l+1) positions, N = 4*c_l, scattered to 2x2 outputs
-      conv(m->up[i], input(xt, Tensor{}, SRC_NORM_GELU, 0, &m->up_norm[i], L1.T, L1.F), L1.T, L1.F, L1.T, L1.F, upt.p,
-           nullptr, upt.st, 0);
+      conv(m->up[i], act(xt, Tensor{}, &m->up_norm[i], L1.T, L1.F), L1.T, L1.F, L1.T, L1.F, upt.p, nullptr, upt.st, 0);
       xt = stack(m->dec[i], upt, skips[l], L);
     }
     // x = x * first_conv_out; x = final_conv(cat([mix, x]))

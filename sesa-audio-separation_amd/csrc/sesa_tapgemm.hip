@@ -69,6 +69,8 @@ __device__ __forceinline__ Src pick_src(const GemmIn& in, int s) {
   r.mul = s ? in.src[1].mul : in.src[0].mul;
   r.C = s ? in.src[1].C : in.src[0].C;
   r.mode = s ? in.src[1].mode : in.src[0].mode;
+  r.hi = s ? in.src[1].hi : in.src[0].hi;
+  r.lo = s ? in.src[1].lo : in.src[0].lo;
   return r;
 }
 
@@ -111,7 +113,7 @@ __device__ __forceinline__ void transform4(float (&v)[4], int mode, const float*
 // all KH*KW taps, then x_chunks chunks of an optional RAW extra input over the centre tap only --
 // the 1x1 shortcut of TFC_TDF (mdx23c_tfc_tdf_v3.py:126, :132, :137) fused into tfc2's conv as
 // extra K, so `s` never round-trips through HBM.
-template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool X3, bool UPS, bool XTRA>
+template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool X3, bool UPS, bool XTRA, bool PRE>
 __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int MI = TM / WM;                 // 32-position MFMA row blocks per wave
@@ -139,10 +141,30 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int l32 = lane & 31, h = lane >> 5;
 
+  // XCD-aware block order (1-D grid over tiles x output-channel blocks): the NB channel blocks of a
+  // spatial tile get ids 8 apart inside a window of 8*NB consecutive ids, so they run at the same
+  // time on the SAME XCD and its L2 serves the shared input halo (the dispatcher deals ids
+  // round-robin over the 8 XCDs; speed only, never correctness).  Requires n_tiles % 8 == 0 for the
+  // full grouping; the tail falls back to the plain order.
   const int tiles_f = a.F_out / kTF;
-  const int t0 = (blockIdx.x / tiles_f) * TM;
-  const int f0 = (blockIdx.x % tiles_f) * kTF;
-  const int nb = blockIdx.y;
+  const int NB = (a.n_cols + BN - 1) / BN;
+  const int n_tiles = ((a.T_out + TM - 1) / TM) * tiles_f;
+  int tile, nb;
+  {
+    const int id = blockIdx.x;
+    const int full = (n_tiles / 8) * 8 * NB;
+    if (id < full) {
+      const int g = id / (8 * NB), r = id - g * 8 * NB;
+      tile = g * 8 + (r & 7);
+      nb = r >> 3;
+    } else {
+      const int r = id - full;
+      tile = (n_tiles / 8) * 8 + r / NB;
+      nb = r % NB;
+    }
+  }
+  const int t0 = (tile / tiles_f) * TM;
+  const int f0 = (tile % tiles_f) * kTF;
   const int b = blockIdx.z;
   const int t_in0 = t0 * S - PAD, f_in0 = f0 * S - PAD;
   const int n_total = a.n_chunks + (XTRA ? a.x_chunks : 0);
@@ -194,6 +216,28 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
       wreg[I] = wsrc[e < w16 ? e : w16 - 1];  // unconditional (clamped) so wreg stays in VGPRs
     });
     avalid = 0;
+    if (PRE && !ext) {
+      // pre-activated planes: item = (position, 8-channel half): 16 B of hi + 16 B of lo
+      constexpr int P_ITEMS = (NPOS * 2 + kThreads - 1) / kThreads;
+      static_assert(2 * P_ITEMS <= A_ITEMS, "PRE staging registers");
+      Unroll<0, P_ITEMS>::run([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const int e = tid + i * kThreads;
+        const int p = e >> 1, hf = e & 1;
+        const int hr = p / HW, hc = p - hr * HW;
+        const int ti = t_in0 + hr, fi = f_in0 + hc;
+        const bool ok = (e < NPOS * 2) && ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in;
+        if (ok) {
+          const int64_t idx = (((int64_t)b * a.T_in + ti) * a.F_in + fi) * src.C + cl0 + 8 * hf;
+          areg[2 * i] = *reinterpret_cast<const f32x4*>(src.hi + idx);
+          areg[2 * i + 1] = *reinterpret_cast<const f32x4*>(src.lo + idx);
+        } else {
+          areg[2 * i] = f32x4{0.f, 0.f, 0.f, 0.f};
+          areg[2 * i + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      });
+      return;
+    }
     Unroll<0, A_ITEMS>::run([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int e = tid + i * kThreads;
@@ -222,11 +266,25 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
       const int e = tid + I * kThreads;
       if (e < w16) wdst[e] = wreg[I];
     });
+    if (PRE && !ext) {  // straight copies (zeros for out-of-bounds positions are already in areg)
+      constexpr int P_ITEMS = (NPOS * 2 + kThreads - 1) / kThreads;
+      Unroll<0, P_ITEMS>::run([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const int e = tid + i * kThreads;
+        if (NPOS * 2 % kThreads != 0 && e >= NPOS * 2) return;
+        const int p = e >> 1, hf = e & 1;
+        const int off = p * 32 + ((hf ^ ((p >> 3) & 1)) << 4);
+        *reinterpret_cast<f32x4*>(A_hi + off) = areg[2 * i];
+        if (X3) *reinterpret_cast<f32x4*>(A_lo + off) = areg[2 * i + 1];
+      });
+      return;
+    }
     Unroll<0, A_ITEMS>::run([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int e = tid + i * kThreads;
       if (NPOS * 4 % kThreads != 0 && e >= NPOS * 4) return;
       const int p = e >> 2, g = e & 3;
+      const int off = p * 32 + ((((g >> 1) ^ ((p >> 3) & 1))) << 4) + ((g & 1) << 3);
       float v[4] = {areg[i][0], areg[i][1], areg[i][2], areg[i][3]};
       if (!ext && (avalid & (1u << i))) {
         const float* mulp = nullptr;
@@ -240,7 +298,6 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
       __bf16 hi[4], lo[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) split_bf16(v[q], hi[q], lo[q]);
-      const int off = p * 32 + ((((g >> 1) ^ ((p >> 3) & 1))) << 4) + ((g & 1) << 3);
       *reinterpret_cast<uint2*>(A_hi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
       if (X3) *reinterpret_cast<uint2*>(A_lo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
     });
@@ -283,7 +340,8 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
     __syncthreads();
     if (kc + 1 < n_total) load_chunk(kc + 1);
     if (!XTRA || kc < a.n_chunks) {
-#pragma unroll 3
+      constexpr int TU = XTRA ? 3 : TAPS;  // the fused-shortcut variant needs the registers
+#pragma unroll TU
       for (int tap = 0; tap < TAPS; ++tap) mfma_tap(tap / KW, tap % KW, tap, W_BYTES);
     } else {
       mfma_tap(CTAP / KW, CTAP % KW, 0, W1_BYTES);
@@ -578,14 +636,58 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
   }
 }
 
-template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool UPS, bool XTRA = false>
+
+// ---------------------------------------------------------------------------------------------
+// act_split: one pass over a normalised tensor, writing the bf16 hi/lo operand planes of its
+// consumer (InstanceNorm affine + exact GELU applied once per element instead of once per
+// consuming tile).  HBM-bound: reads 4 B, writes 2 + 2 B per element.
+__global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t n_pos, int pos_per_block,
+                                                             uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+  __shared__ float sc[kMaxCin], sh[kMaxCin];
+  const int b = blockIdx.y;
+  build_affine(in, b, sc, sh);
+  __syncthreads();
+  const int C = in.C_in;
+  const int groups = C / 8;  // 8 channels per thread-item (C % 16 == 0)
+  const int64_t p0 = (int64_t)blockIdx.x * pos_per_block;
+  const int64_t np = (n_pos - p0) < pos_per_block ? (n_pos - p0) : pos_per_block;
+  const int64_t items = np * groups;
+  for (int64_t e = threadIdx.x; e < items; e += kThreads) {
+    const int64_t p = p0 + e / groups;
+    const int c = (int)(e % groups) * 8;
+    const int s = c < in.C_split ? 0 : 1;
+    const Src src = pick_src(in, s);
+    const int cl = c - (s ? in.C_split : 0);
+    const f32x4* xp = reinterpret_cast<const f32x4*>(src.ptr + ((int64_t)b * n_pos + p) * src.C + cl);
+    const f32x4 x0 = xp[0], x1 = xp[1];
+    float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    __bf16 h8[8], l8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float y = src.mode == SRC_NORM_GELU ? gelu_erf(v[q] * sc[c + q] + sh[c + q]) : v[q];
+      split_bf16(y, h8[q], l8[q]);
+    }
+    const int64_t o = ((int64_t)b * n_pos + p) * C + c;
+    *reinterpret_cast<uint4*>(hi + o) =
+        make_uint4(pack2(h8[0], h8[1]), pack2(h8[2], h8[3]), pack2(h8[4], h8[5]), pack2(h8[6], h8[7]));
+    *reinterpret_cast<uint4*>(lo + o) =
+        make_uint4(pack2(l8[0], l8[1]), pack2(l8[2], l8[3]), pack2(l8[4], l8[5]), pack2(l8[6], l8[7]));
+  }
+}
+
+template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool UPS, bool XTRA, bool PRE>
 int launch_conv_t(int x3, const ConvArgs& a, int batch, hipStream_t st) {
-  dim3 grid((unsigned)(((a.T_out + TM - 1) / TM) * (a.F_out / kTF)), (unsigned)((a.n_cols + BN - 1) / BN),
+  // PRE kernels read only the bf16 planes of the main input
+  SESA_REQUIRE(!PRE || (a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && a.in.src[0].lo && a.in.C_split == a.in.C_in),
+               SESA_ERR_INVALID, "conv: this kernel needs a single pre-activated (act_split) input");
+  SESA_REQUIRE(PRE || (a.in.src[0].mode != SRC_PRE && a.in.src[1].mode != SRC_PRE), SESA_ERR_INVALID,
+               "conv: pre-activated input given to a transforming kernel");
+  dim3 grid((unsigned)(((a.T_out + TM - 1) / TM) * (a.F_out / kTF) * ((a.n_cols + BN - 1) / BN)), 1u,
             (unsigned)batch);
   if (x3)
-    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, true, UPS, XTRA>), grid, dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, true, UPS, XTRA, PRE>), grid, dim3(kThreads), 0, st, a);
   else
-    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, false, UPS, XTRA>), grid, dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, false, UPS, XTRA, PRE>), grid, dim3(kThreads), 0, st, a);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }
@@ -603,16 +705,16 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
       if (a.x_chunks > 0) {
         SESA_REQUIRE(a.xin.C_in % kConvBK == 0 && a.xin.C_split % kConvBK == 0, SESA_ERR_INVALID,
                      "conv: fused shortcut C_in %d must be a multiple of %d", a.xin.C_in, kConvBK);
-        return launch_conv_t<3, 3, 1, 1, 8, 64, 4, false, true>(x3, a, batch, st);
+        return launch_conv_t<3, 3, 1, 1, 8, 64, 4, false, true, true>(x3, a, batch, st);
       }
-      return launch_conv_t<3, 3, 1, 1, 8, 64, 4, false>(x3, a, batch, st);
+      return launch_conv_t<3, 3, 1, 1, 8, 64, 4, false, false, true>(x3, a, batch, st);
     case CONV1X1:
-      if (bn == 32) return launch_conv_t<1, 1, 1, 0, 8, 32, 4, false>(x3, a, batch, st);
-      return launch_conv_t<1, 1, 1, 0, 8, 64, 4, false>(x3, a, batch, st);
+      if (bn == 32) return launch_conv_t<1, 1, 1, 0, 8, 32, 4, false, false, false>(x3, a, batch, st);
+      return launch_conv_t<1, 1, 1, 0, 8, 64, 4, false, false, false>(x3, a, batch, st);
     case CONV2X2S2:
-      return launch_conv_t<2, 2, 2, 0, 4, 64, 4, false>(x3, a, batch, st);
+      return launch_conv_t<2, 2, 2, 0, 4, 64, 4, false, false, true>(x3, a, batch, st);
     case DECONV2X2S2:
-      return launch_conv_t<1, 1, 1, 0, 8, 64, 4, true>(x3, a, batch, st);
+      return launch_conv_t<1, 1, 1, 0, 8, 64, 4, true, false, true>(x3, a, batch, st);
   }
   set_error("conv: unknown kind %d", kind);
   return SESA_ERR_INVALID;
@@ -629,6 +731,16 @@ int launch_tdf_t(int x3, const TdfArgs& a, int batch, hipStream_t st) {
 }
 
 int tdf_block_rows(int M) { return M > 128 ? 256 : 128; }
+
+int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st) {
+  SESA_REQUIRE(in.C_in % 16 == 0 && in.C_split % 8 == 0 && in.C_in <= kMaxCin, SESA_ERR_INVALID,
+               "act_split: C %d must be a multiple of 16 (<= %d)", in.C_in, kMaxCin);
+  const int ppb = (int)((16384 + in.C_in - 1) / in.C_in);  // ~16K elements per block
+  dim3 grid((unsigned)((n_pos + ppb - 1) / ppb), (unsigned)batch);
+  hipLaunchKernelGGL(act_split_kernel, grid, dim3(kThreads), 0, st, in, n_pos, ppb, hi, lo);
+  SESA_CHECK_LAUNCH();
+  return SESA_OK;
+}
 
 // transposed_io: 0 = first Linear (NHWC in, U^T out), 1 = second Linear (U^T in, NHWC out)
 int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io) {

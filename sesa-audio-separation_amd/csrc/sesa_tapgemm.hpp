@@ -9,6 +9,7 @@ enum SrcMode : int {
   SRC_RAW = 0,        // x
   SRC_NORM_GELU = 1,  // GELU(InstanceNorm_affine(x))   (get_norm + get_act, mdx23c_tfc_tdf_v3.py:47-71)
   SRC_MUL = 2,        // x * mul                         (x * first_conv_out, :230)
+  SRC_PRE = 3,        // pre-activated: bf16 hi/lo planes written by act_split (GELU(IN(x)) already applied)
 };
 
 // One input source of a (possibly channel-concatenated) NHWC fp32 activation
@@ -19,6 +20,8 @@ struct Src {
   const float* mul;     // same layout as ptr, for SRC_MUL
   int C;
   int mode;
+  const uint16_t* hi;   // SRC_PRE: bf16 planes, NHWC like ptr
+  const uint16_t* lo;
 };
 
 struct GemmIn {
@@ -61,6 +64,9 @@ struct TdfArgs {
 enum ConvKind : int { CONV3X3 = 0, CONV1X1 = 1, CONV2X2S2 = 2, DECONV2X2S2 = 3 };
 
 int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStream_t st);
+// act_split: hi/lo[b][pos][c] = split_bf16(GELU(IN_affine(x))) for the (possibly two-source,
+// channel-concatenated) input `in` of n_pos positions per batch item.
+int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st);
 int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io);
 int tdf_block_rows(int M);  // BM chosen for a TDF Linear with M output rows (weights packed to match)
 

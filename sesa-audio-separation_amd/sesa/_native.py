@@ -45,7 +45,7 @@ SIGNATURES = {
                                   ctypes.POINTER(ctypes.c_double)]),
 }
 
-KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6}
+KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6, "act": 7}
 
 
 def profile_enable(on):

@@ -6,6 +6,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "sesa_common.hpp"
@@ -32,6 +33,21 @@ T* dalloc(size_t n, float fill_scale = 0.f) {
     for (size_t i = 0; i < n; ++i) h[i] = (T)(fill_scale * ((rand() / (float)RAND_MAX) - 0.5f));
     CK(hipMemcpy(p, h.data(), n * sizeof(T), hipMemcpyHostToDevice));
   }
+  return p;
+}
+
+// random bf16 bit patterns in +-0.05 (non-zero operands: zero MFMA operands raise the clock)
+uint16_t* dalloc_bf16(size_t n) {
+  std::vector<uint16_t> h(n);
+  for (size_t i = 0; i < n; ++i) {
+    float f = 0.1f * ((rand() / (float)RAND_MAX) - 0.5f);
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    h[i] = (uint16_t)(u >> 16);
+  }
+  uint16_t* p;
+  CK(hipMalloc(&p, n * 2));
+  CK(hipMemcpy(p, h.data(), n * 2, hipMemcpyHostToDevice));
   return p;
 }
 
@@ -68,9 +84,12 @@ int main(int argc, char** argv) {
     float* gam = dalloc<float>(s.Cin, 1.f);
     float* bet = dalloc<float>(s.Cin, 0.2f);
     size_t wn = (size_t)((ncols + bn - 1) / bn) * ((s.Cin / 16) * 2 * taps * bn * 16 + (xtra ? (s.Cin / 16) * 2 * bn * 16 : 0));
-    uint16_t* w = dalloc<uint16_t>(wn);
+    uint16_t* w = dalloc_bf16(wn);
+    const bool pre = s.kind != CONV1X1;
+    uint16_t* xh = pre ? dalloc_bf16(in_n) : nullptr;
+    uint16_t* xl = pre ? dalloc_bf16(in_n) : nullptr;
     ConvArgs a{};
-    a.in.src[0] = Src{x, st_in, nullptr, s.Cin, SRC_NORM_GELU};
+    a.in.src[0] = pre ? Src{x, st_in, nullptr, s.Cin, SRC_PRE, xh, xl} : Src{x, st_in, nullptr, s.Cin, SRC_NORM_GELU};
     a.in.src[1] = a.in.src[0];
     a.in.C_split = s.Cin;
     a.in.C_in = s.Cin;
@@ -87,8 +106,8 @@ int main(int argc, char** argv) {
     a.n_chunks = s.Cin / 16;
     if (xtra) {
       a.xin = a.in;
-      a.xin.src[0].mode = SRC_RAW;
-      a.xin.src[1].mode = SRC_RAW;
+      a.xin.src[0] = Src{x, nullptr, nullptr, s.Cin, SRC_RAW};
+      a.xin.src[1] = a.xin.src[0];
       a.x_chunks = s.Cin / 16;
     }
     for (int it = 0; it < 2; ++it)
@@ -108,6 +127,36 @@ int main(int argc, char** argv) {
            x3 ? "bf16x3" : "bf16");
     CK(hipFree(x)); CK(hipFree(y)); CK(hipFree(st_in)); CK(hipFree(st_out)); CK(hipFree(gam)); CK(hipFree(bet));
     CK(hipFree(w));
+    if (pre) { CK(hipFree(xh)); CK(hipFree(xl)); }
+  }
+  {  // act_split over a level-0 tensor
+    const int64_t npos = 256 * 1024;
+    const int C = 128;
+    float* x = dalloc<float>((size_t)B * npos * C, 2.f);
+    double* st_in = dalloc<double>((size_t)B * C * 2);
+    std::vector<double> hs((size_t)B * C * 2);
+    for (size_t i = 0; i < hs.size(); i += 2) { hs[i] = 0.0; hs[i + 1] = (double)npos * 0.33; }
+    CK(hipMemcpy(st_in, hs.data(), hs.size() * 8, hipMemcpyHostToDevice));
+    uint16_t *hi, *lo;
+    CK(hipMalloc(&hi, (size_t)B * npos * C * 2));
+    CK(hipMalloc(&lo, (size_t)B * npos * C * 2));
+    GemmIn in{};
+    in.src[0] = Src{x, st_in, nullptr, C, SRC_NORM_GELU};
+    in.src[1] = in.src[0];
+    in.C_split = C;
+    in.C_in = C;
+    in.inv_count = 1.0 / npos;
+    launch_act_split(in, npos, B, hi, lo, 0);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0, 0));
+    for (int it = 0; it < 5; ++it) launch_act_split(in, npos, B, hi, lo, 0);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= 5;
+    printf("act_split T 256 F 1024 C 128 B%2d: %8.3f ms  %7.1f GB/s (8 B/elem)\n", B, ms, 8.0 * B * npos * C / ms / 1e6);
+    CK(hipFree(x)); CK(hipFree(st_in)); CK(hipFree(hi)); CK(hipFree(lo));
   }
   // TDF
   struct TShape { int T, K, M, C; };
@@ -124,7 +173,7 @@ int main(int argc, char** argv) {
     double* st_out = dalloc<double>((size_t)B * s.C * 2);
     const int BM = tdf_block_rows(s.M);
     size_t wn = (size_t)((s.M + BM - 1) / BM) * ((s.K + 31) / 32) * 2 * BM * 32;
-    uint16_t* w = dalloc<uint16_t>(wn);
+    uint16_t* w = dalloc_bf16(wn);
     TdfArgs a{};
     a.in.src[0] = Src{x, st_in, nullptr, s.C, SRC_NORM_GELU};
     a.in.src[1] = a.in.src[0];
