@@ -269,14 +269,24 @@ struct Fwd {
   size_t stats_cap = 0;
   int rc = SESA_OK;
 
+  size_t float_cap = 0;  // real run: bytes planned by the dry run (guards against plan drift)
+
   float* buf(int64_t nfloat) {
     float* p = dry ? nullptr : reinterpret_cast<float*>(ws + off);
     off += ((size_t)nfloat * 4 + 255) & ~(size_t)255;
+    if (!dry && off > float_cap && !rc) {
+      set_error("mdx23c forward: workspace plan overflow (%zu > %zu)", off, float_cap);
+      rc = SESA_ERR_STATE;  // every later launch is skipped
+    }
     return p;
   }
   double* stats(int C) {
     double* p = dry ? nullptr : reinterpret_cast<double*>(stats_base + stats_off);
     stats_off += (((size_t)B * C * 2 * 8) + 255) & ~(size_t)255;
+    if (!dry && stats_off > stats_cap && !rc) {
+      set_error("mdx23c forward: stats plan overflow (%zu > %zu)", stats_off, stats_cap);
+      rc = SESA_ERR_STATE;
+    }
     return p;
   }
   const float* aff(int64_t off_f) const { return m->d_affine + off_f; }
@@ -284,9 +294,9 @@ struct Fwd {
   GemmIn input(Tensor a, Tensor b, int mode_a, int mode_b, const Norm* nrm, int T, int F) const {
     GemmIn in{};
     in.src[0] = Src{a.p, a.st, nullptr, a.C, mode_a};
-    in.src[1] = b.p ? Src{b.p, b.st, nullptr, b.C, mode_b} : Src{a.p, a.st, nullptr, a.C, mode_a};
+    in.src[1] = b.C > 0 ? Src{b.p, b.st, nullptr, b.C, mode_b} : Src{a.p, a.st, nullptr, a.C, mode_a};
     in.C_split = a.C;
-    in.C_in = a.C + (b.p ? b.C : 0);
+    in.C_in = a.C + (b.C > 0 ? b.C : 0);  // (not b.p: pointers are null in the sizing dry run)
     in.gamma = nrm ? aff(nrm->off_g) : nullptr;
     in.beta = nrm ? aff(nrm->off_b) : nullptr;
     in.inv_count = 1.0 / ((double)T * (double)F);
@@ -340,7 +350,7 @@ struct Fwd {
   // One act_split pass: GELU(InstanceNorm_affine(a [++ b])) -> bf16 hi/lo planes, returned as the
   // single pre-activated source its convolution consumes.
   GemmIn act(Tensor a, Tensor b, const Norm* nrm, int T, int F) {
-    const int C = a.C + (b.p ? b.C : 0);
+    const int C = a.C + (b.C > 0 ? b.C : 0);
     const int64_t n = (int64_t)B * T * F * C;
     uint16_t* hi = reinterpret_cast<uint16_t*>(buf((n + 1) / 2));
     uint16_t* lo = reinterpret_cast<uint16_t*>(buf((n + 1) / 2));
@@ -618,6 +628,7 @@ extern "C" int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, fl
   Fwd f{m, st, false, batch, m->cfg.precision == SESA_PREC_BF16X3 ? 1 : 0, ws};
   f.stats_base = ws + fb;
   f.stats_cap = sb;
+  f.float_cap = fb;
   f.run(x, out);
   return f.rc;
 }

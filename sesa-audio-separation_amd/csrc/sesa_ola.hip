@@ -177,9 +177,11 @@ extern "C" int sesa_ola_accumulate_f32(const float* y, int n_chunks, int n_out_c
 extern "C" int sesa_ola_finalize_f32(const float* result, const float* counter, int n_out_ch, int64_t L_pad,
                                      int64_t border, float* out, void* stream) {
   clear_error();
-  SESA_REQUIRE(result && counter && out && n_out_ch > 0 && border >= 0 && L_pad > 2 * border, SESA_ERR_INVALID,
+  SESA_REQUIRE(n_out_ch > 0 && border >= 0 && L_pad >= 2 * border, SESA_ERR_INVALID,
                "sesa_ola_finalize_f32: bad arguments");
   const int64_t L_out = L_pad - 2 * border;
+  if (L_out == 0) return SESA_OK;  // empty track (the reference returns empty stems)
+  SESA_REQUIRE(result && counter && out, SESA_ERR_INVALID, "sesa_ola_finalize_f32: null pointer");
   hipLaunchKernelGGL(ola_finalize_kernel, dim3(grid_for(L_out, 256)), dim3(256), 0, as_stream(stream), result,
                      counter, n_out_ch, L_pad, border, L_out, out);
   SESA_CHECK_LAUNCH();

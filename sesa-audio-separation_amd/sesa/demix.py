@@ -90,6 +90,10 @@ def demix_device(config, model, mix, device, exec_batch=None, progress=True, chu
     else:
         mix_d = torch.from_numpy(np.ascontiguousarray(mix, dtype=np.float32)).to(device, non_blocking=False)
     n_ch, L = mix_d.shape
+    if L == 0:  # the reference loop never runs and returns empty stems (result/counter of length 0)
+        if chunk_range is not None:
+            return (torch.zeros(ni * n_ch, 0, device=device), torch.zeros(0, device=device), (False, 0, 0))
+        return torch.zeros(ni, n_ch, 0, device=device, dtype=torch.float32)
     padded, border, L_pad, batches, prog = chunk_plan(L, C, ov, bs)
     E = exec_batch or getattr(model, "exec_batch", None) or 8
     win = _Windows(C, device)

@@ -100,6 +100,8 @@ def demix_sharded(config, model, mix_d, device=None, rank=None, world=None, exec
     ni = len(prefer_target_instrument(config))
     n_ch, L = mix_d.shape
     rows = ni * n_ch
+    if L == 0:
+        return torch.zeros(ni, n_ch, 0, device=mix_d.device, dtype=torch.float32)
     plan = shard_plan(config, L, world)
     if local_fn is None:
         local = local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch)

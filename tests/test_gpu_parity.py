@@ -175,3 +175,20 @@ def test_sharded_path_single_rank_matches_demix(dev):
         a = demix_device(c, m, mix, dev, exec_batch=4)
     b = demix_sharded(c, m, mix, dev, rank=0, world=1, exec_batch=4)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("L", [0, 1, 7, 1000, 32256, 32257, 64512])
+def test_demix_edge_lengths_vs_oracle(dev, L):
+    """Empty, tiny and chunk-boundary lengths (reflect/zero tail pads, unpadded tracks), stand-in
+    model: bit-exact against the oracle restatement of the reference loop."""
+    from oracle import demix as od
+    from sesa.demix import demix_device
+    c = _cfg("config_mdx23c_small.yaml")
+    rng = np.random.default_rng(L)
+    mix = (0.1 * rng.standard_normal((2, L))).astype(np.float32)
+    with contextlib.redirect_stdout(io.StringIO()):
+        est = demix_device(c, _StandIn(), mix, dev, exec_batch=2).cpu().numpy()
+    ref = od.demix(c, lambda x: _StandIn()(x), mix)
+    assert est.shape == (2, 2, L)
+    np.testing.assert_array_equal(est[0], ref["vocals"])
+    np.testing.assert_array_equal(est[1], ref["other"])

@@ -1,0 +1,55 @@
+"""HBM traffic per launch of the dominant kernel class from two rocprofv3 PMC passes.
+
+Per MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7: FETCH_SIZE and WRITE_SIZE are collected
+in SEPARATE passes (TCC slots), both in KiB; on gfx950 FETCH_SIZE reports exactly half of the bytes
+of a wide coalesced streaming read, so it is doubled before comparing with byte counts.
+
+usage: python tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> <kernel-substring> [out.json]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def read_counter(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    per = defaultdict(float)   # dispatch id -> value
+    names = {}
+    for fn in files:
+        with open(fn) as f:
+            for r in csv.DictReader(f):
+                if r.get("Counter_Name") != counter:
+                    continue
+                did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+                per[did] += float(r["Counter_Value"])
+                names[did] = r.get("Kernel_Name", "")
+    return per, names
+
+
+def main(fetch_dir, write_dir, substr, out=None):
+    f, fn = read_counter(fetch_dir, "FETCH_SIZE")
+    w, wn = read_counter(write_dir, "WRITE_SIZE")
+    fk = [v for k, v in f.items() if substr in fn[k]]
+    wk = [v for k, v in w.items() if substr in wn[k]]
+    if not fk or not wk:
+        raise SystemExit(f"no dispatches matching {substr!r}")
+    fetch_kib = sum(fk) / len(fk)
+    write_kib = sum(wk) / len(wk)
+    res = {"kernel_match": substr, "launches_fetch_pass": len(fk), "launches_write_pass": len(wk),
+           "fetch_size_kib_avg": round(fetch_kib, 1), "write_size_kib_avg": round(write_kib, 1),
+           "hbm_bytes_per_launch": round((2 * fetch_kib + write_kib) * 1024),
+           "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts half of "
+                         "wide coalesced reads; MI355X_MICROARCH.md §HBM)"}
+    print(json.dumps(res, indent=1))
+    if out:
+        with open(out, "w") as fo:
+            json.dump(res, fo, indent=1)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
