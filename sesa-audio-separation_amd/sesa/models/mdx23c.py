@@ -61,7 +61,8 @@ class TFC_TDF_net:
         for k in self._params:
             self._params[k] = torch.zeros(shapes[k], dtype=torch.float32)
         self._handles = {}      # device index -> native handle
-        self._ws = {}           # (device, batch) -> workspace tensor
+        self._ws = {}           # device index -> workspace tensor (largest batch seen)
+        self._ws_bytes = {}     # batch -> bytes
         self._dirty = True
         self.training = False
 
@@ -100,11 +101,13 @@ class TFC_TDF_net:
         return self
 
     def workspace_bytes(self, batch):
-        h = self._create_handle(self.precision)
-        try:
-            return N.lib().sesa_mdx23c_workspace_size(h, batch)
-        finally:
-            N.lib().sesa_mdx23c_destroy(h)
+        if batch not in self._ws_bytes:
+            h = self._create_handle(self.precision)
+            try:
+                self._ws_bytes[batch] = N.lib().sesa_mdx23c_workspace_size(h, batch)
+            finally:
+                N.lib().sesa_mdx23c_destroy(h)
+        return self._ws_bytes[batch]
 
     # ---- nn.Module-like surface used by the reference callers ----
     def named_parameters(self):
@@ -147,14 +150,15 @@ class TFC_TDF_net:
 
     # ---- forward ----
     def workspace(self, device, batch):
-        key = (device.index, batch)
-        if key not in self._ws:
-            # keep one workspace per device (the largest batch seen)
-            for k in [k for k in self._ws if k[0] == device.index]:
-                del self._ws[k]
-            nbytes = self.workspace_bytes(batch)
-            self._ws[key] = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        return self._ws[key]
+        """One workspace per device, grown to the largest batch seen and reused for smaller ones
+        (the requirement is monotone in batch), so a track's short last group never reallocates."""
+        idx = device.index
+        need = self.workspace_bytes(batch)
+        ws = self._ws.get(idx)
+        if ws is None or ws.numel() < need:
+            self._ws.pop(idx, None)
+            self._ws[idx] = ws = torch.empty(need, dtype=torch.uint8, device=device)
+        return ws
 
     def __call__(self, x):
         return self.forward(x)

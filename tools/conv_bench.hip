@@ -54,6 +54,7 @@ uint16_t* dalloc_bf16(size_t n) {
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 16;
   const int x3 = argc > 2 ? atoi(argv[2]) : 1;
+  const bool nostats = argc > 3 && atoi(argv[3]) == 1;  // ablation: no norm-statistics atomics
   struct Shape { int T, F, Cin, Cout, kind; };
   Shape shapes[] = {{256, 1024, 128, 128, CONV3X3}, {128, 512, 256, 256, CONV3X3}, {64, 256, 384, 384, CONV3X3},
                     {32, 128, 512, 512, CONV3X3}, {16, 64, 640, 640, CONV3X3},  {256, 1024, 128, 128, CONV1X1},
@@ -96,7 +97,7 @@ int main(int argc, char** argv) {
     a.in.gamma = gam;
     a.in.beta = bet;
     a.in.inv_count = 1.0 / ((double)Tin * Fin);
-    a.out = GemmOut{y, nullptr, st_out, s.Cout, 0};
+    a.out = GemmOut{y, nullptr, nostats ? nullptr : st_out, s.Cout, 0};
     a.w = w;
     a.T_in = Tin;
     a.F_in = Fin;
@@ -180,7 +181,7 @@ int main(int argc, char** argv) {
     a.in.C_split = s.C;
     a.in.C_in = s.C;
     a.in.inv_count = 1.0 / ((double)s.T * s.K);
-    a.out = GemmOut{y, nullptr, st_out, s.C, 0};
+    a.out = GemmOut{y, nullptr, nostats ? nullptr : st_out, s.C, 0};
     a.w = w;
     a.T = s.T;
     a.K = s.K;
