@@ -378,7 +378,7 @@ struct Fwd {
       const int64_t plane = (int64_t)B * L.T * L.F * c;
       float* S = buf(plane);  // block output
       float* H = buf(plane);
-      float* U = buf((int64_t)B * L.T * (L.F / bnf) * c);  // U^T [B][T][c][F/bn]
+      float* U = buf(tdf_u_floats((int64_t)B * L.T * c, L.F / bnf));  // tiled U^T (sesa_tapgemm.hip)
       double* st_h1 = stats(c);
       double* st_u = stats(c);
       double* st_h2 = stats(c);

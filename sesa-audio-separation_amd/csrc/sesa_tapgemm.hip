@@ -187,14 +187,15 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
   constexpr int A_ITEMS = (NPOS * 4 + kThreads - 1) / kThreads;
   constexpr int W16 = (X3 ? 2 : 1) * W_BYTES / 16;
   constexpr int W_ITEMS = (W16 + kThreads - 1) / kThreads;
+  constexpr int W1_ITEMS = ((X3 ? 2 : 1) * W1_BYTES / 16 + kThreads - 1) / kThreads;
   static_assert(A_ITEMS <= 32, "valid mask");
   f32x4 areg[A_ITEMS];  // native vectors: HIP's float4/uint4 structs copy via memcpy and defeat SROA
   u32x4 wreg[W_ITEMS];
   uint32_t avalid = 0;
 
   // source of chunk kc: (src, local channel offset, first concatenated channel, is-extra)
-  auto chunk_src = [&](int kc, Src& src, int& cl0, int& k0, bool& ext) {
-    ext = XTRA && kc >= a.n_chunks;
+  auto chunk_src = [&](int kc, auto EXT, Src& src, int& cl0, int& k0) {
+    constexpr bool ext = decltype(EXT)::value;
     k0 = (ext ? kc - a.n_chunks : kc) * kConvBK;
     const GemmIn& g = ext ? a.xin : a.in;
     const int s = k0 < g.C_split ? 0 : 1;
@@ -202,16 +203,17 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
     cl0 = k0 - (s ? g.C_split : 0);
   };
 
-  auto load_chunk = [&](int kc) {
+  auto load_chunk = [&](int kc, auto EXT) {
+    constexpr bool ext = decltype(EXT)::value;
     Src src;
     int cl0, k0;
-    bool ext;
-    chunk_src(kc, src, cl0, k0, ext);
+    chunk_src(kc, EXT, src, cl0, k0);
     const int w16 = ext ? (X3 ? 2 : 1) * W1_BYTES / 16 : W16;
     const u32x4* wsrc = reinterpret_cast<const u32x4*>(
         wblk + (ext ? (int64_t)a.n_chunks * W_BYTES + (int64_t)(kc - a.n_chunks) * W1_BYTES
                     : (int64_t)kc * W_BYTES));
-    Unroll<0, W_ITEMS>::run([&](auto I) {
+    constexpr int WI = ext ? W1_ITEMS : W_ITEMS;
+    Unroll<0, WI>::run([&](auto I) {
       const int e = tid + I * kThreads;
       wreg[I] = wsrc[e < w16 ? e : w16 - 1];  // unconditional (clamped) so wreg stays in VGPRs
     });
@@ -255,14 +257,15 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
     });
   };
 
-  auto store_chunk = [&](int kc) {
+  auto store_chunk = [&](int kc, auto EXT) {
+    constexpr bool ext = decltype(EXT)::value;
     Src src;
     int cl0, k0;
-    bool ext;
-    chunk_src(kc, src, cl0, k0, ext);
+    chunk_src(kc, EXT, src, cl0, k0);
     const int w16 = ext ? (X3 ? 2 : 1) * W1_BYTES / 16 : W16;
     u32x4* wdst = reinterpret_cast<u32x4*>(W_hi);
-    Unroll<0, W_ITEMS>::run([&](auto I) {
+    constexpr int WI = ext ? W1_ITEMS : W_ITEMS;
+    Unroll<0, WI>::run([&](auto I) {
       const int e = tid + I * kThreads;
       if (e < w16) wdst[e] = wreg[I];
     });
@@ -333,17 +336,27 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
       }
   };
 
-  load_chunk(0);
-  for (int kc = 0; kc < n_total; ++kc) {
+  // Main K loop over the normalised input (all taps, fully unrolled), then -- XTRA only -- a
+  // separate loop over the raw shortcut chunks (centre tap), so neither loop body carries the
+  // other's code and register pressure.
+  using kMain = std::false_type;
+  using kExt = std::integral_constant<bool, XTRA>;
+  load_chunk(0, kMain{});
+  for (int kc = 0; kc < a.n_chunks; ++kc) {
     __syncthreads();  // previous chunk's fragment reads are done (and sc/sh are built)
-    store_chunk(kc);
+    store_chunk(kc, kMain{});
     __syncthreads();
-    if (kc + 1 < n_total) load_chunk(kc + 1);
-    if (!XTRA || kc < a.n_chunks) {
-      constexpr int TU = XTRA ? 3 : TAPS;  // the fused-shortcut variant needs the registers
-#pragma unroll TU
-      for (int tap = 0; tap < TAPS; ++tap) mfma_tap(tap / KW, tap % KW, tap, W_BYTES);
-    } else {
+    if (kc + 1 < a.n_chunks) load_chunk(kc + 1, kMain{});
+    else if (XTRA && n_total > a.n_chunks) load_chunk(kc + 1, kExt{});
+#pragma unroll
+    for (int tap = 0; tap < TAPS; ++tap) mfma_tap(tap / KW, tap % KW, tap, W_BYTES);
+  }
+  if (XTRA) {
+    for (int kc = a.n_chunks; kc < n_total; ++kc) {
+      __syncthreads();
+      store_chunk(kc, kExt{});
+      __syncthreads();
+      if (kc + 1 < n_total) load_chunk(kc + 1, kExt{});
       mfma_tap(CTAP / KW, CTAP % KW, 0, W1_BYTES);
     }
   }
@@ -421,39 +434,76 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// TDF linear: per (b, t), D[m = f_out][n = c] = sum_k W[m][k] * act(x[b][t][k][c]).
-// One workgroup covers BM = 128*MI output rows (all of M for the TDF's first Linear, so every
-// input element is normalised + GELU'd once) x BN = 64 channels; 4 waves stacked along M.
-// BK_CONTIG: the input is the transposed U^T [b][t][c][k] written by the first Linear (k
-//   contiguous -> two 16-B loads per 8 k); otherwise NHWC [b][t][k][c] (lanes walk c).
-// OUT_T: write the output transposed as U^T [b][t][c][m] (16-B stores of 4 consecutive rows).
-template <int MI, bool X3, bool BK_CONTIG, bool OUT_T>
-__global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
-  constexpr int BN = 64;
-  constexpr int WM = 4;
-  constexpr int NI = BN / 32;
+// TDF linear (mdx23c_tfc_tdf_v3.py:113-120) as one GEMM per launch over all (b, t):
+//   D[m][n] = sum_k W[m][k] * act(X[k][n]),  n = (b, t, c) flattened over the whole batch.
+// The weight (M x K, <= 1 MB as hi+lo) is the small operand and stays L2-resident; the workgroup
+// tile is BM rows x BN = 128 columns (per-column norm affines computed once in the prologue),
+// 4 waves of MI x NI 32x32 blocks, 2 workgroups per CU so one workgroup's staging overlaps the
+// other's MFMAs.  Every thread stages 4 consecutive columns x 4 k rows of X per K chunk.
+// U (the bottleneck activation between the two Linears) is stored k-major TILED:
+//   [n / 128][ceil(M / 32)][32 m][128 n] fp32 (tdf_u_floats() gives the padded size), so the first
+//   Linear stores full 128-B lines straight from the MFMA layout and each K chunk the second
+//   Linear stages is one contiguous 16 KB block.
+// U_IN:  X is tiled U; else NHWC [(b,t)][k][c].
+// U_OUT: D is written as tiled U; else NHWC [(b,t)][m][c] (+ in-place residual, x + tdf(x), :136),
+//   transposed through LDS so every thread moves 16 B of a row (residual load, add, store).
+//   Epilogue: per-column sum / sum-of-squares for the next InstanceNorm (fp64 atomics per (b, c)).
+template <int WM, int WN, int MI, int NI, bool X3, bool U_IN, bool U_OUT>
+__global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BN = WN * NI * 32;
   constexpr int BM = WM * MI * 32;
+  static_assert(BN == 128, "U tiling and the epilogue assume 128-column tiles");
   constexpr int ROWB = kTdfBK * 2;            // 64 B per image row (32 bf16)
   constexpr int AW_BYTES = BM * ROWB;
   constexpr int B_BYTES = BN * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * AW_BYTES + 2 * B_BYTES + 2 * kMaxCin * 4];
+  constexpr int EPI_ROWS = 32;                // rows per epilogue pass through LDS
+  constexpr int EPI_BYTES = EPI_ROWS * BN * 4;
+  constexpr int MAIN_BYTES = 2 * AW_BYTES + 2 * B_BYTES;
+  constexpr int SM_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SM_BYTES + 3 * BN * 4 + 2 * NT * 4 * 4];
   char* Whi = smem;
   char* Wlo = smem + AW_BYTES;
   char* Bhi = smem + 2 * AW_BYTES;
   char* Blo = Bhi + B_BYTES;
-  float* sc = reinterpret_cast<float*>(Blo + B_BYTES);
-  float* sh = sc + kMaxCin;
+  float* csc = reinterpret_cast<float*>(smem + SM_BYTES);  // per-column affine
+  float* csh = csc + BN;
+  int* cvalid = reinterpret_cast<int*>(csh + BN);
+  float* red = reinterpret_cast<float*>(cvalid + BN);      // [2][NT][4] column partial sums
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wm = tid >> 6;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
   const int l32 = lane & 31, h = lane >> 5;
-  const int mb = blockIdx.x, c0 = blockIdx.y * BN;
-  const int bt = blockIdx.z;
-  const int b = bt / a.T;
+  const int n_mb = (a.M + BM - 1) / BM;
+  const int mb = blockIdx.x % n_mb;
+  const int64_t n0 = (int64_t)(blockIdx.x / n_mb) * BN;
   const Src src = pick_src(a.in, 0);
   const int C = src.C;
+  const int64_t n_total = (int64_t)a.batch * a.T * C;
 
-  build_affine(a.in, b, sc, sh);
+  // per-column InstanceNorm affine of the consumer (norm over (T, K) per (b, c), :113/:117)
+  for (int j = tid; j < BN; j += NT) {
+    const int64_t n = n0 + j;
+    float scale = 1.f, shift = 0.f;
+    const int ok = n < n_total;
+    if (ok && src.mode == SRC_NORM_GELU) {
+      const int c = (int)(n % C);
+      const int b = (int)(n / ((int64_t)a.T * C));
+      const double* st = src.stats + ((int64_t)b * C + c) * 2;
+      const double mean = st[0] * a.in.inv_count;
+      double var = st[1] * a.in.inv_count - mean * mean;
+      if (var < 0) var = 0;
+      const float rstd = (float)(1.0 / sqrt(var + 1e-5));
+      const float g = a.in.gamma ? a.in.gamma[c] : 1.f;
+      const float be = a.in.beta ? a.in.beta[c] : 0.f;
+      scale = g * rstd;
+      shift = be - (float)mean * scale;
+    }
+    csc[j] = scale;
+    csh[j] = shift;
+    cvalid[j] = ok;
+  }
 
   f32x16 acc[MI][NI];
 #pragma unroll
@@ -463,75 +513,82 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const float* xin = src.ptr + (int64_t)bt * a.K * C;  // this (b, t) slice, either layout
   const uint16_t* wblk = a.w + (int64_t)mb * a.n_chunks * (2 * AW_BYTES / 2);
 
   constexpr int N16 = (X3 ? 2 : 1) * AW_BYTES / 16;
-  constexpr int W_ITEMS = (N16 + kThreads - 1) / kThreads;
-  constexpr int B_ITEMS = (BN * 4 + kThreads - 1) / kThreads;
+  constexpr int W_ITEMS = (N16 + NT - 1) / NT;
+  constexpr int B_ITEMS_ALL = BN * 2;  // (4 columns, 4 k) items per 32-k chunk
+  constexpr int B_ITEMS = (B_ITEMS_ALL + NT - 1) / NT;
   u32x4 wreg[W_ITEMS];
-  f32x4 breg[B_ITEMS][2];
+  f32x4 breg[B_ITEMS][4];
 
   auto load_chunk = [&](int kc) {
     const u32x4* s4 = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * (2 * AW_BYTES / 2));
     Unroll<0, W_ITEMS>::run([&](auto I) {
-      const int e = tid + I * kThreads;
+      const int e = tid + I * NT;
       wreg[I] = s4[e < N16 ? e : N16 - 1];
     });
     const int k0 = kc * kTdfBK;
     Unroll<0, B_ITEMS>::run([&](auto I) {
-      const int e = tid + I * kThreads;
-      const int n = e % BN, g = e / BN;
-      const int c = c0 + n;
-      const int k = k0 + 8 * g;
-      const bool ok = (e < BN * 4) && c < C && k < a.K;
-      if (BK_CONTIG) {
-        // k-contiguous: K is a multiple of 8, so a group of 8 is wholly in or out
-        const f32x4* p4 = reinterpret_cast<const f32x4*>(xin + (int64_t)(ok ? c : 0) * a.K + (ok ? k : 0));
-        breg[I][0] = ok ? p4[0] : f32x4{0.f, 0.f, 0.f, 0.f};
-        breg[I][1] = ok ? p4[1] : f32x4{0.f, 0.f, 0.f, 0.f};
-      } else {
+      const int e = tid + I * NT;
+      const int j = (e % (BN / 4)) * 4, g = e / (BN / 4);  // 4 columns, k = k0 + 4g .. +3
+      const int64_t n = n0 + j;
+      const bool okn = (e < B_ITEMS_ALL) && n < n_total;  // n_total % 4 == 0 (C % 4 == 0)
+      if (U_IN) {
+        const float* blk = src.ptr + (((n0 >> 7) * a.n_chunks + kc) << 12) + j;  // contiguous [32 k][128 n]
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const bool okj = ok && k + j < a.K;
-          breg[I][j >> 2][j & 3] = okj ? xin[(int64_t)(k + j) * C + c] : 0.f;
+        for (int q = 0; q < 4; ++q) {
+          const bool ok = okn && k0 + 4 * g + q < a.K;
+          breg[I][q] = ok ? *reinterpret_cast<const f32x4*>(blk + (4 * g + q) * 128) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
+      } else {
+        const int64_t bt = n / C;
+        const int c = (int)(n - bt * C);  // C % 4 == 0: the 4 columns share (b, t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = k0 + 4 * g + q;
+          const bool ok = okn && k < a.K;
+          breg[I][q] = ok ? *reinterpret_cast<const f32x4*>(src.ptr + (bt * a.K + k) * C + c)
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    });
+  };
+
+  auto store_chunk = [&](int kc) {
+    u32x4* d4 = reinterpret_cast<u32x4*>(Whi);
+    Unroll<0, W_ITEMS>::run([&](auto I) {
+      const int e = tid + I * NT;
+      if (N16 % NT == 0 || e < N16) d4[e] = wreg[I];
+    });
+    const int k0 = kc * kTdfBK;
+    Unroll<0, B_ITEMS>::run([&](auto I) {
+      const int e = tid + I * NT;
+      if (B_ITEMS_ALL % NT != 0 && e >= B_ITEMS_ALL) return;
+      const int j0 = (e % (BN / 4)) * 4, g = e / (BN / 4);
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const int j = j0 + cc;
+        const float scale = csc[j], shift = csh[j];
+        const bool okc = cvalid[j];
+        __bf16 hi[4], lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float x = breg[I][q][cc];
+          if (src.mode == SRC_NORM_GELU) x = (okc && k0 + 4 * g + q < a.K) ? gelu_erf(x * scale + shift) : 0.f;
+          split_bf16(x, hi[q], lo[q]);
+        }
+        const int off = j * ROWB + ((((g >> 1) ^ ((j >> 2) & 3))) << 4) + ((g & 1) << 3);
+        *reinterpret_cast<uint2*>(Bhi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
+        if (X3) *reinterpret_cast<uint2*>(Blo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
       }
     });
   };
 
   load_chunk(0);
   for (int kc = 0; kc < a.n_chunks; ++kc) {
-    __syncthreads();
-    {
-      u32x4* d4 = reinterpret_cast<u32x4*>(Whi);
-      Unroll<0, W_ITEMS>::run([&](auto I) {
-        const int e = tid + I * kThreads;
-        if (N16 % kThreads == 0 || e < N16) d4[e] = wreg[I];
-      });
-      const int k0 = kc * kTdfBK;
-      Unroll<0, B_ITEMS>::run([&](auto I) {
-        const int e = tid + I * kThreads;
-        if (BN * 4 % kThreads != 0 && e >= BN * 4) return;
-        const int n = e % BN, g = e / BN;
-        const int c = c0 + n;
-        const bool ok = c < C && k0 + 8 * g < a.K;
-        const float scale = ok ? sc[c] : 1.f, shift = ok ? sh[c] : 0.f;
-        __bf16 hi[8], lo[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float x = breg[I][j >> 2][j & 3];
-          if (src.mode == SRC_NORM_GELU && ok && k0 + 8 * g + j < a.K) x = gelu_erf(x * scale + shift);
-          split_bf16(x, hi[j], lo[j]);
-        }
-        const int off = n * ROWB + ((g ^ ((n >> 2) & 3)) << 4);
-        *reinterpret_cast<uint4*>(Bhi + off) =
-            make_uint4(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]), pack2(hi[4], hi[5]), pack2(hi[6], hi[7]));
-        if (X3)
-          *reinterpret_cast<uint4*>(Blo + off) =
-              make_uint4(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]), pack2(lo[4], lo[5]), pack2(lo[6], lo[7]));
-      });
-    }
+    __syncthreads();  // previous chunk's fragment reads done (and the column affines are built)
+    store_chunk(kc);
     __syncthreads();
     if (kc + 1 < a.n_chunks) load_chunk(kc + 1);
 #pragma unroll
@@ -547,7 +604,7 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int n = j * 32 + l32;
+        const int n = (wn * NI + j) * 32 + l32;
         const int off = n * ROWB + ((q ^ ((n >> 2) & 3)) << 4);
         bh[j] = *reinterpret_cast<const bf16x8*>(Bhi + off);
         if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(Blo + off);
@@ -565,77 +622,136 @@ __global__ void __launch_bounds__(kThreads, 2) tdf_kernel(TdfArgs a) {
     }
   }
 
-  float ssum[NI], ssq[NI];
+  // ---- epilogue ----
+  // Each thread ends up owning column partial sums for 4 consecutive columns (cs4 = tid % 32).
+  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+  const int cs4 = (tid % (BN / 4)) * 4;
+  if (U_OUT) {
+    // tiled U: for each register, lanes 0-31 / 32-63 store two full 128-B rows (32 consecutive n)
+    const int mchunks = (a.M + 31) >> 5;
+    float* ublk = a.out.ptr + (((n0 >> 7) * mchunks) << 12);
+    float* red2 = reinterpret_cast<float*>(smem);  // [WM][BN][2] (main-loop LDS is dead)
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < NI; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
-  const int Cout = a.out.C_out;
+    for (int j = 0; j < NI; ++j) {
+      const int jl = (wn * NI + j) * 32 + l32;
+      const bool nok = n0 + jl < n_total;
+      float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int c = c0 + j * 32 + l32;
-    if (c >= Cout) continue;
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mb * BM + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (!nok || m >= a.M) continue;
+          const float v = acc[i][j][r];
+          ublk[((m >> 5) << 12) + (m & 31) * 128 + jl] = v;
+          s0 += v;
+          s1 += v * v;
+        }
+      s0 += __shfl_xor(s0, 32);
+      s1 += __shfl_xor(s1, 32);
+      if (h == 0) {
+        red2[(wm * BN + jl) * 2 + 0] = s0;
+        red2[(wm * BN + jl) * 2 + 1] = s1;
+      }
+    }
+    __syncthreads();
+    if (a.out.stats) {
+      for (int jl = tid; jl < BN; jl += NT) {
+        const int64_t n = n0 + jl;
+        if (n >= n_total) continue;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          s0 += red2[(w * BN + jl) * 2 + 0];
+          s1 += red2[(w * BN + jl) * 2 + 1];
+        }
+        const int c = (int)(n % C);
+        const int b = (int)(n / ((int64_t)a.T * C));
+        double* st = a.out.stats + ((int64_t)b * C + c) * 2;
+        atomicAdd(st + 0, (double)s0);
+        atomicAdd(st + 1, (double)s1);
+      }
+    }
+    return;
+  }
+
+  // NHWC output through LDS, EPI_ROWS rows per pass.  A 128-column tile lies in one (b, t) when
+  // C % 128 == 0 (every real config); otherwise each 4-column group computes its own (b, t).
+  float* stage = reinterpret_cast<float*>(smem);  // [EPI_ROWS][BN] fp32, row-swizzled by 16-B groups
+  constexpr int ITEMS = EPI_ROWS * BN / 4 / NT;   // f32x4 items per thread per pass
+  static_assert(EPI_ROWS * BN / 4 % NT == 0, "epilogue items");
+  const int64_t ncol = n0 + cs4;
+  const bool col_ok = ncol < n_total;
+  const int64_t bt = ncol / C;
+  const int c = (int)(ncol - bt * C);
+  for (int p = 0; p < BM / EPI_ROWS; ++p) {
+    const int row0 = mb * BM + p * EPI_ROWS;
+    // residual loads first (they alias the output, so they are issued before any store of this pass)
+    f32x4 res[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      const int rl = (tid + it * NT) / (BN / 4);
+      const int m = row0 + rl;
+      res[it] = (a.out.residual && col_ok && m < a.M)
+                    ? *reinterpret_cast<const f32x4*>(a.out.residual + (bt * a.M + m) * C + c)
+                    : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();  // previous pass's stage reads (and the main loop's LDS reads) are done
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
+      const int rb = (wm * MI + i) * 32;  // tile-local row block of this MFMA block
+      if (rb < p * EPI_ROWS || rb >= (p + 1) * EPI_ROWS) continue;
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int m0 = mb * BM + (wm * MI + i) * 32 + 8 * g4 + 4 * h;  // rows m0 .. m0+3 in regs 4*g4 ..
-        if (OUT_T) {
-          // U^T [b][t][c][m]; M is a multiple of 4 here (F / bottleneck_factor, checked on the host)
-          if (m0 >= a.M) continue;
-          f32x4 v4;
+      for (int j = 0; j < NI; ++j) {
+        const int jl = (wn * NI + j) * 32 + l32;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float v = acc[i][j][4 * g4 + q];
-            v4[q] = v;
-            ssum[j] += v;
-            ssq[j] += v * v;
-          }
-          *reinterpret_cast<f32x4*>(a.out.ptr + ((int64_t)bt * Cout + c) * a.M + m0) = v4;
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int m = m0 + q;
-            if (m >= a.M) continue;
-            const int64_t idx = ((int64_t)bt * a.M + m) * Cout + c;
-            float v = acc[i][j][4 * g4 + q];
-            if (a.out.residual) v += a.out.residual[idx];
-            a.out.ptr[idx] = v;
-            ssum[j] += v;
-            ssq[j] += v * v;
-          }
+        for (int r = 0; r < 16; ++r) {
+          const int rl = rb - p * EPI_ROWS + (r & 3) + 8 * (r >> 2) + 4 * h;
+          stage[rl * BN + (((jl >> 2) ^ (rl & 31)) << 2) + (jl & 3)] = acc[i][j][r];
         }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      const int rl = (tid + it * NT) / (BN / 4);
+      const int m = row0 + rl;
+      if (!col_ok || m >= a.M) continue;
+      f32x4 v = *reinterpret_cast<const f32x4*>(stage + rl * BN + (((cs4 >> 2) ^ (rl & 31)) << 2));
+      v += res[it];
+      *reinterpret_cast<f32x4*>(a.out.ptr + (bt * a.M + m) * C + c) = v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ssum[q] += v[q];
+        ssq[q] += v[q] * v[q];
       }
     }
   }
   if (a.out.stats) {
+    // threads tid, tid + 32, ... own the same 4 columns: reduce through LDS
+    f32x4* r4 = reinterpret_cast<f32x4*>(red);
+    r4[tid] = f32x4{ssum[0], ssum[1], ssum[2], ssum[3]};
+    r4[NT + tid] = f32x4{ssq[0], ssq[1], ssq[2], ssq[3]};
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      ssum[j] += __shfl_xor(ssum[j], 32);
-      ssq[j] += __shfl_xor(ssq[j], 32);
-      if (h == 0) {
-        const int n = j * 32 + l32;
-        red[(wm * BN + n) * 2 + 0] = ssum[j];
-        red[(wm * BN + n) * 2 + 1] = ssq[j];
+    if (tid < BN / 4 && col_ok) {
+      f32x4 s0 = r4[tid], s1 = r4[NT + tid];
+      for (int t = tid + BN / 4; t < NT; t += BN / 4) {
+        s0 += r4[t];
+        s1 += r4[NT + t];
       }
-    }
-    __syncthreads();
-    for (int n = tid; n < BN; n += kThreads) {
-      const int c = c0 + n;
-      if (c >= Cout) continue;
-      float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        s0 += red[(w * BN + n) * 2 + 0];
-        s1 += red[(w * BN + n) * 2 + 1];
+      for (int q = 0; q < 4; ++q) {
+        const int64_t n = ncol + q;
+        const int cq = (int)(n % C);
+        const int b = (int)(n / ((int64_t)a.T * C));
+        double* st = a.out.stats + ((int64_t)b * C + cq) * 2;
+        atomicAdd(st + 0, (double)s0[q]);
+        atomicAdd(st + 1, (double)s1[q]);
       }
-      double* st = a.out.stats + ((int64_t)b * Cout + c) * 2;
-      atomicAdd(st + 0, (double)s0);
-      atomicAdd(st + 1, (double)s1);
     }
   }
 }
-
 
 // ---------------------------------------------------------------------------------------------
 // act_split: one pass over a normalised tensor, writing the bf16 hi/lo operand planes of its
@@ -720,17 +836,33 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
   return SESA_ERR_INVALID;
 }
 
-template <int MI, bool BKC, bool OT>
-int launch_tdf_t(int x3, const TdfArgs& a, int batch, hipStream_t st) {
-  constexpr int BM = 4 * MI * 32;
-  dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)((a.out.C_out + 63) / 64), (unsigned)(batch * a.T));
-  if (x3) hipLaunchKernelGGL((tdf_kernel<MI, true, BKC, OT>), grid, dim3(kThreads), 0, st, a);
-  else hipLaunchKernelGGL((tdf_kernel<MI, false, BKC, OT>), grid, dim3(kThreads), 0, st, a);
+template <int WM, int WN, int MI, int NI, bool KC, bool OT>
+int launch_tdf_t(int x3, const TdfArgs& a, hipStream_t st) {
+  constexpr int BM = WM * MI * 32, BN = WN * NI * 32, NT = 64 * WM * WN;
+  const int64_t n_total = (int64_t)a.batch * a.T * a.in.src[0].C;
+  const int64_t blocks = ((a.M + BM - 1) / BM) * ((n_total + BN - 1) / BN);
+  SESA_REQUIRE(blocks < (1ll << 31), SESA_ERR_INVALID, "tdf: grid too large");
+  if (x3) hipLaunchKernelGGL((tdf_kernel<WM, WN, MI, NI, true, KC, OT>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((tdf_kernel<WM, WN, MI, NI, false, KC, OT>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }
 
-int tdf_block_rows(int M) { return M > 128 ? 256 : 128; }
+// BN = 128 columns; BM from the row count (weights are packed per BM-row block to match)
+template <bool KC, bool OT>
+int launch_tdf_bm(int x3, const TdfArgs& a, hipStream_t st) {
+  switch (tdf_block_rows(a.M)) {
+    case 256: return launch_tdf_t<4, 1, 2, 4, KC, OT>(x3, a, st);
+    case 128: return launch_tdf_t<2, 2, 2, 2, KC, OT>(x3, a, st);
+    case 64: return launch_tdf_t<1, 4, 2, 1, KC, OT>(x3, a, st);
+    default: return launch_tdf_t<1, 4, 1, 1, KC, OT>(x3, a, st);
+  }
+}
+
+int64_t tdf_u_floats(int64_t n_cols, int M) { return ((n_cols + 127) / 128) * 128 * (int64_t)((M + 31) / 32 * 32); }
+
+int tdf_block_rows(int M) { return M > 128 ? 256 : M > 64 ? 128 : M > 32 ? 64 : 32; }
+
 
 int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st) {
   SESA_REQUIRE(in.C_in % 16 == 0 && in.C_split % 8 == 0 && in.C_in <= kMaxCin, SESA_ERR_INVALID,
@@ -744,15 +876,15 @@ int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, u
 
 // transposed_io: 0 = first Linear (NHWC in, U^T out), 1 = second Linear (U^T in, NHWC out)
 int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io) {
-  SESA_REQUIRE(a.in.C_in <= kMaxCin, SESA_ERR_INVALID, "tdf: C %d > %d", a.in.C_in, kMaxCin);
+  TdfArgs b = a;
+  b.batch = batch;
+  SESA_REQUIRE(a.in.src[0].C % 4 == 0, SESA_ERR_INVALID, "tdf: C %d must be a multiple of 4", a.in.src[0].C);
   if (transposed_io == 0) {
     SESA_REQUIRE(a.M % 4 == 0, SESA_ERR_INVALID, "tdf: M %d must be a multiple of 4", a.M);
-    return tdf_block_rows(a.M) == 256 ? launch_tdf_t<2, false, true>(x3, a, batch, st)
-                                      : launch_tdf_t<1, false, true>(x3, a, batch, st);
+    return launch_tdf_bm<false, true>(x3, b, st);
   }
   SESA_REQUIRE(a.K % 8 == 0, SESA_ERR_INVALID, "tdf: K %d must be a multiple of 8", a.K);
-  return tdf_block_rows(a.M) == 256 ? launch_tdf_t<2, true, false>(x3, a, batch, st)
-                                    : launch_tdf_t<1, true, false>(x3, a, batch, st);
+  return launch_tdf_bm<true, false>(x3, b, st);
 }
 
 }  // namespace sesa

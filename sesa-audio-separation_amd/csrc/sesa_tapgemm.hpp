@@ -58,6 +58,7 @@ struct TdfArgs {
   const uint16_t* w;         // packed [M/BM][K/32][BM][32] hi, lo (BM = tdf_block_rows(M))
   int T, K, M;               // F_in = K, F_out = M
   int n_chunks;              // ceil(K / 32)
+  int batch;                 // set by launch_tdf
 };
 
 // conv kinds
@@ -68,7 +69,9 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
 // channel-concatenated) input `in` of n_pos positions per batch item.
 int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st);
 int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io);
-int tdf_block_rows(int M);  // BM chosen for a TDF Linear with M output rows (weights packed to match)
+int tdf_block_rows(int M);
+// floats of the tiled U^T buffer [n/128][ceil(M/32)][128][32] for n_cols = B*T*C columns
+int64_t tdf_u_floats(int64_t n_cols, int M);  // BM chosen for a TDF Linear with M output rows (weights packed to match)
 
 // Tile geometry shared by the host packer and the kernels.
 constexpr int kTF = 32;       // output columns per tile (one MFMA 32-row block = one tile row)

@@ -63,7 +63,10 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  const bool only_tdf = getenv("ONLY_TDF") != nullptr;
+  const bool only_conv = getenv("ONLY_CONV") != nullptr;
   for (auto& s0 : shapes) {
+    if (only_tdf) break;
     Shape s = s0;
     const bool xtra = s.kind >= 100;  // conv3x3 with the block input fused as a 1x1 shortcut (extra K)
     if (xtra) s.kind -= 100;
@@ -130,7 +133,7 @@ int main(int argc, char** argv) {
     CK(hipFree(w));
     if (pre) { CK(hipFree(xh)); CK(hipFree(xl)); }
   }
-  {  // act_split over a level-0 tensor
+  if (!only_tdf) {  // act_split over a level-0 tensor
     const int64_t npos = 256 * 1024;
     const int C = 128;
     float* x = dalloc<float>((size_t)B * npos * C, 2.f);
@@ -160,14 +163,15 @@ int main(int argc, char** argv) {
     CK(hipFree(x)); CK(hipFree(st_in)); CK(hipFree(hi)); CK(hipFree(lo));
   }
   // TDF
+  if (only_conv) return 0;
   struct TShape { int T, K, M, C; };
   TShape ts[] = {{256, 1024, 256, 128}, {256, 256, 1024, 128}, {128, 512, 128, 256}, {128, 128, 512, 256},
-                 {32, 128, 32, 512}};
-  int tio[] = {0, 1, 0, 1, 0};
+                 {32, 128, 32, 512}, {32, 32, 128, 512}, {8, 32, 8, 768}, {8, 8, 32, 768}};
+  int tio[] = {0, 1, 0, 1, 0, 1, 0, 1};
   int ti = 0;
   for (auto& s : ts) {
     const int io = tio[ti++];
-    size_t in_n = (size_t)B * s.T * s.K * s.C, out_n = (size_t)B * s.T * s.M * s.C;
+    size_t in_n = (size_t)tdf_u_floats((int64_t)B * s.T * s.C, s.K), out_n = (size_t)tdf_u_floats((int64_t)B * s.T * s.C, s.M);
     float* x = dalloc<float>(in_n, 2.f);
     float* y = dalloc<float>(out_n);
     double* st_in = dalloc<double>((size_t)B * s.C * 2);
@@ -181,7 +185,7 @@ int main(int argc, char** argv) {
     a.in.C_split = s.C;
     a.in.C_in = s.C;
     a.in.inv_count = 1.0 / ((double)s.T * s.K);
-    a.out = GemmOut{y, nullptr, nostats ? nullptr : st_out, s.C, 0};
+    a.out = GemmOut{y, (io == 1 && !getenv("NORES")) ? y : nullptr, nostats ? nullptr : st_out, s.C, 0};  // lin2: in-place residual
     a.w = w;
     a.T = s.T;
     a.K = s.K;
