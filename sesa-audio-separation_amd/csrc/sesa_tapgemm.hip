@@ -434,6 +434,299 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// conv3x3_db_kernel: the TFC 3x3 convolutions (mdx23c_tfc_tdf_v3.py:104-112, 121-129) on the
+// pre-activated bf16 hi/lo planes of act_split, with LDS DOUBLE-BUFFERING and one barrier per K
+// chunk.  512 threads (8 waves, 2 per SIMD, one workgroup per CU): tile 16 rows (t) x 32 columns
+// (f) x 64 output channels, wave w owns output rows 2w, 2w+1 (MI = 2) x 64 channels (NI = 2).
+// Per 16-channel chunk one stage holds the 18x34 input halo (hi + lo, 39 KB) and the 9-tap weight
+// image (hi + lo, 36 KB); two stages = 152 KB.  Iteration k: MFMAs on stage k&1 while the
+// registers holding chunk k+1 (loaded during iteration k-1) are written to stage (k+1)&1, then
+// chunk k+2 is loaded to registers, then one barrier.  Twice the positions per workgroup of
+// tap_gemm_kernel halves the weight traffic per FLOP.
+// XTRA: the raw block input rides along as extra K over the centre tap (the 1x1 shortcut, :126,
+// :137): its chunks load only the 16x32 inner positions (fp32, split in registers).
+// Weight image and A-image layouts are exactly tap_gemm_kernel's (same host packing).
+template <bool X3, bool XTRA>
+__global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
+  constexpr int NT = 512;
+  constexpr int TM = 16, WM = 8, MI = 2, NI = 2, BN = 64;
+  constexpr int HT = TM + 2, HW = kTF + 2, NPOS = HT * HW;
+  constexpr int A_BYTES = NPOS * 32;           // one (hi or lo) image
+  constexpr int W_BYTES = 9 * BN * 32;
+  constexpr int W1_BYTES = BN * 32;
+  constexpr int STAGE = 2 * A_BYTES + 2 * W_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wm = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+
+  // XCD-aware block order, as tap_gemm_kernel: the NB channel blocks of a tile run together
+  const int tiles_f = a.F_out / kTF;
+  const int NB = (a.n_cols + BN - 1) / BN;
+  const int n_tiles = ((a.T_out + TM - 1) / TM) * tiles_f;
+  int tile, nb;
+  {
+    const int id = blockIdx.x;
+    const int full = (n_tiles / 8) * 8 * NB;
+    if (id < full) {
+      const int g = id / (8 * NB), r = id - g * 8 * NB;
+      tile = g * 8 + (r & 7);
+      nb = r >> 3;
+    } else {
+      const int r = id - full;
+      tile = (n_tiles / 8) * 8 + r / NB;
+      nb = r % NB;
+    }
+  }
+  const int t0 = (tile / tiles_f) * TM;
+  const int f0 = (tile % tiles_f) * kTF;
+  const int b = blockIdx.z;
+  const int t_in0 = t0 - 1, f_in0 = f0 - 1;
+  const int n_main = a.n_chunks;
+  const uint16_t* wblk = a.w + (int64_t)nb * (n_main * W_BYTES + (XTRA ? a.x_chunks * W1_BYTES : 0));
+  const Src src = pick_src(a.in, 0);
+  const int C = src.C;
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  constexpr int P_ITEMS = (NPOS * 2 + NT - 1) / NT;           // (position, 8-ch half): 16 B hi + 16 B lo
+  constexpr int W16 = (X3 ? 2 : 1) * W_BYTES / 16;
+  constexpr int W_ITEMS = (W16 + NT - 1) / NT;
+  constexpr int X_ITEMS = TM * kTF * 4 / NT;                 // ext: (inner position, 4-ch group) fp32
+  constexpr int W1_16 = (X3 ? 2 : 1) * W1_BYTES / 16;
+  static_assert(2 * P_ITEMS >= X_ITEMS && W_ITEMS >= 1 && W1_16 <= NT, "staging");
+  f32x4 areg[2 * P_ITEMS];
+  u32x4 wreg[W_ITEMS];
+  uint32_t avalid = 0;  // per staging item: inside the input image (else stored as zeros)
+
+  auto load_main = [&](int kc) {
+    const u32x4* wsrc = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * W_BYTES);
+    Unroll<0, W_ITEMS>::run([&](auto I) {
+      const int e = tid + I * NT;
+      wreg[I] = wsrc[e < W16 ? e : W16 - 1];
+    });
+    const int cl0 = kc * kConvBK;
+    Unroll<0, P_ITEMS>::run([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      // straight-line (no branches, so the scheduler can spread it under the MFMAs): surplus
+      // threads repeat the last item; out-of-image halo positions load a clamped address and zero it
+      const int e = min(tid + i * NT, NPOS * 2 - 1);
+      const int p = e >> 1, hf = e & 1;
+      const int hr = p / HW, hc = p - hr * HW;
+      const int ti = t_in0 + hr, fi = f_in0 + hc;
+      const bool ok = ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in;
+      const int tc = min(max(ti, 0), a.T_in - 1), fc = min(max(fi, 0), a.F_in - 1);
+      const int64_t idx = (((int64_t)b * a.T_in + tc) * a.F_in + fc) * C + cl0 + 8 * hf;
+      areg[2 * i] = *reinterpret_cast<const f32x4*>(src.hi + idx);
+      areg[2 * i + 1] = *reinterpret_cast<const f32x4*>(src.lo + idx);
+      if (i == 0) avalid = 0;
+      avalid |= (uint32_t)ok << i;  // zeroing is applied at store time, so nothing waits on the load here
+    });
+  };
+  auto store_main = [&](char* stg) {
+    char* A_hi = stg;
+    char* A_lo = stg + A_BYTES;
+    u32x4* wdst = reinterpret_cast<u32x4*>(stg + 2 * A_BYTES);
+    Unroll<0, W_ITEMS>::run([&](auto I) {
+      const int e = min(tid + I * NT, W16 - 1);  // duplicates write identical values
+      wdst[e] = wreg[I];
+    });
+    Unroll<0, P_ITEMS>::run([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int e = min(tid + i * NT, NPOS * 2 - 1);
+      const int p = e >> 1, hf = e & 1;
+      const int off = p * 32 + ((hf ^ ((p >> 3) & 1)) << 4);
+      const bool ok = (avalid >> i) & 1u;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(A_hi + off) = ok ? areg[2 * i] : z;
+      if (X3) *reinterpret_cast<f32x4*>(A_lo + off) = ok ? areg[2 * i + 1] : z;
+    });
+  };
+  // ext chunk kx (0-based over the shortcut input's channels): raw fp32, inner positions only
+  auto load_ext = [&](int kx) {
+    const u32x4* wsrc =
+        reinterpret_cast<const u32x4*>(wblk + (int64_t)n_main * W_BYTES + (int64_t)kx * W1_BYTES);
+    wreg[0] = wsrc[tid < W1_16 ? tid : W1_16 - 1];
+    const int k0 = kx * kConvBK;
+    const int s = k0 < a.xin.C_split ? 0 : 1;
+    const Src xs = pick_src(a.xin, s);
+    const int cl0 = k0 - (s ? a.xin.C_split : 0);
+    Unroll<0, X_ITEMS>::run([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int e = tid + i * NT;
+      const int p = e >> 2, g = e & 3;
+      const int r = p / kTF, cc = p - r * kTF;
+      const int ti = t0 + r, fi = f0 + cc;
+      const int tc = min(ti, a.T_in - 1);
+      areg[i] = *reinterpret_cast<const f32x4*>(xs.ptr + (((int64_t)b * a.T_in + tc) * a.F_in + fi) * xs.C +
+                                                  cl0 + 4 * g);
+      if (i == 0) avalid = 0;
+      avalid |= (uint32_t)(ti < a.T_in) << i;
+    });
+  };
+  auto store_ext = [&](char* stg) {
+    char* A_hi = stg;
+    char* A_lo = stg + A_BYTES;
+    u32x4* wdst = reinterpret_cast<u32x4*>(stg + 2 * A_BYTES);
+    wdst[min(tid, W1_16 - 1)] = wreg[0];
+    Unroll<0, X_ITEMS>::run([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int e = tid + i * NT;
+      const int pi = e >> 2, g = e & 3;
+      const int r = pi / kTF, cc = pi - r * kTF;
+      const int p = (r + 1) * HW + cc + 1;  // halo coordinates of the centre-tap window
+      const int off = p * 32 + ((((g >> 1) ^ ((p >> 3) & 1))) << 4) + ((g & 1) << 3);
+      const bool ok = (avalid >> i) & 1u;
+      __bf16 hi[4], lo[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) split_bf16(ok ? areg[i][q] : 0.f, hi[q], lo[q]);
+      *reinterpret_cast<uint2*>(A_hi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
+      if (X3) *reinterpret_cast<uint2*>(A_lo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
+    });
+  };
+  // Fragment registers are double-buffered across taps: the LDS reads of tap t+1 are issued before
+  // the MFMAs of tap t, so only the first tap of a chunk waits on LDS latency.
+  struct Frags {
+    bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
+  };
+  auto read_frags = [&](Frags& fr, const char* stg, int dy, int dx, int wt, int wimg) {
+    const char* A_hi = stg;
+    const char* A_lo = stg + A_BYTES;
+    const char* W_hi = stg + 2 * A_BYTES;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * MI + i;
+      const int p = (row + dy) * HW + l32 + dx;
+      const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+      fr.ah[i] = *reinterpret_cast<const bf16x8*>(A_hi + off);
+      if (X3) fr.al[i] = *reinterpret_cast<const bf16x8*>(A_lo + off);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int p = wt * BN + j * 32 + l32;
+      const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+      fr.bh[j] = *reinterpret_cast<const bf16x8*>(W_hi + off);
+      if (X3) fr.bl[j] = *reinterpret_cast<const bf16x8*>(W_hi + wimg + off);
+    }
+  };
+  auto mfmas = [&](const Frags& fr) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        if (X3) {
+          acc[i][j] = mfma32(fr.al[i], fr.bh[j], acc[i][j]);
+          acc[i][j] = mfma32(fr.ah[i], fr.bl[j], acc[i][j]);
+        }
+        acc[i][j] = mfma32(fr.ah[i], fr.bh[j], acc[i][j]);
+      }
+  };
+
+  // ---- main chunks: straight-line pipelined body, clamped (redundant) prefetch at the tail ----
+  load_main(0);
+  store_main(smem);
+  load_main(min(1, n_main - 1));
+  __syncthreads();
+  for (int kc = 0; kc < n_main; ++kc) {
+    char* cur = smem + (kc & 1) * STAGE;
+    char* nxt = smem + ((kc + 1) & 1) * STAGE;
+    Frags fr[2];
+    read_frags(fr[0], cur, 0, 0, 0, W_BYTES);
+    Unroll<0, 9>::run([&](auto T) {
+      constexpr int tap = decltype(T)::value;
+      if (tap + 1 < 9) read_frags(fr[(tap + 1) & 1], cur, (tap + 1) / 3, (tap + 1) % 3, tap + 1, W_BYTES);
+      mfmas(fr[tap & 1]);
+      if (tap == 1) {
+        // stage chunk kc+1 (in registers since the previous iteration) under the MFMAs, then
+        // start loading chunk kc+2; past the end both are harmless repeats of the last chunk
+        store_main(nxt);
+        load_main(min(kc + 2, n_main - 1));
+      }
+    });
+    __syncthreads();
+  }
+  // ---- fused 1x1 shortcut chunks (centre tap), same double-buffered pipeline ----
+  if (XTRA && a.x_chunks > 0) {
+    const int nx = a.x_chunks;
+    load_ext(0);
+    store_ext(smem);
+    load_ext(min(1, nx - 1));
+    __syncthreads();
+    for (int kx = 0; kx < nx; ++kx) {
+      char* cur = smem + (kx & 1) * STAGE;
+      char* nxt = smem + ((kx + 1) & 1) * STAGE;
+      Frags fr;
+      read_frags(fr, cur, 1, 1, 0, W1_BYTES);
+      mfmas(fr);
+      store_ext(nxt);
+      load_ext(min(kx + 2, nx - 1));
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: fp32 store + per-channel sum / sum-of-squares for the next InstanceNorm ----
+  float ssum[NI], ssq[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
+  const int C_out = a.out.C_out;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int co = nb * BN + j * 32 + l32;
+    if (co >= C_out) continue;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int t = t0 + wm * MI + i;
+      if (t >= a.T_out) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = f0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t idx = (((int64_t)b * a.T_out + t) * a.F_out + f) * C_out + co;
+        const float v = acc[i][j][r];
+        a.out.ptr[idx] = v;
+        ssum[j] += v;
+        ssq[j] += v * v;
+      }
+    }
+  }
+  if (a.out.stats) {
+    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2] (the last barrier retired all LDS reads)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      ssum[j] += __shfl_xor(ssum[j], 32);
+      ssq[j] += __shfl_xor(ssq[j], 32);
+      if (h == 0) {
+        const int n = j * 32 + l32;
+        red[(wm * BN + n) * 2 + 0] = ssum[j];
+        red[(wm * BN + n) * 2 + 1] = ssq[j];
+      }
+    }
+    __syncthreads();
+    for (int n = tid; n < BN; n += NT) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s0 += red[(w * BN + n) * 2 + 0];
+        s1 += red[(w * BN + n) * 2 + 1];
+      }
+      const int co = nb * BN + n;
+      if (co < C_out) {
+        double* st = a.out.stats + ((int64_t)b * C_out + co) * 2;
+        atomicAdd(st + 0, (double)s0);
+        atomicAdd(st + 1, (double)s1);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // TDF linear (mdx23c_tfc_tdf_v3.py:113-120) as one GEMM per launch over all (b, t):
 //   D[m][n] = sum_k W[m][k] * act(X[k][n]),  n = (b, t, c) flattened over the whole batch.
 // The weight (M x K, <= 1 MB as hi+lo) is the small operand and stays L2-resident; the workgroup
@@ -818,6 +1111,24 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
                kMaxCin);
   switch (kind) {
     case CONV3X3:
+      if (a.T_out >= 32 && a.out.residual == nullptr && a.out.gelu == 0) {
+        // double-buffered 16-row tile (levels with T >= 32); tile rows past T_out are masked
+        SESA_REQUIRE(a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && a.in.src[0].lo && a.in.C_split == a.in.C_in,
+                     SESA_ERR_INVALID, "conv3x3: needs a single pre-activated (act_split) input");
+        dim3 grid((unsigned)(((a.T_out + 15) / 16) * (a.F_out / kTF) * ((a.n_cols + 63) / 64)), 1u, (unsigned)batch);
+        if (a.x_chunks > 0) {
+          SESA_REQUIRE(a.xin.C_in % kConvBK == 0 && a.xin.C_split % kConvBK == 0 && a.xin.src[0].mode == SRC_RAW &&
+                           a.xin.src[1].mode == SRC_RAW,
+                       SESA_ERR_INVALID, "conv3x3: fused shortcut must be a raw input, C_in multiple of %d", kConvBK);
+          if (x3) hipLaunchKernelGGL((conv3x3_db_kernel<true, true>), grid, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv3x3_db_kernel<false, true>), grid, dim3(512), 0, st, a);
+        } else {
+          if (x3) hipLaunchKernelGGL((conv3x3_db_kernel<true, false>), grid, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv3x3_db_kernel<false, false>), grid, dim3(512), 0, st, a);
+        }
+        SESA_CHECK_LAUNCH();
+        return SESA_OK;
+      }
       if (a.x_chunks > 0) {
         SESA_REQUIRE(a.xin.C_in % kConvBK == 0 && a.xin.C_split % kConvBK == 0, SESA_ERR_INVALID,
                      "conv: fused shortcut C_in %d must be a multiple of %d", a.xin.C_in, kConvBK);
