@@ -119,6 +119,34 @@ int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, float* out, v
 int sesa_mdx23c_destroy(sesa_mdx23c* m);
 
 /* ---------------------------------------------------------------------------------------
+ * BS-Roformer (models/bs_roformer/bs_roformer.py:327-587, BSRoformer).
+ * STFT n_fft = win = 2048 (any hop dividing chunk_size), stereo or mono, dim_head 64,
+ * mask_estimator_depth 2, linear_transformer_depth 0, skip_connection False (released configs).
+ * Parameters are the reference state_dict() keys (incl. layers.*.rotary_embed.freqs).
+ */
+typedef struct sesa_bsr_config {
+  int chunk_size, audio_channels, n_fft, hop_length, win_length;
+  int dim, depth, heads, dim_head, time_transformer_depth, freq_transformer_depth;
+  int num_stems, mask_estimator_depth, mlp_expansion_factor;
+  int n_bands;
+  const int* freqs_per_bands;   /* host array [n_bands], copied by sesa_bsr_create */
+  int precision;                /* SESA_PREC_*                                       */
+} sesa_bsr_config;
+
+typedef struct sesa_bsr sesa_bsr;
+
+int sesa_bsr_create(const sesa_bsr_config* cfg, sesa_bsr** out);
+int sesa_bsr_num_params(const sesa_bsr* m);
+int sesa_bsr_param_info(const sesa_bsr* m, int i, const char** name, int64_t* numel);
+int sesa_bsr_set_param(sesa_bsr* m, const char* name, const float* host, int64_t numel);
+int sesa_bsr_finalize(sesa_bsr* m, void* stream);
+size_t sesa_bsr_workspace_size(const sesa_bsr* m, int batch);
+/* x [batch, audio_channels, chunk_size] -> out [batch, num_stems, audio_channels, chunk_size] */
+int sesa_bsr_forward(sesa_bsr* m, const float* x, int batch, float* out, void* workspace,
+                     size_t workspace_bytes, void* stream);
+int sesa_bsr_destroy(sesa_bsr* m);
+
+/* ---------------------------------------------------------------------------------------
  * Kernel timing (measurement support for bench.py; not part of the reference surface).
  * While enabled, every launch issued by libsesa is bracketed by a hipEvent pair on its own
  * stream and tagged with its kernel class and ALGORITHMIC work (reference FLOPs for the
@@ -133,7 +161,9 @@ int sesa_mdx23c_destroy(sesa_mdx23c* m);
 #define SESA_KCLASS_STFT 5
 #define SESA_KCLASS_ISTFT 6
 #define SESA_KCLASS_ACT 7     /* act_split: norm + GELU + bf16 split pass (work = HBM bytes) */
-#define SESA_KCLASS_COUNT 8
+#define SESA_KCLASS_TOKGEMM 8 /* token-major Linear layers (transformer models)           */
+#define SESA_KCLASS_ATTN 9    /* flash attention (work = 4 L^2 d FLOP per sequence-head)    */
+#define SESA_KCLASS_COUNT 10
 int sesa_profile_enable(int enable);   /* 1: start recording (clears previous records), 0: stop */
 int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work);
 

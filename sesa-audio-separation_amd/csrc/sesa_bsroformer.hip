@@ -1,0 +1,772 @@
+// BS-Roformer (band-split RoPE transformer): parameter registry, weight packing, spectral front /
+// back end and the forward pass (gfx950).
+//
+// Reference: models/bs_roformer/bs_roformer.py:327-587 (BSRoformer), :43-310 (RMSNorm,
+// FeedForward, Attention, Transformer, BandSplit, MaskEstimator), attend.py:76-95 (SDPA).
+// Parameter names / shapes are the reference state_dict keys (incl. the per-layer rotary
+// `freqs`, whose values drive the rotary tables), so released checkpoints load by name.
+//
+// Data layout (all token-major fp32, tokens ordered (b, t, band) = 'b t f d'):
+//   spec  [B*T][F*ch*2]      STFT features in the reference's '(f s) c' order (:495-497)
+//   X     [B*T*nb][dim]      the residual stream; the time transformer's sequences are the strided
+//                            views (b, band) -> t and the freq transformer's (b, t) -> band (:526-543),
+//                            consumed in place by the attention kernel (no rearranges)
+//   QKV   [tokens][3*inner + heads (pad 4)]  q | k | v | gate logits
+//   mask  [stem][B*T][F*ch*2] GLU outputs concatenated over bands (:310)
+// Forward per transformer layer: QKV+gates GEMM (RMSNorm + rotary fused) -> attention (gates
+// fused) -> to_out GEMM (+x) -> FF1 GEMM (RMSNorm, bias, GELU) -> FF2 GEMM (bias, +x).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sesa_common.hpp"
+#include "sesa_internal.hpp"
+#include "sesa_tokgemm.hpp"
+
+namespace sesa {
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// Spectral kernels for n_fft = 2048 (1024-point complex radix-4 Stockham + real split),
+// torch.stft / torch.istft semantics: center=True, reflect pad, periodic Hann(win = n_fft),
+// onesided 1025 bins incl. Nyquist, istft(length = chunk) = OLA / sum(w^2), trimmed.
+constexpr int kN = 2048;
+constexpr int kH = 1024;  // complex FFT length
+constexpr int kFT = 256;  // threads
+
+struct BsrTables {
+  float2* tw = nullptr;   // exp(-2 pi i j / 1024), j < 1024
+  float2* twN = nullptr;  // exp(-2 pi i k / 2048), k <= 1024
+  float* win = nullptr;   // periodic Hann(2048)
+};
+std::mutex g_mu;
+std::vector<BsrTables> g_tabs;
+
+int get_tables(BsrTables* out) {
+  int dev = 0;
+  SESA_CHECK_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_mu);
+  if ((int)g_tabs.size() <= dev) g_tabs.resize(dev + 1);
+  BsrTables& t = g_tabs[dev];
+  if (!t.tw) {
+    std::vector<float2> a(kH), b(kH + 1);
+    std::vector<float> w(kN);
+    for (int j = 0; j < kH; ++j) {
+      const double ang = -2.0 * M_PI * j / kH;
+      a[j] = make_float2((float)cos(ang), (float)sin(ang));
+    }
+    for (int k = 0; k <= kH; ++k) {
+      const double ang = -2.0 * M_PI * k / kN;
+      b[k] = make_float2((float)cos(ang), (float)sin(ang));
+    }
+    for (int n = 0; n < kN; ++n) w[n] = (float)(0.5 - 0.5 * cos(2.0 * M_PI * n / kN));
+    SESA_CHECK_HIP(hipMalloc(&t.tw, kH * sizeof(float2)));
+    SESA_CHECK_HIP(hipMalloc(&t.twN, (kH + 1) * sizeof(float2)));
+    SESA_CHECK_HIP(hipMalloc(&t.win, kN * sizeof(float)));
+    SESA_CHECK_HIP(hipMemcpy(t.tw, a.data(), kH * sizeof(float2), hipMemcpyHostToDevice));
+    SESA_CHECK_HIP(hipMemcpy(t.twN, b.data(), (kH + 1) * sizeof(float2), hipMemcpyHostToDevice));
+    SESA_CHECK_HIP(hipMemcpy(t.win, w.data(), kN * sizeof(float), hipMemcpyHostToDevice));
+  }
+  *out = t;
+  return SESA_OK;
+}
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+
+template <bool INV>
+__device__ float2* fft1024(float2* x, float2* y, const float2* __restrict__ tw) {
+  int n = kH, s = 1;
+#pragma unroll 1
+  for (int stage = 0; stage < 5; ++stage) {
+    const int m = n >> 2;
+    __syncthreads();
+    const int bfly = threadIdx.x;  // 256 butterflies per stage
+    const int q = bfly & (s - 1);
+    const int p = bfly >> __builtin_ctz(s);
+    float2 a = x[q + s * p], b = x[q + s * (p + m)], c = x[q + s * (p + 2 * m)], d = x[q + s * (p + 3 * m)];
+    float2 w1 = tw[p * s], w2 = tw[2 * p * s], w3 = tw[3 * p * s];
+    if (INV) { w1 = cconj(w1); w2 = cconj(w2); w3 = cconj(w3); }
+    const float2 apc = cadd(a, c), amc = csub(a, c), bpd = cadd(b, d), bmd = csub(b, d);
+    const float2 jbmd = INV ? make_float2(-bmd.y, bmd.x) : make_float2(bmd.y, -bmd.x);
+    y[q + s * (4 * p + 0)] = cadd(apc, bpd);
+    y[q + s * (4 * p + 1)] = cmul(w1, cadd(amc, jbmd));
+    y[q + s * (4 * p + 2)] = cmul(w2, csub(apc, bpd));
+    y[q + s * (4 * p + 3)] = cmul(w3, csub(amc, jbmd));
+    float2* t = x; x = y; y = t;
+    n = m;
+    s <<= 2;
+  }
+  __syncthreads();
+  return x;
+}
+
+// x [B][ch][len] -> spec [B][T][F][ch][2], F = 1025 (bs_roformer.py:485-497)
+__global__ void __launch_bounds__(kFT) bsr_stft_kernel(const float* __restrict__ x, int ch, int len, int hop,
+                                                       int frames, BsrTables tb, float* __restrict__ spec) {
+  __shared__ float2 bufA[kH];
+  __shared__ float2 bufB[kH];
+  const int t = blockIdx.x;
+  const int sig = blockIdx.y;  // b * ch + s
+  const int b = sig / ch, s = sig - b * ch;
+  const float* xs = x + (int64_t)sig * len;
+  const int64_t base = (int64_t)t * hop - kN / 2;
+  for (int m = threadIdx.x; m < kH; m += kFT) {
+    float v[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = 2 * m + e;
+      int64_t pos = base + n;
+      if (pos < 0) pos = -pos;
+      if (pos >= len) pos = 2 * (int64_t)(len - 1) - pos;
+      v[e] = xs[pos] * tb.win[n];
+    }
+    bufA[m] = make_float2(v[0], v[1]);
+  }
+  float2* Z = fft1024<false>(bufA, bufB, tb.tw);
+  float* o = spec + ((int64_t)b * frames + t) * (kH + 1) * ch * 2;
+  for (int k = threadIdx.x; k <= kH; k += kFT) {
+    const float2 zk = Z[k & (kH - 1)];
+    const float2 zm = cconj(Z[(kH - k) & (kH - 1)]);
+    const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y + zm.y));
+    const float2 D = csub(zk, zm);
+    const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
+    const float2 X = cadd(E, cmul(tb.twN[k], O));
+    *reinterpret_cast<float2*>(o + ((int64_t)k * ch + s) * 2) = X;
+  }
+}
+
+// (spec * mask) -> windowed inverse frames; sig = (b * stems + n) * ch + s  (:560-577)
+__global__ void __launch_bounds__(kFT) bsr_istft_frames_kernel(const float* __restrict__ spec,
+                                                                const float* __restrict__ mask, int ch, int stems,
+                                                                int B, int frames, BsrTables tb,
+                                                                float* __restrict__ frame_ws) {
+  __shared__ float2 bufA[kH];
+  __shared__ float2 bufB[kH + 1];
+  const int t = blockIdx.x;
+  const int sig = blockIdx.y;
+  const int s = sig % ch, bn = sig / ch;
+  const int n = bn % stems, b = bn / stems;
+  const int64_t row = (int64_t)b * frames + t;
+  const int64_t feat = (int64_t)(kH + 1) * ch * 2;
+  const float* sp = spec + row * feat;
+  const float* mk = mask + ((int64_t)n * B * frames + row) * feat;
+  for (int k = threadIdx.x; k <= kH; k += kFT) {
+    const float2 X = *reinterpret_cast<const float2*>(sp + ((int64_t)k * ch + s) * 2);
+    const float2 Mk = *reinterpret_cast<const float2*>(mk + ((int64_t)k * ch + s) * 2);
+    float2 Y = cmul(X, Mk);
+    if (k == 0 || k == kH) Y.y = 0.f;  // C2R ignores the imaginary parts of DC and Nyquist
+    bufB[k] = Y;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < kH; k += kFT) {
+    const float2 xk = bufB[k];
+    const float2 xm = cconj(bufB[kH - k]);
+    const float2 E = make_float2(0.5f * (xk.x + xm.x), 0.5f * (xk.y + xm.y));
+    const float2 w = cconj(tb.twN[k]);
+    const float2 D = csub(xk, xm);
+    const float2 O = cmul(make_float2(0.5f * D.x, 0.5f * D.y), w);
+    bufA[k] = make_float2(E.x - O.y, E.y + O.x);
+  }
+  __syncthreads();  // bufB is reused as the FFT ping-pong buffer
+  float2* z = fft1024<true>(bufA, bufB, tb.tw);
+  float* fw = frame_ws + ((int64_t)sig * frames + t) * kN;
+  const float scale = 1.0f / (float)kH;
+  for (int m = threadIdx.x; m < kH; m += kFT) {
+    const float2 v = z[m];
+    reinterpret_cast<float2*>(fw)[m] = make_float2(v.x * scale * tb.win[2 * m], v.y * scale * tb.win[2 * m + 1]);
+  }
+}
+
+__global__ void bsr_istft_ola_kernel(const float* __restrict__ frame_ws, int frames, int hop, int out_len,
+                                     const float* __restrict__ win, float* __restrict__ out) {
+  const int sig = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= out_len) return;
+  const int n = j + kN / 2;
+  const int t_lo = n - kN + 1 <= 0 ? 0 : (n - kN + hop) / hop;
+  int t_hi = n / hop;
+  if (t_hi > frames - 1) t_hi = frames - 1;
+  const float* fw = frame_ws + (int64_t)sig * frames * kN;
+  float acc = 0.f, env = 0.f;
+  for (int t = t_lo; t <= t_hi; ++t) {
+    const int o = n - t * hop;
+    acc += fw[(int64_t)t * kN + o];
+    const float w = win[o];
+    env += w * w;
+  }
+  out[(int64_t)sig * out_len + j] = acc / env;
+}
+
+// ---------------------------------------------------------------------------------------------
+uint16_t f2bf(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+float bf2f(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+struct Param {
+  std::string name;
+  std::vector<int64_t> shape;
+  int64_t numel = 0;
+  std::vector<float> host;
+  bool set = false;
+};
+
+struct Gemm {          // one packed (possibly grouped) GEMM
+  std::vector<TokGroup> groups;
+  TokGroup* d_groups = nullptr;
+  int n_tiles_n = 0;
+};
+
+struct Layer {         // one transformer layer (Attention + FeedForward)
+  std::string prefix;  // layers.i.j.layers.l
+  int time = 1;
+  Gemm qkv, out, ff1, ff2;
+  int64_t rope_off = 0;  // float2 offset into the rope blob
+};
+
+}  // namespace
+}  // namespace sesa
+
+struct sesa_bsr {
+  sesa_bsr_config cfg;
+  std::vector<int> fpb;  // freqs per band
+  std::vector<int> dims; // band input dims 2*f*ch
+  std::vector<int> offs; // band feature offsets
+  int nb = 0, F = 0, T = 0, inner = 0, ff = 0, hidden = 0, qkv_ld = 0, feat = 0;
+  std::vector<sesa::Param> params;
+  std::map<std::string, int> by_name;
+  std::vector<sesa::Layer> layers;
+  sesa::Gemm band, mlp1, mlp2;  // mlp1/mlp2 hold stems * nb groups
+  uint16_t* d_w = nullptr;
+  float* d_bias = nullptr;
+  float2* d_rope = nullptr;
+  bool finalized = false;
+};
+
+namespace sesa {
+namespace {
+
+int add_param(sesa_bsr* m, const std::string& name, std::vector<int64_t> shape) {
+  Param p;
+  p.name = name;
+  p.shape = shape;
+  p.numel = 1;
+  for (auto s : shape) p.numel *= s;
+  m->by_name[name] = (int)m->params.size();
+  m->params.push_back(std::move(p));
+  return (int)m->params.size() - 1;
+}
+
+const std::vector<float>& P(sesa_bsr* m, const std::string& name) { return m->params[m->by_name.at(name)].host; }
+
+// Pack W[n][k] (row accessor) of an N x K GEMM for one group; returns the TokGroup with w_off/b_off set.
+template <class RowFn, class BiasFn>
+TokGroup pack_group(int N, int K, RowFn row_val, bool has_bias, BiasFn bias_val, std::vector<uint16_t>& blob,
+                    std::vector<float>& bias) {
+  TokGroup g{};
+  g.K = K;
+  g.N = N;
+  g.w_off = (int64_t)blob.size();
+  const int nt = (N + kTokBN - 1) / kTokBN, nch = (K + kTokBK - 1) / kTokBK;
+  const int64_t img = (int64_t)kTokBN * kTokBK;
+  blob.resize(blob.size() + (size_t)nt * nch * 2 * img, 0);
+  uint16_t* base = blob.data() + g.w_off;
+  for (int t = 0; t < nt; ++t)
+    for (int kc = 0; kc < nch; ++kc) {
+      uint16_t* hi = base + ((int64_t)t * nch + kc) * 2 * img;
+      uint16_t* lo = hi + img;
+      for (int r = 0; r < kTokBN; ++r) {
+        const int n = t * kTokBN + r;
+        for (int kk = 0; kk < kTokBK; ++kk) {
+          const int k = kc * kTokBK + kk;
+          const float v = (n < N && k < K) ? row_val(n, k) : 0.f;
+          const int64_t o = (int64_t)r * kTokBK + (((kk >> 3) ^ ((r >> 2) & 3)) << 3) + (kk & 7);
+          const uint16_t h = f2bf(v);
+          hi[o] = h;
+          lo[o] = f2bf(v - bf2f(h));
+        }
+      }
+    }
+  g.b_off = -1;
+  if (has_bias) {
+    g.b_off = (int64_t)bias.size();
+    for (int n = 0; n < N; ++n) bias.push_back(bias_val(n));
+    while (bias.size() % 4) bias.push_back(0.f);
+  }
+  return g;
+}
+
+int upload_groups(Gemm& gm) {
+  if (gm.d_groups) (void)hipFree(gm.d_groups);
+  SESA_CHECK_HIP(hipMalloc(&gm.d_groups, gm.groups.size() * sizeof(TokGroup)));
+  SESA_CHECK_HIP(hipMemcpy(gm.d_groups, gm.groups.data(), gm.groups.size() * sizeof(TokGroup), hipMemcpyHostToDevice));
+  gm.n_tiles_n = 0;
+  for (auto& g : gm.groups) gm.n_tiles_n = std::max(gm.n_tiles_n, (g.N + kTokBN - 1) / kTokBN);
+  return SESA_OK;
+}
+
+}  // namespace
+}  // namespace sesa
+
+using namespace sesa;
+
+extern "C" int sesa_bsr_create(const sesa_bsr_config* cfg, sesa_bsr** out) {
+  clear_error();
+  SESA_REQUIRE(cfg && out && cfg->freqs_per_bands && cfg->n_bands > 1, SESA_ERR_INVALID, "sesa_bsr_create: bad arguments");
+  const sesa_bsr_config& c = *cfg;
+  SESA_REQUIRE(c.n_fft == 2048 && c.win_length == 2048, SESA_ERR_INVALID, "bsr: only n_fft = win_length = 2048");
+  SESA_REQUIRE(c.hop_length > 0 && c.chunk_size % c.hop_length == 0 && c.chunk_size > c.n_fft / 2, SESA_ERR_INVALID,
+               "bsr: chunk_size must be a multiple of hop_length and > n_fft/2");
+  SESA_REQUIRE(c.audio_channels == 1 || c.audio_channels == 2, SESA_ERR_INVALID, "bsr: audio_channels 1 or 2");
+  SESA_REQUIRE(c.dim_head == 64, SESA_ERR_INVALID, "bsr: dim_head must be 64 (attention kernel)");
+  SESA_REQUIRE(c.dim % 4 == 0 && c.heads >= 1 && c.depth >= 1 && c.num_stems >= 1, SESA_ERR_INVALID, "bsr: bad dims");
+  SESA_REQUIRE(c.mask_estimator_depth == 2, SESA_ERR_INVALID, "bsr: mask_estimator_depth 2 only (released configs)");
+  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16, SESA_ERR_INVALID, "bsr: precision");
+  sesa_bsr* m = new sesa_bsr();
+  m->cfg = c;
+  m->fpb.assign(c.freqs_per_bands, c.freqs_per_bands + c.n_bands);
+  m->cfg.freqs_per_bands = nullptr;
+  int sum = 0, off = 0;
+  for (int f : m->fpb) {
+    sum += f;
+    m->dims.push_back(2 * f * c.audio_channels);
+    m->offs.push_back(off);
+    off += 2 * f * c.audio_channels;
+  }
+  if (sum != c.n_fft / 2 + 1) {
+    delete m;
+    set_error("bsr: freqs_per_bands sums to %d, expected %d", sum, c.n_fft / 2 + 1);
+    return SESA_ERR_INVALID;
+  }
+  m->nb = c.n_bands;
+  m->F = c.n_fft / 2 + 1;
+  m->T = c.chunk_size / c.hop_length + 1;
+  m->inner = c.heads * c.dim_head;
+  m->ff = c.dim * 4;
+  m->hidden = c.dim * c.mlp_expansion_factor;
+  m->qkv_ld = (3 * m->inner + c.heads + 3) / 4 * 4;
+  m->feat = m->F * c.audio_channels * 2;
+  const int dim = c.dim, inner = m->inner;
+  for (int i = 0; i < c.depth; ++i)
+    for (int j = 0; j < 2; ++j) {
+      const int dep = j == 0 ? c.time_transformer_depth : c.freq_transformer_depth;
+      for (int l = 0; l < dep; ++l) {
+        const std::string p = "layers." + std::to_string(i) + "." + std::to_string(j) + ".layers." + std::to_string(l);
+        add_param(m, p + ".0.rotary_embed.freqs", {c.dim_head / 2});
+        add_param(m, p + ".0.norm.gamma", {dim});
+        add_param(m, p + ".0.to_qkv.weight", {3 * inner, dim});
+        add_param(m, p + ".0.to_gates.weight", {c.heads, dim});
+        add_param(m, p + ".0.to_gates.bias", {c.heads});
+        add_param(m, p + ".0.to_out.0.weight", {dim, inner});
+        add_param(m, p + ".1.net.0.gamma", {dim});
+        add_param(m, p + ".1.net.1.weight", {m->ff, dim});
+        add_param(m, p + ".1.net.1.bias", {m->ff});
+        add_param(m, p + ".1.net.4.weight", {dim, m->ff});
+        add_param(m, p + ".1.net.4.bias", {dim});
+        Layer L;
+        L.prefix = p;
+        L.time = j == 0;
+        m->layers.push_back(L);
+      }
+    }
+  add_param(m, "final_norm.gamma", {dim});
+  for (int b = 0; b < m->nb; ++b) {
+    const std::string p = "band_split.to_features." + std::to_string(b);
+    add_param(m, p + ".0.gamma", {m->dims[b]});
+    add_param(m, p + ".1.weight", {dim, m->dims[b]});
+    add_param(m, p + ".1.bias", {dim});
+  }
+  for (int n = 0; n < c.num_stems; ++n)
+    for (int b = 0; b < m->nb; ++b) {
+      const std::string p = "mask_estimators." + std::to_string(n) + ".to_freqs." + std::to_string(b) + ".0";
+      add_param(m, p + ".0.weight", {m->hidden, dim});
+      add_param(m, p + ".0.bias", {m->hidden});
+      add_param(m, p + ".2.weight", {2 * m->dims[b], m->hidden});
+      add_param(m, p + ".2.bias", {2 * m->dims[b]});
+    }
+  *out = m;
+  return SESA_OK;
+}
+
+extern "C" int sesa_bsr_num_params(const sesa_bsr* m) { return m ? (int)m->params.size() : 0; }
+
+extern "C" int sesa_bsr_param_info(const sesa_bsr* m, int i, const char** name, int64_t* numel) {
+  clear_error();
+  SESA_REQUIRE(m && i >= 0 && i < (int)m->params.size(), SESA_ERR_INVALID, "bsr param_info: index out of range");
+  if (name) *name = m->params[i].name.c_str();
+  if (numel) *numel = m->params[i].numel;
+  return SESA_OK;
+}
+
+extern "C" int sesa_bsr_set_param(sesa_bsr* m, const char* name, const float* host, int64_t numel) {
+  clear_error();
+  SESA_REQUIRE(m && name && host, SESA_ERR_INVALID, "bsr set_param: null argument");
+  auto it = m->by_name.find(name);
+  SESA_REQUIRE(it != m->by_name.end(), SESA_ERR_INVALID, "bsr set_param: unknown parameter '%s'", name);
+  Param& p = m->params[it->second];
+  SESA_REQUIRE(p.numel == numel, SESA_ERR_INVALID, "bsr set_param: '%s' expects %lld elements, got %lld", name,
+               (long long)p.numel, (long long)numel);
+  p.host.assign(host, host + numel);
+  p.set = true;
+  m->finalized = false;
+  return SESA_OK;
+}
+
+extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
+  clear_error();
+  SESA_REQUIRE(m, SESA_ERR_INVALID, "bsr finalize: null model");
+  for (auto& p : m->params)
+    SESA_REQUIRE(p.set, SESA_ERR_STATE, "bsr finalize: parameter '%s' was never set", p.name.c_str());
+  const sesa_bsr_config& c = m->cfg;
+  const int dim = c.dim, inner = m->inner;
+  std::vector<uint16_t> blob;
+  std::vector<float> bias;
+  std::vector<float2> rope;
+  // band split: W' = W diag(gamma) (RMSNorm folded)
+  m->band.groups.clear();
+  for (int b = 0; b < m->nb; ++b) {
+    const std::string p = "band_split.to_features." + std::to_string(b);
+    const auto& W = P(m, p + ".1.weight");
+    const auto& G = P(m, p + ".0.gamma");
+    const auto& Bv = P(m, p + ".1.bias");
+    const int K = m->dims[b];
+    TokGroup g = pack_group(dim, K, [&](int n, int k) { return W[(int64_t)n * K + k] * G[k]; }, true,
+                            [&](int n) { return Bv[n]; }, blob, bias);
+    g.x_off = m->offs[b];
+    g.o_off = (int64_t)b * dim;
+    m->band.groups.push_back(g);
+  }
+  for (auto& L : m->layers) {
+    const std::string& p = L.prefix;
+    const auto& Wqkv = P(m, p + ".0.to_qkv.weight");
+    const auto& Wg = P(m, p + ".0.to_gates.weight");
+    const auto& bg = P(m, p + ".0.to_gates.bias");
+    const auto& ga = P(m, p + ".0.norm.gamma");
+    const int Nq = 3 * inner + c.heads;
+    TokGroup g = pack_group(
+        Nq, dim,
+        [&](int n, int k) {
+          return (n < 3 * inner ? Wqkv[(int64_t)n * dim + k] : Wg[(int64_t)(n - 3 * inner) * dim + k]) * ga[k];
+        },
+        true, [&](int n) { return n < 3 * inner ? 0.f : bg[n - 3 * inner]; }, blob, bias);
+    g.x_off = 0;
+    g.o_off = 0;
+    L.qkv.groups = {g};
+    const auto& Wo = P(m, p + ".0.to_out.0.weight");
+    g = pack_group(dim, inner, [&](int n, int k) { return Wo[(int64_t)n * inner + k]; }, false, [](int) { return 0.f; },
+                   blob, bias);
+    g.x_off = g.o_off = 0;
+    L.out.groups = {g};
+    const auto& W1 = P(m, p + ".1.net.1.weight");
+    const auto& b1 = P(m, p + ".1.net.1.bias");
+    const auto& gf = P(m, p + ".1.net.0.gamma");
+    g = pack_group(m->ff, dim, [&](int n, int k) { return W1[(int64_t)n * dim + k] * gf[k]; }, true,
+                   [&](int n) { return b1[n]; }, blob, bias);
+    g.x_off = g.o_off = 0;
+    L.ff1.groups = {g};
+    const auto& W2 = P(m, p + ".1.net.4.weight");
+    const auto& b2 = P(m, p + ".1.net.4.bias");
+    const int ffd = m->ff;
+    g = pack_group(dim, ffd, [&](int n, int k) { return W2[(int64_t)n * ffd + k]; }, true, [&](int n) { return b2[n]; },
+                   blob, bias);
+    g.x_off = g.o_off = 0;
+    L.ff2.groups = {g};
+    // rotary table from this layer's freqs: angle = fp32(pos * freq) (the library's fp32 einsum)
+    const auto& fr = P(m, p + ".0.rotary_embed.freqs");
+    const int npos = L.time ? m->T : m->nb;
+    L.rope_off = (int64_t)rope.size();
+    for (int pos = 0; pos < npos; ++pos)
+      for (int i = 0; i < c.dim_head / 2; ++i) {
+        const float ang = (float)pos * fr[i];
+        rope.push_back(make_float2((float)cos((double)ang), (float)sin((double)ang)));
+      }
+  }
+  // mask estimators: final RMSNorm gamma folded into every band's first Linear; second Linear's
+  // rows interleaved (a_j, b_j) so the GLU pairs sit in adjacent columns
+  const auto& gfin = P(m, "final_norm.gamma");
+  m->mlp1.groups.clear();
+  m->mlp2.groups.clear();
+  const int hid = m->hidden;
+  for (int n = 0; n < c.num_stems; ++n)
+    for (int b = 0; b < m->nb; ++b) {
+      const std::string p = "mask_estimators." + std::to_string(n) + ".to_freqs." + std::to_string(b) + ".0";
+      const auto& W1 = P(m, p + ".0.weight");
+      const auto& b1 = P(m, p + ".0.bias");
+      TokGroup g = pack_group(hid, dim, [&](int r, int k) { return W1[(int64_t)r * dim + k] * gfin[k]; }, true,
+                              [&](int r) { return b1[r]; }, blob, bias);
+      g.x_off = (int64_t)b * dim;
+      g.o_off = (int64_t)b * hid;
+      m->mlp1.groups.push_back(g);
+      const auto& W2 = P(m, p + ".2.weight");
+      const auto& b2 = P(m, p + ".2.bias");
+      const int din = m->dims[b];
+      auto src_row = [din](int r) { return (r & 1) ? din + (r >> 1) : (r >> 1); };
+      g = pack_group(2 * din, hid, [&](int r, int k) { return W2[(int64_t)src_row(r) * hid + k]; }, true,
+                     [&](int r) { return b2[src_row(r)]; }, blob, bias);
+      g.x_off = (int64_t)b * hid;
+      g.o_off = m->offs[b];
+      m->mlp2.groups.push_back(g);
+    }
+  if (m->d_w) (void)hipFree(m->d_w);
+  if (m->d_bias) (void)hipFree(m->d_bias);
+  if (m->d_rope) (void)hipFree(m->d_rope);
+  m->d_w = nullptr;
+  m->d_bias = nullptr;
+  m->d_rope = nullptr;
+  SESA_REQUIRE(hipMalloc(&m->d_w, blob.size() * 2) == hipSuccess, SESA_ERR_NOMEM, "bsr finalize: hipMalloc weights");
+  SESA_REQUIRE(hipMalloc(&m->d_bias, std::max<size_t>(bias.size(), 1) * 4) == hipSuccess, SESA_ERR_NOMEM,
+               "bsr finalize: hipMalloc bias");
+  SESA_REQUIRE(hipMalloc(&m->d_rope, std::max<size_t>(rope.size(), 1) * sizeof(float2)) == hipSuccess, SESA_ERR_NOMEM,
+               "bsr finalize: hipMalloc rope");
+  hipStream_t st = as_stream(stream);
+  SESA_CHECK_HIP(hipMemcpyAsync(m->d_w, blob.data(), blob.size() * 2, hipMemcpyHostToDevice, st));
+  if (!bias.empty()) SESA_CHECK_HIP(hipMemcpyAsync(m->d_bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice, st));
+  if (!rope.empty())
+    SESA_CHECK_HIP(hipMemcpyAsync(m->d_rope, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice, st));
+  SESA_CHECK_HIP(hipStreamSynchronize(st));
+  int rc = upload_groups(m->band);
+  if (!rc) rc = upload_groups(m->mlp1);
+  if (!rc) rc = upload_groups(m->mlp2);
+  for (auto& L : m->layers) {
+    if (!rc) rc = upload_groups(L.qkv);
+    if (!rc) rc = upload_groups(L.out);
+    if (!rc) rc = upload_groups(L.ff1);
+    if (!rc) rc = upload_groups(L.ff2);
+  }
+  if (rc) return rc;
+  BsrTables tb;
+  rc = get_tables(&tb);
+  if (rc) return rc;
+  m->finalized = true;
+  return SESA_OK;
+}
+
+namespace {
+
+struct Plan {
+  size_t spec, x, qkv, ao, h, mask, frames, total;
+};
+
+Plan plan(const sesa_bsr* m, int B) {
+  auto al = [](size_t n) { return (n * 4 + 255) & ~(size_t)255; };
+  const int64_t tok = (int64_t)B * m->T * m->nb;
+  Plan p{};
+  size_t off = 0;
+  p.spec = off; off += al((size_t)B * m->T * m->feat);
+  p.x = off; off += al((size_t)tok * m->cfg.dim);
+  p.qkv = off; off += al((size_t)tok * m->qkv_ld);
+  p.ao = off; off += al((size_t)tok * m->inner);
+  p.h = off; off += al((size_t)tok * std::max(m->ff, m->hidden));
+  p.mask = off; off += al((size_t)m->cfg.num_stems * B * m->T * m->feat);
+  p.frames = off; off += al((size_t)B * m->cfg.num_stems * m->cfg.audio_channels * m->T * kN);
+  p.total = off;
+  return p;
+}
+
+TokGemmArgs gemm_args(const sesa_bsr* m, const Gemm& gm, const float* x, int64_t x_ld, float* out, int64_t o_ld,
+                      int M) {
+  TokGemmArgs a{};
+  a.x = x;
+  a.x_ld = x_ld;
+  a.out = out;
+  a.o_ld = o_ld;
+  a.w = m->d_w;
+  a.bias = m->d_bias;
+  a.groups = gm.d_groups;
+  a.n_groups = (int)gm.groups.size();
+  a.n_tiles_n = gm.n_tiles_n;
+  a.M = M;
+  a.act = TOK_ACT_NONE;
+  a.dim_head = m->cfg.dim_head;
+  return a;
+}
+
+double gemm_flops(const Gemm& gm, int64_t M) {
+  double f = 0;
+  for (auto& g : gm.groups) f += 2.0 * (double)M * g.N * g.K;
+  return f;
+}
+
+}  // namespace
+
+extern "C" size_t sesa_bsr_workspace_size(const sesa_bsr* m, int batch) {
+  if (!m || batch <= 0) return 0;
+  return plan(m, batch).total;
+}
+
+extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+  clear_error();
+  SESA_REQUIRE(m && x && out && workspace && B > 0, SESA_ERR_INVALID, "bsr forward: bad arguments");
+  SESA_REQUIRE(m->finalized, SESA_ERR_STATE, "bsr forward: call sesa_bsr_finalize first");
+  const Plan pl = plan(m, B);
+  SESA_REQUIRE(workspace_bytes >= pl.total, SESA_ERR_INVALID, "bsr forward: workspace %zu < required %zu",
+               workspace_bytes, pl.total);
+  const sesa_bsr_config& c = m->cfg;
+  hipStream_t st = as_stream(stream);
+  char* ws = reinterpret_cast<char*>(workspace);
+  float* spec = reinterpret_cast<float*>(ws + pl.spec);
+  float* X = reinterpret_cast<float*>(ws + pl.x);
+  float* QKV = reinterpret_cast<float*>(ws + pl.qkv);
+  float* AO = reinterpret_cast<float*>(ws + pl.ao);
+  float* H = reinterpret_cast<float*>(ws + pl.h);
+  float* MASK = reinterpret_cast<float*>(ws + pl.mask);
+  float* FR = reinterpret_cast<float*>(ws + pl.frames);
+  const int x3 = c.precision == SESA_PREC_BF16X3 ? 1 : 0;
+  const int ch = c.audio_channels, dim = c.dim;
+  const int T = m->T, nb = m->nb;
+  const int64_t Mtok = (int64_t)B * T * nb;
+  SESA_REQUIRE(Mtok < (1ll << 31), SESA_ERR_INVALID, "bsr forward: batch too large");
+  const int M = (int)Mtok;
+  BsrTables tb;
+  int rc = get_tables(&tb);
+  if (rc) return rc;
+
+  void* tok = profile_begin(st);
+  hipLaunchKernelGGL(bsr_stft_kernel, dim3(T, B * ch), dim3(kFT), 0, st, x, ch, c.chunk_size, c.hop_length, T, tb, spec);
+  SESA_CHECK_LAUNCH();
+  profile_end(tok, st, SESA_KCLASS_STFT, 4.0 * B * ch * ((double)c.chunk_size + (double)T * m->F * 2));
+
+  auto gemm = [&](const TokGemmArgs& a, const Gemm& gm, int64_t rows) {
+    if (rc) return;
+    void* t0 = profile_begin(st);
+    rc = launch_tok_gemm(a, x3, st);
+    profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(gm, rows));
+  };
+  // band split: rows (b, t), groups over bands -> X rows (b, t, band)
+  {
+    TokGemmArgs a = gemm_args(m, m->band, spec, m->feat, X, (int64_t)nb * dim, B * T);
+    a.rownorm = 1;
+    gemm(a, m->band, B * T);
+  }
+  for (auto& L : m->layers) {
+    // attention: QKV + gates (RMSNorm, rotary on q/k)
+    {
+      TokGemmArgs a = gemm_args(m, L.qkv, X, dim, QKV, m->qkv_ld, M);
+      a.rownorm = 1;
+      a.rope = m->d_rope + L.rope_off;
+      a.rope_cols = 2 * m->inner;
+      a.pos_F = nb;
+      a.pos_T = T;
+      a.pos_time = L.time;
+      gemm(a, L.qkv, M);
+    }
+    if (rc) return rc;
+    {
+      AttnArgs a{};
+      a.qkv = QKV;
+      a.ld = m->qkv_ld;
+      a.k_off = m->inner;
+      a.v_off = 2 * m->inner;
+      a.g_off = 3 * m->inner;
+      a.out = AO;
+      a.o_ld = m->inner;
+      a.heads = c.heads;
+      if (L.time) {  // sequences (b, band) over t
+        a.L = T;
+        a.n_seq = B * nb;
+        a.sdiv = nb;
+        a.smul_a = (int64_t)T * nb;
+        a.smul_b = 1;
+        a.pstride = nb;
+      } else {       // sequences (b, t) over bands
+        a.L = nb;
+        a.n_seq = B * T;
+        a.sdiv = 1;
+        a.smul_a = nb;
+        a.smul_b = 0;
+        a.pstride = 1;
+      }
+      void* t0 = profile_begin(st);
+      rc = launch_attention(a, x3, st);
+      profile_end(t0, st, SESA_KCLASS_ATTN, 4.0 * (double)a.n_seq * c.heads * (double)a.L * a.L * c.dim_head);
+    }
+    {
+      TokGemmArgs a = gemm_args(m, L.out, AO, m->inner, X, dim, M);
+      a.residual = X;
+      gemm(a, L.out, M);
+    }
+    {
+      TokGemmArgs a = gemm_args(m, L.ff1, X, dim, H, m->ff, M);
+      a.rownorm = 1;
+      a.act = TOK_ACT_GELU;
+      gemm(a, L.ff1, M);
+    }
+    {
+      TokGemmArgs a = gemm_args(m, L.ff2, H, m->ff, X, dim, M);
+      a.residual = X;
+      gemm(a, L.ff2, M);
+    }
+    if (rc) return rc;
+  }
+  // mask estimators (final RMSNorm folded into MLP1); per stem: MLP1 (tanh) then MLP2 (GLU)
+  for (int n = 0; n < c.num_stems && !rc; ++n) {
+    Gemm g1, g2;
+    g1.groups.assign(m->mlp1.groups.begin() + n * nb, m->mlp1.groups.begin() + (n + 1) * nb);
+    g2.groups.assign(m->mlp2.groups.begin() + n * nb, m->mlp2.groups.begin() + (n + 1) * nb);
+    TokGemmArgs a = gemm_args(m, m->mlp1, X, (int64_t)nb * dim, H, (int64_t)nb * m->hidden, B * T);
+    a.groups = m->mlp1.d_groups + n * nb;
+    a.n_groups = nb;
+    a.rownorm = 1;
+    a.act = TOK_ACT_TANH;
+    gemm(a, g1, B * T);
+    TokGemmArgs b = gemm_args(m, m->mlp2, H, (int64_t)nb * m->hidden, MASK + (int64_t)n * B * T * m->feat, m->feat,
+                              B * T);
+    b.groups = m->mlp2.d_groups + n * nb;
+    b.n_groups = nb;
+    b.glu = 1;
+    gemm(b, g2, B * T);
+  }
+  if (rc) return rc;
+  const int n_sig = B * c.num_stems * ch;
+  tok = profile_begin(st);
+  hipLaunchKernelGGL(bsr_istft_frames_kernel, dim3(T, n_sig), dim3(kFT), 0, st, spec, MASK, ch, c.num_stems, B, T, tb,
+                     FR);
+  SESA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bsr_istft_ola_kernel, dim3((c.chunk_size + 255) / 256, n_sig), dim3(256), 0, st, FR, T,
+                     c.hop_length, c.chunk_size, tb.win, out);
+  SESA_CHECK_LAUNCH();
+  profile_end(tok, st, SESA_KCLASS_ISTFT, 4.0 * n_sig * ((double)T * m->F * 4 + 2.0 * T * kN + c.chunk_size));
+  return SESA_OK;
+}
+
+extern "C" int sesa_bsr_destroy(sesa_bsr* m) {
+  if (!m) return SESA_OK;
+  if (m->d_w) (void)hipFree(m->d_w);
+  if (m->d_bias) (void)hipFree(m->d_bias);
+  if (m->d_rope) (void)hipFree(m->d_rope);
+  auto fr = [](Gemm& g) {
+    if (g.d_groups) (void)hipFree(g.d_groups);
+  };
+  fr(m->band);
+  fr(m->mlp1);
+  fr(m->mlp2);
+  for (auto& L : m->layers) {
+    fr(L.qkv);
+    fr(L.out);
+    fr(L.ff1);
+    fr(L.ff2);
+  }
+  delete m;
+  return SESA_OK;
+}

@@ -21,6 +21,13 @@ class SesaMdx23cConfig(ctypes.Structure):
         "growth", "bottleneck_factor", "scale_t", "scale_f", "num_instruments", "precision")]
 
 
+class SesaBsrConfig(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "chunk_size", "audio_channels", "n_fft", "hop_length", "win_length", "dim", "depth", "heads", "dim_head",
+        "time_transformer_depth", "freq_transformer_depth", "num_stems", "mask_estimator_depth",
+        "mlp_expansion_factor", "n_bands")] + [("freqs_per_bands", ctypes.POINTER(c_int)), ("precision", c_int)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/sesa.h
 SIGNATURES = {
     "sesa_version": (c_int, []),
@@ -40,12 +47,21 @@ SIGNATURES = {
     "sesa_mdx23c_workspace_size": (c_size_t, [c_void_p, c_int]),
     "sesa_mdx23c_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
     "sesa_mdx23c_destroy": (c_int, [c_void_p]),
+    "sesa_bsr_create": (c_int, [ctypes.POINTER(SesaBsrConfig), ctypes.POINTER(c_void_p)]),
+    "sesa_bsr_num_params": (c_int, [c_void_p]),
+    "sesa_bsr_param_info": (c_int, [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64)]),
+    "sesa_bsr_set_param": (c_int, [c_void_p, c_char_p, P_f32, c_int64]),
+    "sesa_bsr_finalize": (c_int, [c_void_p, c_void_p]),
+    "sesa_bsr_workspace_size": (c_size_t, [c_void_p, c_int]),
+    "sesa_bsr_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
+    "sesa_bsr_destroy": (c_int, [c_void_p]),
     "sesa_profile_enable": (c_int, [c_int]),
     "sesa_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
                                   ctypes.POINTER(ctypes.c_double)]),
 }
 
-KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6, "act": 7}
+KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6, "act": 7, "tokgemm": 8,
+          "attn": 9}
 
 
 def profile_enable(on):

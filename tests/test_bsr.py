@@ -1,0 +1,114 @@
+"""BS-Roformer on the native path.
+
+CPU (no device work): the Python and native parameter registries both equal the reference
+state_dict keys.  GPU (marked ``gpu``): the native forward / demix against the golden vectors of
+the real reference (tests/golden/make_golden_bsr.py), per-sample RMS <= 1e-4 (north_star gate)
+in bf16x3; the bf16 throughput mode is measured and reported, not gated.
+"""
+import contextlib
+import ctypes
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import CONFIGS, GOLDEN, rms
+
+RMS_GATE = 1e-4
+
+
+def _model(cfg_name, affine="random", precision="bf16x3"):
+    from oracle import bs_roformer as ob
+    from sesa.utils import get_model_from_config
+    m, c = get_model_from_config("bs_roformer", os.path.join(CONFIGS, cfg_name))
+    sd = ob.synth_params(ob.load_cfg(os.path.join(CONFIGS, cfg_name)), affine)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    m.set_precision(precision)
+    return m, c
+
+
+@pytest.mark.parametrize("cfg_name,tag", [("config_bs_roformer_vocals.yaml", "vocals"),
+                                          ("config_bs_roformer_small.yaml", "small")])
+def test_registry_matches_reference_state_dict(cfg_name, tag):
+    from sesa import _native as N
+    from sesa.utils import get_model_from_config
+    m, c = get_model_from_config("bs_roformer", os.path.join(CONFIGS, cfg_name))
+    with open(os.path.join(GOLDEN, f"params_bsr_{tag}.json")) as f:
+        ref = [(n, tuple(s)) for n, s in json.load(f)]
+    assert [(n, tuple(t.shape)) for n, t in m.named_parameters()] == ref
+    h = m._create(c.audio.chunk_size)          # host-side plan only: no device allocation
+    try:
+        names = []
+        for i in range(N.lib().sesa_bsr_num_params(h)):
+            nm, numel = ctypes.c_char_p(), ctypes.c_int64()
+            assert N.lib().sesa_bsr_param_info(h, i, ctypes.byref(nm), ctypes.byref(numel)) == 0
+            names.append((nm.value.decode(), numel.value))
+    finally:
+        N.lib().sesa_bsr_destroy(h)
+    assert names == [(n, int(np.prod(s))) for n, s in ref]
+
+
+def test_create_rejects_unsupported():
+    from sesa import _native as N
+    fpb = (ctypes.c_int * 2)(500, 500)                 # does not sum to 1025
+    c = N.SesaBsrConfig(chunk_size=44100, audio_channels=2, n_fft=2048, hop_length=441, win_length=2048, dim=64,
+                        depth=1, heads=1, dim_head=64, time_transformer_depth=1, freq_transformer_depth=1,
+                        num_stems=1, mask_estimator_depth=2, mlp_expansion_factor=4, n_bands=2, freqs_per_bands=fpb,
+                        precision=0)
+    h = ctypes.c_void_p()
+    assert N.lib().sesa_bsr_create(ctypes.byref(c), ctypes.byref(h)) == -1
+    assert b"freqs_per_bands" in N.lib().sesa_last_error()
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+@pytest.mark.gpu
+def test_forward_small_matches_reference(golden, dev):
+    g = golden("bsr_small.npz")
+    m, _ = _model("config_bs_roformer_small.yaml", str(g["affine"]))
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    assert y.shape == g["y"].shape
+    err = rms(y, g["y"])
+    print(f"bsr small forward rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    assert err <= RMS_GATE
+
+
+@pytest.mark.gpu
+def test_forward_small_bf16_reports_deviation(golden, dev):
+    g = golden("bsr_small.npz")
+    m, _ = _model("config_bs_roformer_small.yaml", str(g["affine"]), precision="bf16")
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"bsr small forward bf16 rms {err:.3e}")
+    assert np.isfinite(y).all() and err < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(os.path.join(GOLDEN, "bsr_full_chunk.npz")), reason="full fixture absent")
+def test_forward_full_chunk_matches_reference(golden, dev):
+    g = golden("bsr_full_chunk.npz")
+    m, _ = _model("config_bs_roformer_vocals.yaml", str(g["affine"]))
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"bsr vocals full chunk rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    assert err <= RMS_GATE
+
+
+@pytest.mark.gpu
+def test_demix_matches_reference(golden, dev):
+    from sesa.demix import demix_pytorch_optimized
+    g = golden("demix_bsr_small.npz")
+    m, c = _model("config_bs_roformer_small.yaml", "random")
+    with contextlib.redirect_stdout(io.StringIO()) as out:
+        res = demix_pytorch_optimized(c, m, g["mix"], dev)
+    prog = [ln for ln in out.getvalue().splitlines() if ln.startswith("[SESA_PROGRESS]")]
+    assert prog == list(g["progress"])
+    assert res["vocals"].shape == g["vocals"].shape
+    assert rms(res["vocals"], g["vocals"]) <= RMS_GATE
