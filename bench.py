@@ -33,8 +33,15 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 SR = 44100
-CFG = os.path.join(REPO, "sesa-audio-separation_amd", "sesa", "configs", "config_vocals_mdx23c.yaml")
-FLOP_PER_CHUNK = 2.4341e12  # SURVEY §6 (FlopCounterMode on the reference)
+CFG_DIR = os.path.join(REPO, "sesa-audio-separation_amd", "sesa", "configs")
+# model -> (config, algorithmic FLOP per chunk (FlopCounterMode on the reference),
+#           dominant kernel class, its description)
+MODELS = {
+    "mdx23c": ("config_vocals_mdx23c.yaml", 2.4341e12, "conv3x3",
+               "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)"),
+    "bs_roformer": ("config_bs_roformer_vocals.yaml", 7.6429e12, "tokgemm",
+                    "tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)"),
+}
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
 
 
@@ -42,35 +49,47 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg, n_chunks_track, track_seconds, sample_chunks):
+def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chunks):
     """Oracle (PyTorch-CPU fp32) forward on `sample_chunks` chunks; extrapolated to the track."""
-    from oracle import mdx23c as om
-    from oracle.weights import synth_state_dict
     threads = torch.get_num_threads()
-    params = om.to_torch_params(synth_state_dict(om.param_shapes(cfg)))
+    if model_name == "mdx23c":
+        import yaml
+        from oracle import mdx23c as om
+        from oracle.weights import synth_state_dict
+        with open(cfg_path) as f:
+            cfg = yaml.safe_load(f)
+        params = om.to_torch_params(synth_state_dict(om.param_shapes(cfg)))
+        fwd = om.forward
+    else:
+        from oracle import bs_roformer as ob
+        cfg = ob.load_cfg(cfg_path)
+        params = ob.to_torch(ob.synth_params(cfg))
+        fwd = ob.forward
     rng = np.random.default_rng(0)
     x = torch.from_numpy((0.1 * rng.standard_normal((1, 2, int(cfg["audio"]["chunk_size"])))).astype(np.float32))
     t0 = time.time()
     with torch.inference_mode():
         for _ in range(sample_chunks):
-            om.forward(params, cfg, x)
+            fwd(params, cfg, x)
     per_chunk = (time.time() - t0) / sample_chunks
     return {"value": round(track_seconds / (per_chunk * n_chunks_track), 4), "unit": "separated-audio sec/sec",
             "cores": threads, "kind": "port",
-            "sample": f"{sample_chunks} of {n_chunks_track} chunks of the same 4-min track, full-width MDX23C "
-                      f"vocals config, oracle/mdx23c.py PyTorch-CPU fp32, {per_chunk:.2f} s/chunk, "
+            "sample": f"{sample_chunks} of {n_chunks_track} chunks of the same 4-min track, full-width {model_name} "
+                      f"vocals config, oracle/{'mdx23c' if model_name == 'mdx23c' else 'bs_roformer'}.py PyTorch-CPU "
+                      f"fp32, {per_chunk:.2f} s/chunk, "
                       f"extrapolated per chunk (OLA <1% of CPU time, SURVEY §6)"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--model", default="mdx23c", choices=sorted(MODELS))
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"])
-    ap.add_argument("--exec-batch", type=int, default=16)
+    ap.add_argument("--exec-batch", type=int, default=0, help="chunks per forward (0: 16 mdx23c / 4 bs_roformer)")
     ap.add_argument("--track-seconds", type=float, default=240.0)
-    ap.add_argument("--cpu-sample-chunks", type=int, default=2)
+    ap.add_argument("--cpu-sample-chunks", type=int, default=0, help="0: 2 (mdx23c) / 1 (bs_roformer)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -88,8 +107,25 @@ def main():
     from sesa.utils import get_model_from_config
     from sesa.weights import synth_state_dict
 
-    model, cfg = get_model_from_config("mdx23c", CFG)
-    model.load_state_dict(synth_state_dict(model), strict=True)   # random-init weights (no checkpoint offline)
+    cfg_name, flop_per_chunk, kclass, kdesc = MODELS[args.model]
+    cfg_path = os.path.join(CFG_DIR, cfg_name)
+    exec_batch = args.exec_batch or (16 if args.model == "mdx23c" else 4)
+    model, cfg = get_model_from_config(args.model, cfg_path)
+    if args.model == "mdx23c":
+        model.load_state_dict(synth_state_dict(model), strict=True)   # random-init weights (no checkpoint offline)
+    else:
+        import zlib
+        sd = {}
+        for name, shape in model.param_shapes():                      # name-keyed random init, PyTorch bounds
+            t = model.state_dict()[name]
+            if name.endswith("freqs") or name.endswith("gamma"):
+                sd[name] = t
+                continue
+            rng = np.random.Generator(np.random.PCG64(zlib.crc32(name.encode()) ^ 0x5E5A))
+            fan_in = shape[1] if len(shape) == 2 else dict(model.param_shapes())[name[:-5] + ".weight"][1]
+            b = 1.0 / np.sqrt(fan_in)
+            sd[name] = torch.from_numpy(rng.uniform(-b, b, size=shape).astype(np.float32))
+        model.load_state_dict(sd, strict=True)
     model.set_precision(args.precision)
     n = int(round(args.track_seconds * SR))
     rng = np.random.default_rng(0)
@@ -99,7 +135,7 @@ def main():
                                                     cfg.inference.batch_size)[3])
 
     def step():
-        return demix_sharded(cfg, model, mix_d, dev, rank=rank, world=world, exec_batch=args.exec_batch)
+        return demix_sharded(cfg, model, mix_d, dev, rank=rank, world=world, exec_batch=exec_batch)
 
     for _ in range(args.warmup):
         step()
@@ -123,43 +159,50 @@ def main():
         elapsed = float(t.item())
     assert torch.isfinite(est).all().item()
 
-    ms, launches, work = _native.profile_read("conv3x3")
+    ms, launches, work = _native.profile_read(kclass)
     passes = 3 if args.precision == "bf16x3" else 1
     achieved = work / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     peak = BF16_DENSE_TFLOPS / passes
     traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_conv3x3.json")
+    pmc = os.path.join(REPO, "profiles", f"pmc_{kclass}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,
-            "kernel": "tap_gemm_kernel<3x3> (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)",
+            "kernel": kdesc,
             "launches": launches, "avg_launch_ms": round(ms / max(launches, 1), 4),
             "flop_per_launch": round(work / max(launches, 1)),
             "peak_note": f"2.5 PF/s dense bf16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"}
-    path_tflops = n_chunks * FLOP_PER_CHUNK * args.steps / elapsed / 1e12
+    path_tflops = n_chunks * flop_per_chunk * args.steps / elapsed / 1e12
 
     value = args.track_seconds * args.steps / elapsed
     if rank == 0:
+        C, ov = int(cfg.audio.chunk_size), int(cfg.inference.num_overlap)
+        wl = ("mdx23c_tfc_tdf_v3 vocals config" if args.model == "mdx23c" else
+              "bs_roformer (viperx 1297: dim 512, depth 12, 8x64 heads, 62 bands) vocals config")
         line = {
-            "metric": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X",
+            "metric": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X"
+                      if args.model == "mdx23c" else "separated-audio sec/sec (RTF), BS-Roformer 44.1kHz stereo, MI355X",
             "value": round(value, 3), "unit": "separated-audio sec/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic: 0.1*N(0,1) stereo mix (seed 0), name-keyed random-init weights",
-            "config": {"workload": f"mdx23c_tfc_tdf_v3 vocals config, {args.track_seconds:.0f} s 44.1 kHz stereo "
-                                   f"track chunked (C=261120, overlap 4, {n_chunks} chunks), mix resident in HBM",
-                       "chunks": n_chunks, "exec_batch": args.exec_batch,
+            "config": {"workload": f"{wl}, {args.track_seconds:.0f} s 44.1 kHz stereo track chunked (C={C}, "
+                                   f"overlap {ov}, {n_chunks} chunks), mix resident in HBM",
+                       "model": args.model, "chunks": n_chunks, "exec_batch": exec_batch,
                        "parallelism": f"chunk-shard x{world} + RCCL all_gather" if world > 1 else "1 GPU",
                        "path_tflops_algorithmic": round(path_tflops, 2)},
             "roofline": roof,
         }
+        if args.model == "bs_roformer":
+            ams, alaunch, awork = _native.profile_read("attn")
+            line["attention"] = {"kernel": "attn_kernel (flash, S^T = K Q^T, bf16x3 MFMA)",
+                                 "achieved_tflops": round(awork / (ams * 1e-3) / 1e12, 2) if ams > 0 else 0.0,
+                                 "launches": alaunch, "avg_launch_ms": round(ams / max(alaunch, 1), 4)}
         if world == 1 and not args.no_cpu_baseline:
-            with open(CFG) as f:
-                import yaml
-                raw = yaml.safe_load(f)
-            line["cpu_baseline"] = cpu_baseline(raw, n_chunks, args.track_seconds, args.cpu_sample_chunks)
+            line["cpu_baseline"] = cpu_baseline(args.model, cfg_path, n_chunks, args.track_seconds,
+                                                args.cpu_sample_chunks or (2 if args.model == "mdx23c" else 1))
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -147,6 +147,28 @@ int sesa_bsr_forward(sesa_bsr* m, const float* x, int batch, float* out, void* w
 int sesa_bsr_destroy(sesa_bsr* m);
 
 /* ---------------------------------------------------------------------------------------
+ * Ensemble blend (ensemble.py:172-407, AudioEnsembleEngine.process_waveform / process_spectral /
+ * run_ensemble's buffer loop).  Methods in the reference's --type order.
+ *   x   [n_files][n_ch][L] fp32 (device; the inputs cut to the shortest, ensemble.py:304-306)
+ *   out [n_ch][L] float64 (device; written as PCM_24 by the caller, :311)
+ *   weights: host float[n_files] or NULL (normalised in float32 exactly as :288-293)
+ * Spectral methods process independent `buffer`-sample pieces (scipy stft/istft per piece,
+ * nperseg = min(1024, piece)); pieces < 256 samples use avg_wave (:355-357).  They need a
+ * caller-owned workspace of sesa_blend_workspace_size(n_ch, buffer) bytes.  1 <= n_files <= 8.
+ */
+#define SESA_BLEND_AVG_WAVE 0
+#define SESA_BLEND_MEDIAN_WAVE 1
+#define SESA_BLEND_MAX_WAVE 2
+#define SESA_BLEND_MIN_WAVE 3
+#define SESA_BLEND_MAX_FFT 4
+#define SESA_BLEND_MIN_FFT 5
+#define SESA_BLEND_MEDIAN_FFT 6
+size_t sesa_blend_workspace_size(int n_ch, int64_t buffer);
+int sesa_blend_f32(const float* x, int n_files, int n_ch, int64_t L, int64_t buffer, int method,
+                   const float* weights, double* out, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Kernel timing (measurement support for bench.py; not part of the reference surface).
  * While enabled, every launch issued by libsesa is bracketed by a hipEvent pair on its own
  * stream and tagged with its kernel class and ALGORITHMIC work (reference FLOPs for the

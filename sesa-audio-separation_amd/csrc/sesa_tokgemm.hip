@@ -6,8 +6,8 @@
 //   residual :214), FeedForward (:55-74, GELU / + residual :215), MaskEstimator MLPs (:277-310,
 //   grouped, Tanh and GLU in the epilogues).  RMSNorm (:43-50) is fused: gamma is folded into W at
 //   pack time and the row scale sqrt(K)/max(||x||, 1e-12) is computed from the staged A values.
-//   Workgroup tile 128 tokens x 128 columns, 4 waves of 64x64 (2x2 blocks of 32x32), K chunks of
-//   32 staged fp32 -> bf16 hi/lo in LDS; weights arrive pre-split and pre-swizzled.
+//   Workgroup tile 256 tokens x 256 columns, 8 waves of 64x128 (2x4 blocks of 32x32), K chunks of
+//   32 staged fp32 -> bf16 hi/lo in double-buffered LDS; weights arrive pre-split and pre-swizzled.
 //   Precision bf16x3 (hi*hi + hi*lo + lo*hi, fp32 accumulate) or bf16 (one pass).
 // attn_kernel -- softmax(Q K^T / sqrt(64)) V per (sequence, head) (attend.py:76-95, SDPA), the
 //   flash formulation with S^T = K Q^T so every query owns one lane column: row max / sum are
@@ -17,6 +17,7 @@
 //   token-major buffer, so the time/freq transformers (:526-543) need no transposes.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "sesa_common.hpp"
@@ -52,18 +53,20 @@ __device__ __forceinline__ uint32_t pack2(__bf16 a, __bf16 b) {
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
 // ---------------------------------------------------------------------------------------------
-template <bool X3>
-__global__ void __launch_bounds__(kThreads, 2) tok_gemm_kernel(TokGemmArgs a) {
-  constexpr int BM = kTokBM, BN = kTokBN, BK = kTokBK;
-  constexpr int MI = 2, NI = 2;
+// 512 threads (8 waves: 4 along M x 2 along N, 64x128 each), tile 256 tokens x 256 columns, LDS
+// double-buffered (2 x 64 KB) with ONE barrier per 32-wide K chunk (48 MFMAs per wave per barrier): iteration k runs the MFMAs of
+// stage k&1, writes chunk k+1 (already in registers) to the other stage and issues the global loads
+// of chunk k+2.  The body is straight-line (clamped addresses, validity applied at store time).
+template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB>
+__global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a) {
+  constexpr int BN = kTokBN, BK = kTokBK;
+  static_assert((NT / 64) == (BM / (32 * MI)) * WN && BN == WN * NI * 32, "tile");
   constexpr int ROWB = BK * 2;                 // 64 B per image row (32 bf16)
   constexpr int A_BYTES = BM * ROWB;
   constexpr int W_BYTES = BN * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * A_BYTES + 2 * W_BYTES];
+  constexpr int STAGE = 2 * A_BYTES + 2 * W_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE];
   __shared__ float rs[BM];
-  char* Ahi = smem;
-  char* Alo = smem + A_BYTES;
-  char* Whi = smem + 2 * A_BYTES;              // hi then lo, as packed
 
   const TokGroup g = a.groups[blockIdx.y];
   const int n_tile = blockIdx.x % a.n_tiles_n;
@@ -74,7 +77,7 @@ __global__ void __launch_bounds__(kThreads, 2) tok_gemm_kernel(TokGemmArgs a) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int l32 = lane & 31, h = lane >> 5;
   const int n_chunks = (g.K + BK - 1) / BK;
 
@@ -86,49 +89,57 @@ __global__ void __launch_bounds__(kThreads, 2) tok_gemm_kernel(TokGemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // A staging: item (row, 4 k); thread tid covers rows (tid >> 3) + 32 i, k quad (tid & 7)
+  // A staging: item (row, 4 k); thread covers rows (tid >> 3) + (NT / 8) i, k quad (tid & 7)
+  constexpr int AI = BM * 8 / NT;
+  constexpr int RS = NT / 8;
   const int arow0 = tid >> 3, akq = (tid & 7) * 4;
-  f32x4 areg[4];
-  float ss[4] = {0.f, 0.f, 0.f, 0.f};
-  const float* xrow[4];
-  bool rok[4];
+  f32x4 areg[AI];
+  float ss[AI];
+  const float* xrow[AI];
+  bool rok[AI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + arow0 + 32 * i;
+  for (int i = 0; i < AI; ++i) {
+    ss[i] = 0.f;
+    const int m = m0 + arow0 + RS * i;
     rok[i] = m < a.M;
-    xrow[i] = a.x + (int64_t)(rok[i] ? m : 0) * a.x_ld + g.x_off;
+    xrow[i] = a.x + (int64_t)(rok[i] ? m : a.M - 1) * a.x_ld + g.x_off;
   }
+  bool kok = true;
   constexpr int W16 = (X3 ? 2 : 1) * W_BYTES / 16;
-  constexpr int W_ITEMS = (W16 + kThreads - 1) / kThreads;
+  constexpr int W_ITEMS = (W16 + NT - 1) / NT;
   u32x4 wreg[W_ITEMS];
   const uint16_t* wblk = a.w + g.w_off + (int64_t)n_tile * n_chunks * (2 * W_BYTES / 2);
 
   auto load_chunk = [&](int kc) {
     const u32x4* s4 = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * (2 * W_BYTES / 2));
     Unroll<0, W_ITEMS>::run([&](auto I) {
-      const int e = tid + I * kThreads;
+      const int e = tid + I * NT;
       wreg[I] = s4[e < W16 ? e : W16 - 1];
     });
     const int k = kc * BK + akq;
-    const bool kok = k < g.K;  // K % 4 == 0 (host check): a quad is wholly in or out
+    kok = k < g.K;  // K % 4 == 0 (host check): a quad is wholly in or out
+    const int kc_ = kok ? k : 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      areg[i] = (rok[i] && kok) ? *reinterpret_cast<const f32x4*>(xrow[i] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < AI; ++i) areg[i] = *reinterpret_cast<const f32x4*>(xrow[i] + kc_);
   };
-  auto store_chunk = [&]() {
-    u32x4* d4 = reinterpret_cast<u32x4*>(Whi);
+  // count: 1 when this store is a real chunk (0 for the clamped repeat past the end: no RMS sum)
+  auto store_chunk = [&](char* stg, float count) {
+    char* Ahi = stg;
+    char* Alo = stg + A_BYTES;
+    u32x4* d4 = reinterpret_cast<u32x4*>(stg + 2 * A_BYTES);
     Unroll<0, W_ITEMS>::run([&](auto I) {
-      const int e = tid + I * kThreads;
-      if (W16 % kThreads == 0 || e < W16) d4[e] = wreg[I];
+      const int e = min(tid + I * NT, W16 - 1);  // duplicates write identical values
+      d4[e] = wreg[I];
     });
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = arow0 + 32 * i;
+    for (int i = 0; i < AI; ++i) {
+      const int row = arow0 + RS * i;
+      const bool ok = rok[i] && kok;
       __bf16 hi[4], lo[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float v = areg[i][q];
-        ss[i] += v * v;
+        const float v = ok ? areg[i][q] : 0.f;
+        ss[i] = fmaf(v * count, v, ss[i]);
         split_bf16(v, hi[q], lo[q]);
       }
       const int off = row * ROWB + ((((akq >> 3) ^ ((row >> 2) & 3))) << 4) + ((akq & 4) << 1);
@@ -136,110 +147,128 @@ __global__ void __launch_bounds__(kThreads, 2) tok_gemm_kernel(TokGemmArgs a) {
       if (X3) *reinterpret_cast<uint2*>(Alo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
     }
   };
-
-  load_chunk(0);
-  for (int kc = 0; kc < n_chunks; ++kc) {
-    __syncthreads();
-    store_chunk();
-    __syncthreads();
-    if (kc + 1 < n_chunks) load_chunk(kc + 1);
+  auto kstep = [&](const char* stg, int ks) {
+    const char* Ahi = stg;
+    const char* Alo = stg + A_BYTES;
+    const char* Whi = stg + 2 * A_BYTES;
+    bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
+    const int q = ks * 2 + h;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
-      const int q = ks * 2 + h;
+    for (int i = 0; i < MI; ++i) {
+      const int row = (wm * MI + i) * 32 + l32;
+      const int off = row * ROWB + ((q ^ ((row >> 2) & 3)) << 4);
+      ah[i] = *reinterpret_cast<const bf16x8*>(Ahi + off);
+      if (X3) al[i] = *reinterpret_cast<const bf16x8*>(Alo + off);
+    }
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int row = (wm * MI + i) * 32 + l32;
-        const int off = row * ROWB + ((q ^ ((row >> 2) & 3)) << 4);
-        ah[i] = *reinterpret_cast<const bf16x8*>(Ahi + off);
-        if (X3) al[i] = *reinterpret_cast<const bf16x8*>(Alo + off);
-      }
+    for (int j = 0; j < NI; ++j) {
+      const int n = (wn * NI + j) * 32 + l32;
+      const int off = n * ROWB + ((q ^ ((n >> 2) & 3)) << 4);
+      bh[j] = *reinterpret_cast<const bf16x8*>(Whi + off);
+      if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(Whi + W_BYTES + off);
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int n = (wn * NI + j) * 32 + l32;
-        const int off = n * ROWB + ((q ^ ((n >> 2) & 3)) << 4);
-        bh[j] = *reinterpret_cast<const bf16x8*>(Whi + off);
-        if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(Whi + W_BYTES + off);
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          if (X3) {
-            acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
-            acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
-          }
-          acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+        if (X3) {
+          acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
         }
+        acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+      }
+  };
+
+  if (DB) {
+    load_chunk(0);
+    store_chunk(smem, 1.f);
+    load_chunk(min(1, n_chunks - 1));
+    __syncthreads();
+    for (int kc = 0; kc < n_chunks; ++kc) {
+      const char* cur = smem + (kc & 1) * STAGE;
+      char* nxt = smem + ((kc + 1) & 1) * STAGE;
+      kstep(cur, 0);
+      store_chunk(nxt, kc + 1 < n_chunks ? 1.f : 0.f);
+      load_chunk(min(kc + 2, n_chunks - 1));
+      kstep(cur, 1);
+      __syncthreads();
+    }
+  } else {
+    // single stage, two barriers per chunk, register prefetch of the next chunk under the MFMAs;
+    // two workgroups per CU overlap one's staging / epilogue with the other's MFMAs
+    load_chunk(0);
+    for (int kc = 0; kc < n_chunks; ++kc) {
+      __syncthreads();
+      store_chunk(smem, 1.f);
+      __syncthreads();
+      load_chunk(min(kc + 1, n_chunks - 1));
+      kstep(smem, 0);
+      kstep(smem, 1);
     }
   }
 
   // ---- RMSNorm row scales: 8 threads share a row ----
   if (a.rownorm) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < AI; ++i) {
       float v = ss[i];
       v += __shfl_xor(v, 1);
       v += __shfl_xor(v, 2);
       v += __shfl_xor(v, 4);
-      if ((tid & 7) == 0) rs[arow0 + 32 * i] = sqrtf((float)g.K) / fmaxf(sqrtf(v), 1e-12f);
+      if ((tid & 7) == 0) rs[arow0 + RS * i] = sqrtf((float)g.K) / fmaxf(sqrtf(v), 1e-12f);
     }
     __syncthreads();
   }
 
-  // ---- epilogue: scale, bias, activation, rotary / GLU, residual, store ----
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
+  // ---- epilogue, one 32x32 block at a time (compile-time block indices: acc stays in VGPRs):
+  // scale, bias, activation, rotary / GLU, then residual loads (all before any store: residual may
+  // alias out), then stores ----
+  Unroll<0, MI>::run([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    Unroll<0, NI>::run([&](auto J) {
+      constexpr int j = decltype(J)::value;
       const int n = n0 + (wn * NI + j) * 32 + l32;
-      const float bias = (g.b_off >= 0 && n < g.N) ? a.bias[g.b_off + n] : 0.f;
+      const bool n_ok = n < g.N;
+      const float bias = (g.b_off >= 0 && n_ok) ? a.bias[g.b_off + n] : 0.f;
+      const int d = n % a.dim_head;
+      const bool rot = a.rope && n < a.rope_cols;
+      f32x16 v = acc[i][j];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ml = (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        float v = acc[i][j][r];
-        if (a.rownorm) v *= rs[ml];
-        v += bias;
-        if (a.act == TOK_ACT_GELU) v = gelu_erf(v);
-        else if (a.act == TOK_ACT_TANH) v = tanhf(v);
-        const float partner = __shfl_xor(v, 1);  // column n ^ 1, same row
-        if (a.rope && n < a.rope_cols) {
+        float x = v[r];
+        if (a.rownorm) x *= rs[ml];
+        x += bias;
+        if (a.act == TOK_ACT_GELU) x = gelu_erf(x);
+        else if (a.act == TOK_ACT_TANH) x = tanhf(x);
+        const float partner = __shfl_xor(x, 1);  // column n ^ 1, same row
+        if (rot) {
           const int m = m0 + ml;
           const int pos = a.pos_time ? (m / a.pos_F) % a.pos_T : m % a.pos_F;
-          const int d = n % a.dim_head;
           const float2 cs = a.rope[(int64_t)pos * (a.dim_head >> 1) + (d >> 1)];
-          v = (d & 1) ? fmaf(v, cs.x, partner * cs.y) : fmaf(v, cs.x, -partner * cs.y);
+          x = (d & 1) ? fmaf(x, cs.x, partner * cs.y) : fmaf(x, cs.x, -partner * cs.y);
         }
-        if (a.glu) v = v * sigmoidf_(partner);  // valid on even columns (a_j), odd lanes discarded
-        acc[i][j][r] = v;
+        if (a.glu) x = x * sigmoidf_(partner);  // valid on even columns (a_j); odd lanes discarded
+        v[r] = x;
       }
-    }
-  if (a.residual) {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int n = n0 + (wn * NI + j) * 32 + l32;
+      const int rb = m0 + (wm * MI + i) * 32 + 4 * h;
+      if (a.residual && n_ok) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (m < a.M && n < g.N) acc[i][j][r] += a.residual[(int64_t)m * a.o_ld + g.o_off + n];
+          const int m = rb + (r & 3) + 8 * (r >> 2);
+          if (m < a.M) v[r] += a.residual[(int64_t)m * a.o_ld + g.o_off + n];
         }
       }
-  }
+      if (n_ok && !(a.glu && (n & 1))) {
+        const int nc = a.glu ? n >> 1 : n;
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int n = n0 + (wn * NI + j) * 32 + l32;
-      if (n >= g.N || (a.glu && (n & 1))) continue;
-      const int nc = a.glu ? n >> 1 : n;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < a.M) a.out[(int64_t)m * a.o_ld + g.o_off + nc] = acc[i][j][r];
+        for (int r = 0; r < 16; ++r) {
+          const int m = rb + (r & 3) + 8 * (r >> 2);
+          if (m < a.M) a.out[(int64_t)m * a.o_ld + g.o_off + nc] = v[r];
+        }
       }
-    }
+    });
+  });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -442,11 +471,21 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
 int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
   SESA_REQUIRE(a.n_groups >= 1 && a.n_tiles_n >= 1 && a.M >= 0, SESA_ERR_INVALID, "tok_gemm: bad grid");
   if (a.M == 0) return SESA_OK;
-  const int64_t m_tiles = (a.M + kTokBM - 1) / kTokBM;
+  const int64_t m_tiles = (a.M + 127) / 128;
   SESA_REQUIRE(m_tiles * a.n_tiles_n < (1ll << 31) && a.n_groups < 65536, SESA_ERR_INVALID, "tok_gemm: grid too large");
   dim3 grid((unsigned)(m_tiles * a.n_tiles_n), (unsigned)a.n_groups);
-  if (x3) hipLaunchKernelGGL(tok_gemm_kernel<true>, grid, dim3(kThreads), 0, st, a);
-  else hipLaunchKernelGGL(tok_gemm_kernel<false>, grid, dim3(kThreads), 0, st, a);
+  // variant 0: 256 threads, 128 x 256 tile (4 waves of 64 x 128), single stage, 2 WG / CU
+  // variant 1: 512 threads, 256 x 256 tile (8 waves of 64 x 128), double-buffered, 1 WG / CU
+  static const int variant = getenv("SESA_TOKGEMM_VARIANT") ? atoi(getenv("SESA_TOKGEMM_VARIANT")) : 0;
+  if (variant == 1) {
+    const int64_t mt = (a.M + 255) / 256;
+    dim3 g1((unsigned)(mt * a.n_tiles_n), (unsigned)a.n_groups);
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 512, 256, 2, 2, 4, true>), g1, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 4, true>), g1, dim3(512), 0, st, a);
+  } else {
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 4, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 4, false>), grid, dim3(256), 0, st, a);
+  }
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }

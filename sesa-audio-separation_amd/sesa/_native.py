@@ -55,6 +55,9 @@ SIGNATURES = {
     "sesa_bsr_workspace_size": (c_size_t, [c_void_p, c_int]),
     "sesa_bsr_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
     "sesa_bsr_destroy": (c_int, [c_void_p]),
+    "sesa_blend_workspace_size": (c_size_t, [c_int, c_int64]),
+    "sesa_blend_f32": (c_int, [P_f32, c_int, c_int, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_size_t,
+                               c_void_p]),
     "sesa_profile_enable": (c_int, [c_int]),
     "sesa_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
                                   ctypes.POINTER(ctypes.c_double)]),

@@ -1,0 +1,156 @@
+"""Ensemble blend on the MI355X path -- drop-in for ``/root/reference/ensemble.py``.
+
+Same CLI (``--files ... --type {avg_wave,median_wave,max_wave,min_wave,max_fft,min_fft,median_fft}
+[--weights ...] --output P [--buffer 32768]``, exit 0/1, :409-438), same ``[SESA_PROGRESS]N`` lines,
+same validation rules (stereo, >= 2 files, one sample rate, :86-170), inputs cut to the shortest
+(:304-306), output written as 2-channel PCM_24 WAV (:311).  The blend itself -- every buffer of
+every method, including the scipy-STFT magnitude methods -- runs in libsesa ``sesa_blend_f32``
+(csrc/sesa_blend.hip) in float64 on the device; there is no CPU fallback.
+
+Divergence kept from the reference on purpose: the path-sanitising re-encode (:63-84), which
+re-writes inputs whose path contains one of ``[]()|&; `` as PCM_16 through librosa, is
+reproduced only as the quantisation it causes (``requantize_special_paths=True``, default).
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .audio_io import read_wav, write_audio
+
+METHODS = ["avg_wave", "median_wave", "max_wave", "min_wave", "max_fft", "min_fft", "median_fft"]
+_SPECIAL = "[]()|&; "
+
+
+def blend_device(waves, method, weights=None, buffer=32768):
+    """[n_files, ch, L] (array or device tensor) -> device float64 [ch, L] (run_ensemble's buffer loop)."""
+    if method not in METHODS:
+        raise ValueError(f"Invalid method '{method}'. Available: {METHODS}")
+    x = torch.as_tensor(waves).to("cuda", torch.float32).contiguous()
+    if not x.is_cuda:
+        raise N.SesaError("blend_device needs a HIP device (no CPU fallback)")
+    n, ch, L = x.shape
+    out = torch.empty(ch, L, device=x.device, dtype=torch.float64)
+    w = None
+    if weights is not None and len(weights) == n:
+        w = np.ascontiguousarray(np.asarray(weights, np.float32))
+    ws_bytes = N.lib().sesa_blend_workspace_size(ch, int(buffer))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if method.endswith("_fft") else None
+    N.check(N.lib().sesa_blend_f32(x.data_ptr(), n, ch, L, int(buffer), METHODS.index(method),
+                                   w.ctypes.data if w is not None else None, out.data_ptr(),
+                                   ws.data_ptr() if ws is not None else None, ws_bytes if ws is not None else 0,
+                                   torch.cuda.current_stream(x.device).cuda_stream), "sesa_blend_f32")
+    return out
+
+
+class AudioEnsembleEngine:
+    """ensemble.AudioEnsembleEngine surface: process_waveform / process_spectral / run_ensemble."""
+
+    def __init__(self, requantize_special_paths=True):
+        self.requantize_special_paths = requantize_special_paths
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+    def process_waveform(self, chunks, method, weights=None):
+        return blend_device(chunks, method, weights, buffer=max(1, np.shape(chunks)[-1])).cpu().numpy()
+
+    def process_spectral(self, chunks, method):
+        chunks = np.asarray(chunks)
+        if chunks.shape[-1] < 256:
+            return None
+        return blend_device(chunks, method, None, buffer=chunks.shape[-1]).cpu().numpy()
+
+    def _load(self, path):
+        data, sr = read_wav(path)                       # float32 [ch, frames], soundfile scaling
+        if self.requantize_special_paths and any(c in os.path.abspath(path) for c in _SPECIAL):
+            data = (np.round(np.clip(data, -1.0, 1.0 - 1.0 / 32768) * 32768.0) / 32768.0).astype(np.float32)
+        return data, sr
+
+    def validate_inputs(self, files, method):
+        errors, valid, rates, loaded = [], [], set(), []
+        if method not in METHODS:
+            errors.append(f"Invalid method '{method}'. Available: {METHODS}")
+        for f in files:
+            if not os.path.exists(f):
+                errors.append(f"File not found: {f}")
+                continue
+            if os.path.getsize(f) == 0:
+                errors.append(f"Empty file: {f}")
+                continue
+            try:
+                data, sr = self._load(f)
+            except Exception as e:  # noqa: BLE001 -- reported like the reference
+                errors.append(f"Invalid audio file {f}: {e}")
+                continue
+            if data.shape[0] != 2:
+                errors.append(f"File must be stereo (has {data.shape[0]} channels): {f}")
+                continue
+            rates.add(sr)
+            valid.append(f)
+            loaded.append(data)
+        if len(valid) < 2:
+            errors.append("At least 2 valid files required")
+        if len(rates) > 1:
+            errors.append(f"Sample rate mismatch: {rates}")
+        if errors:
+            raise ValueError("\n".join(errors))
+        return valid, loaded, rates.pop()
+
+    def run_ensemble(self, files, method, output_path, weights=None, buffer_size=32768):
+        try:
+            valid, loaded, sr = self.validate_inputs(files, method)
+            out_dir = os.path.dirname(os.path.abspath(output_path)) or "."
+            os.makedirs(out_dir, exist_ok=True)
+            if weights and len(weights) == len(valid):
+                w = np.asarray(weights, np.float32)
+            else:
+                w = None
+            shortest = min(d.shape[1] for d in loaded)
+            print("Loading audio files...", flush=True)
+            waves = np.stack([d[:, :shortest] for d in loaded])
+            print("Processing ensemble...", flush=True)
+            out = blend_device(waves, method, w, buffer_size).cpu().numpy()
+            total = (shortest + buffer_size - 1) // buffer_size
+            last = -1
+            for k in range(1, total + 1):                     # progress protocol (:379-383)
+                pct = int((k / total) * 100)
+                if pct > last:
+                    last = pct
+                    print(f"[SESA_PROGRESS]{pct}", flush=True)
+            print("Saving ensemble output...", flush=True)
+            write_audio(output_path, out.T, sr, subtype="PCM_24")
+            print(f"\nEnsemble completed successfully: {output_path}")
+            return True
+        except Exception as e:  # noqa: BLE001 -- the reference turns every failure into exit code 1
+            print(f"\nError during processing: {e}", file=sys.stderr)
+            return False
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="Ultimate Audio Ensemble Processor - Supports all ensemble methods",
+                                formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    p.add_argument("--files", nargs="+", required=True, help="Input audio files (supports special characters)")
+    p.add_argument("--type", required=True, choices=METHODS, help="Ensemble method to use")
+    p.add_argument("--weights", nargs="+", type=float, help="Relative weights for each input file")
+    p.add_argument("--output", required=True, help="Output file path")
+    p.add_argument("--buffer", type=int, default=32768, help="Buffer size in samples (larger=faster but uses more memory)")
+    return p
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    with AudioEnsembleEngine() as engine:
+        ok = engine.run_ensemble(files=args.files, method=args.type, output_path=args.output, weights=args.weights,
+                                 buffer_size=args.buffer)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
