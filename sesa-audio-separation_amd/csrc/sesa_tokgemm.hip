@@ -474,17 +474,17 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
   const int64_t m_tiles = (a.M + 127) / 128;
   SESA_REQUIRE(m_tiles * a.n_tiles_n < (1ll << 31) && a.n_groups < 65536, SESA_ERR_INVALID, "tok_gemm: grid too large");
   dim3 grid((unsigned)(m_tiles * a.n_tiles_n), (unsigned)a.n_groups);
-  // variant 0: 256 threads, 128 x 256 tile (4 waves of 64 x 128), single stage, 2 WG / CU
-  // variant 1: 512 threads, 256 x 256 tile (8 waves of 64 x 128), double-buffered, 1 WG / CU
+  // variant 0 (default): 256 threads, 128 x 128 tile (4 waves of 64 x 64), single stage, 2 WG / CU
+  // variant 1: 512 threads, 256 x 128 tile (8 waves of 64 x 64), double-buffered, 1 WG / CU
   static const int variant = getenv("SESA_TOKGEMM_VARIANT") ? atoi(getenv("SESA_TOKGEMM_VARIANT")) : 0;
   if (variant == 1) {
     const int64_t mt = (a.M + 255) / 256;
     dim3 g1((unsigned)(mt * a.n_tiles_n), (unsigned)a.n_groups);
-    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 512, 256, 2, 2, 4, true>), g1, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 4, true>), g1, dim3(512), 0, st, a);
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 512, 256, 2, 2, 2, true>), g1, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 2, true>), g1, dim3(512), 0, st, a);
   } else {
-    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 4, false>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 4, false>), grid, dim3(256), 0, st, a);
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false>), grid, dim3(256), 0, st, a);
   }
   SESA_CHECK_LAUNCH();
   return SESA_OK;

@@ -7,7 +7,7 @@
 namespace sesa {
 
 constexpr int kTokBM = 256;  // token rows per workgroup tile
-constexpr int kTokBN = 256;  // output columns per workgroup tile (= packed weight row block)
+constexpr int kTokBN = 128;  // output columns per workgroup tile (= packed weight row block)
 constexpr int kTokBK = 32;   // K per staged chunk
 
 enum TokAct : int { TOK_ACT_NONE = 0, TOK_ACT_GELU = 1, TOK_ACT_TANH = 2 };
@@ -17,7 +17,7 @@ struct TokGroup {
   int K, N;        // contraction length; output columns (GLU: pre-GLU columns, interleaved a/b)
   int64_t x_off;   // float offset of the group's A block inside a token row
   int64_t o_off;   // float offset of the group's output block inside an output row
-  int64_t w_off;   // uint16 offset of the packed weight [ceil(N/256)][ceil(K/32)][hi,lo][256][32]
+  int64_t w_off;   // uint16 offset of the packed weight [ceil(N/128)][ceil(K/32)][hi,lo][128][32]
   int64_t b_off;   // float offset of the bias (< 0: none)
 };
 
