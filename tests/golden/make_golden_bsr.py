@@ -47,6 +47,50 @@ def build_ref(cfg, affine):
     return model, ref_keys
 
 
+def install_librosa_stub():
+    """The reference mel_band_roformer does `from librosa import filters`: use the restated mel."""
+    import importlib
+    sys.modules.pop("librosa", None)
+    sys.modules["librosa"] = importlib.import_module("librosa")   # oracle/_stubs/librosa
+
+
+def build_ref_mel(cfg, affine):
+    from models.bs_roformer.mel_band_roformer import MelBandRoformer
+    from oracle import mel_band_roformer as om
+    model = MelBandRoformer(**om.model_kwargs(cfg)).eval()
+    sd = om.synth_params(cfg, affine)
+    ref_keys = [(k, tuple(v.shape)) for k, v in model.state_dict().items()]
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    return model, ref_keys
+
+
+@torch.inference_mode()
+def gen_mel():
+    from oracle import mel_band_roformer as om
+    for name, tag in (("config_mel_band_roformer_vocals.yaml", "vocals"), ("config_mel_band_roformer_small.yaml", "small")):
+        cfg = _cfg(name)
+        model, keys = build_ref_mel(cfg, "unit")
+        with open(os.path.join(HERE, f"params_mbr_{tag}.json"), "w") as f:
+            json.dump([[n, list(s)] for n, s in keys], f)
+        k = om.model_kwargs(cfg)
+        fpb, idx, nbpf = om.bands(k)
+        assert torch.equal(model.freq_indices, idx) and torch.equal(model.num_bands_per_freq, nbpf)
+    cfg = _cfg("config_mel_band_roformer_small.yaml")
+    model, _ = build_ref_mel(cfg, "random")
+    C = cfg["audio"]["chunk_size"]
+    x = np.stack([mg.mix_signal(51 + b, C) for b in range(2)])
+    mg.save("mbr_small.npz", x=x, y=model(torch.from_numpy(x)).numpy(), affine=np.array("random"),
+            freq_indices=model.freq_indices.numpy(), num_bands_per_freq=model.num_bands_per_freq.numpy())
+
+
+@torch.inference_mode()
+def gen_mel_full():
+    cfg = _cfg("config_mel_band_roformer_vocals.yaml")
+    model, _ = build_ref_mel(cfg, "random")
+    x = mg.mix_signal(0, cfg["audio"]["chunk_size"])[None]
+    mg.save("mbr_full_chunk.npz", x=x, y=model(torch.from_numpy(x)).numpy(), affine=np.array("random"))
+
+
 def gen_params(cfg_name, tag):
     cfg = _cfg(cfg_name)
     _, keys = build_ref(cfg, "unit")
@@ -88,8 +132,9 @@ def main():
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     mg.install_stubs()
+    install_librosa_stub()
     torch.set_num_threads(os.cpu_count())
-    todo = args.only.split(",") if args.only else ["params", "fwd", "demix"]
+    todo = args.only.split(",") if args.only else ["params", "fwd", "demix", "mel"]
     if "params" in todo:
         gen_params("config_bs_roformer_vocals.yaml", "vocals")
         gen_params("config_bs_roformer_small.yaml", "small")
@@ -97,6 +142,10 @@ def main():
         gen_forward("config_bs_roformer_small.yaml", "bsr_small.npz", 2, 41, "random")
     if "demix" in todo:
         gen_demix()
+    if "mel" in todo:
+        gen_mel()
+    if "melfull" in todo:
+        gen_mel_full()
     if args.full or "full" in todo:
         gen_forward("config_bs_roformer_vocals.yaml", "bsr_full_chunk.npz", 1, 0, "random")
 
