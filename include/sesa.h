@@ -119,7 +119,8 @@ int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, float* out, v
 int sesa_mdx23c_destroy(sesa_mdx23c* m);
 
 /* ---------------------------------------------------------------------------------------
- * BS-Roformer (models/bs_roformer/bs_roformer.py:327-587, BSRoformer).
+ * BS-Roformer (models/bs_roformer/bs_roformer.py:327-587, BSRoformer)
+ * and Mel-Band-Roformer (same engine, `mel` fields below).
  * STFT n_fft = win = 2048 (any hop dividing chunk_size), stereo or mono, dim_head 64,
  * mask_estimator_depth 2, linear_transformer_depth 0, skip_connection False (released configs).
  * Parameters are the reference state_dict() keys (incl. layers.*.rotary_embed.freqs).
@@ -129,8 +130,15 @@ typedef struct sesa_bsr_config {
   int dim, depth, heads, dim_head, time_transformer_depth, freq_transformer_depth;
   int num_stems, mask_estimator_depth, mlp_expansion_factor;
   int n_bands;
-  const int* freqs_per_bands;   /* host array [n_bands], copied by sesa_bsr_create */
+  const int* freqs_per_bands;   /* host array [n_bands] (frequencies per band), copied by create */
   int precision;                /* SESA_PREC_*                                       */
+  /* Mel-Band-Roformer (models/bs_roformer/mel_band_roformer.py:324-620) when mel != 0:
+   * overlapping bands gathered by freq_indices ((f, s) rows, reference buffer `freq_indices`,
+   * :431-437), RMSNorm after every Transformer (norm_output, :218), no final_norm, mask MLPs of
+   * mask_estimator_depth + 1 Linear layers (:261-283), masks scatter-averaged (:596-606). */
+  int mel;
+  int n_freq_indices;
+  const int* freq_indices;      /* host array [n_freq_indices], copied by create (mel only) */
 } sesa_bsr_config;
 
 typedef struct sesa_bsr sesa_bsr;

@@ -208,6 +208,46 @@ __global__ void bsr_istft_ola_kernel(const float* __restrict__ frame_ws, int fra
   out[(int64_t)sig * out_len + j] = acc / env;
 }
 
+// Mel-Band-Roformer helpers (mel_band_roformer.py:522-533, :218, :596-606).
+// gather: xg[row][j] = spec[row][gidx[j]]
+__global__ void mel_gather_kernel(const float* __restrict__ spec, int feat, const int* __restrict__ gidx, int G,
+                                  int64_t rows, float* __restrict__ xg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * G) return;
+  const int64_t r = i / G;
+  const int j = (int)(i - r * G);
+  xg[i] = spec[r * feat + gidx[j]];
+}
+
+// in-place RMSNorm of token rows (Transformer.norm, norm_output=True): one wave per row
+__global__ void rownorm_kernel(float* __restrict__ x, int64_t rows, int dim, const float* __restrict__ gamma) {
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float* xr = x + row * dim;
+  float ss = 0.f;
+  for (int d = lane; d < dim; d += 64) ss += xr[d] * xr[d];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+  const float s = sqrtf((float)dim) / fmaxf(sqrtf(ss), 1e-12f);
+  for (int d = lane; d < dim; d += 64) xr[d] = xr[d] * s * gamma[d];
+}
+
+// scatter-average: out[row][f] = sum_{j in inv(f)} mg[row][j] / max(|inv(f)|, 1e-8), j ascending
+__global__ void mel_scatter_avg_kernel(const float* __restrict__ mg, int G, const int* __restrict__ inv_ptr,
+                                       const int* __restrict__ inv_idx, int feat, int64_t rows,
+                                       float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * feat) return;
+  const int64_t r = i / feat;
+  const int f = (int)(i - r * feat);
+  const float* src = mg + r * G;
+  float acc = 0.f;
+  const int b = inv_ptr[f], e = inv_ptr[f + 1];
+  for (int k = b; k < e; ++k) acc += src[inv_idx[k]];
+  out[i] = acc / fmaxf((float)(e - b), 1e-8f);
+}
+
 // ---------------------------------------------------------------------------------------------
 uint16_t f2bf(float f) {
   uint32_t u;
@@ -249,14 +289,23 @@ struct Layer {         // one transformer layer (Attention + FeedForward)
 
 struct sesa_bsr {
   sesa_bsr_config cfg;
+  std::vector<int> fidx; // mel: gathered (f, s) rows
   std::vector<int> fpb;  // freqs per band
   std::vector<int> dims; // band input dims 2*f*ch
   std::vector<int> offs; // band feature offsets
   int nb = 0, F = 0, T = 0, inner = 0, ff = 0, hidden = 0, qkv_ld = 0, feat = 0;
+  int gfeat = 0;          // band-split input width (= feat for BS; gathered width for mel)
+  int n_lin = 0;          // Linear layers per mask MLP
+  int* d_gidx = nullptr;  // mel: gathered feature -> spectrum feature
+  int* d_inv_ptr = nullptr;  // mel: CSR spectrum feature -> gathered features (scatter-average)
+  int* d_inv_idx = nullptr;
+  float* d_affine = nullptr;                    // mel: per-Transformer output norm gammas
+  std::map<std::string, int64_t> norm_off;      // "layers.i.j" -> float offset into d_affine
   std::vector<sesa::Param> params;
   std::map<std::string, int> by_name;
   std::vector<sesa::Layer> layers;
-  sesa::Gemm band, mlp1, mlp2;  // mlp1/mlp2 hold stems * nb groups
+  sesa::Gemm band;
+  std::vector<sesa::Gemm> mlp;  // per Linear layer of the mask MLPs, stems * nb groups each
   uint16_t* d_w = nullptr;
   float* d_bias = nullptr;
   float2* d_rope = nullptr;
@@ -340,12 +389,18 @@ extern "C" int sesa_bsr_create(const sesa_bsr_config* cfg, sesa_bsr** out) {
   SESA_REQUIRE(c.audio_channels == 1 || c.audio_channels == 2, SESA_ERR_INVALID, "bsr: audio_channels 1 or 2");
   SESA_REQUIRE(c.dim_head == 64, SESA_ERR_INVALID, "bsr: dim_head must be 64 (attention kernel)");
   SESA_REQUIRE(c.dim % 4 == 0 && c.heads >= 1 && c.depth >= 1 && c.num_stems >= 1, SESA_ERR_INVALID, "bsr: bad dims");
-  SESA_REQUIRE(c.mask_estimator_depth == 2, SESA_ERR_INVALID, "bsr: mask_estimator_depth 2 only (released configs)");
+  SESA_REQUIRE(c.mask_estimator_depth >= 1 && c.mask_estimator_depth <= 4, SESA_ERR_INVALID,
+               "bsr: mask_estimator_depth 1..4");
+  SESA_REQUIRE(!c.mel || (c.freq_indices && c.n_freq_indices > 0), SESA_ERR_INVALID, "bsr: mel needs freq_indices");
+  SESA_REQUIRE(c.mel || c.mask_estimator_depth >= 2, SESA_ERR_INVALID, "bsr: BS-Roformer mask MLP needs depth >= 2");
   SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16, SESA_ERR_INVALID, "bsr: precision");
   sesa_bsr* m = new sesa_bsr();
   m->cfg = c;
   m->fpb.assign(c.freqs_per_bands, c.freqs_per_bands + c.n_bands);
   m->cfg.freqs_per_bands = nullptr;
+  if (c.mel) m->fidx.assign(c.freq_indices, c.freq_indices + c.n_freq_indices);
+  m->cfg.freq_indices = nullptr;
+  m->n_lin = c.mel ? c.mask_estimator_depth + 1 : c.mask_estimator_depth;
   int sum = 0, off = 0;
   for (int f : m->fpb) {
     sum += f;
@@ -353,11 +408,18 @@ extern "C" int sesa_bsr_create(const sesa_bsr_config* cfg, sesa_bsr** out) {
     m->offs.push_back(off);
     off += 2 * f * c.audio_channels;
   }
-  if (sum != c.n_fft / 2 + 1) {
+  if ((!c.mel && sum != c.n_fft / 2 + 1) || (c.mel && sum * c.audio_channels != c.n_freq_indices)) {
     delete m;
-    set_error("bsr: freqs_per_bands sums to %d, expected %d", sum, c.n_fft / 2 + 1);
+    set_error("bsr: freqs_per_bands sums to %d, expected %d", sum,
+              c.mel ? c.n_freq_indices / c.audio_channels : c.n_fft / 2 + 1);
     return SESA_ERR_INVALID;
   }
+  for (int v : m->fidx)
+    if (v < 0 || v >= (c.n_fft / 2 + 1) * c.audio_channels) {
+      delete m;
+      set_error("bsr: freq_indices entry %d out of range", v);
+      return SESA_ERR_INVALID;
+    }
   m->nb = c.n_bands;
   m->F = c.n_fft / 2 + 1;
   m->T = c.chunk_size / c.hop_length + 1;
@@ -366,6 +428,7 @@ extern "C" int sesa_bsr_create(const sesa_bsr_config* cfg, sesa_bsr** out) {
   m->hidden = c.dim * c.mlp_expansion_factor;
   m->qkv_ld = (3 * m->inner + c.heads + 3) / 4 * 4;
   m->feat = m->F * c.audio_channels * 2;
+  m->gfeat = c.mel ? 2 * c.n_freq_indices : m->feat;
   const int dim = c.dim, inner = m->inner;
   for (int i = 0; i < c.depth; ++i)
     for (int j = 0; j < 2; ++j) {
@@ -388,8 +451,9 @@ extern "C" int sesa_bsr_create(const sesa_bsr_config* cfg, sesa_bsr** out) {
         L.time = j == 0;
         m->layers.push_back(L);
       }
+      if (c.mel) add_param(m, "layers." + std::to_string(i) + "." + std::to_string(j) + ".norm.gamma", {dim});
     }
-  add_param(m, "final_norm.gamma", {dim});
+  if (!c.mel) add_param(m, "final_norm.gamma", {dim});
   for (int b = 0; b < m->nb; ++b) {
     const std::string p = "band_split.to_features." + std::to_string(b);
     add_param(m, p + ".0.gamma", {m->dims[b]});
@@ -399,10 +463,12 @@ extern "C" int sesa_bsr_create(const sesa_bsr_config* cfg, sesa_bsr** out) {
   for (int n = 0; n < c.num_stems; ++n)
     for (int b = 0; b < m->nb; ++b) {
       const std::string p = "mask_estimators." + std::to_string(n) + ".to_freqs." + std::to_string(b) + ".0";
-      add_param(m, p + ".0.weight", {m->hidden, dim});
-      add_param(m, p + ".0.bias", {m->hidden});
-      add_param(m, p + ".2.weight", {2 * m->dims[b], m->hidden});
-      add_param(m, p + ".2.bias", {2 * m->dims[b]});
+      for (int li = 0; li < m->n_lin; ++li) {
+        const int in = li == 0 ? dim : m->hidden;
+        const int out = li == m->n_lin - 1 ? 2 * m->dims[b] : m->hidden;
+        add_param(m, p + "." + std::to_string(2 * li) + ".weight", {out, in});
+        add_param(m, p + "." + std::to_string(2 * li) + ".bias", {out});
+      }
     }
   *out = m;
   return SESA_OK;
@@ -501,31 +567,35 @@ extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
         rope.push_back(make_float2((float)cos((double)ang), (float)sin((double)ang)));
       }
   }
-  // mask estimators: final RMSNorm gamma folded into every band's first Linear; second Linear's
-  // rows interleaved (a_j, b_j) so the GLU pairs sit in adjacent columns
-  const auto& gfin = P(m, "final_norm.gamma");
-  m->mlp1.groups.clear();
-  m->mlp2.groups.clear();
+  // mask estimators: (BS) final RMSNorm gamma folded into every band's first Linear; the last
+  // Linear's rows interleaved (a_j, b_j) so the GLU pairs sit in adjacent columns
   const int hid = m->hidden;
+  std::vector<float> ones(dim, 1.f);
+  const std::vector<float>& gfin = c.mel ? ones : P(m, "final_norm.gamma");
+  m->mlp.assign(m->n_lin, Gemm{});
   for (int n = 0; n < c.num_stems; ++n)
     for (int b = 0; b < m->nb; ++b) {
       const std::string p = "mask_estimators." + std::to_string(n) + ".to_freqs." + std::to_string(b) + ".0";
-      const auto& W1 = P(m, p + ".0.weight");
-      const auto& b1 = P(m, p + ".0.bias");
-      TokGroup g = pack_group(hid, dim, [&](int r, int k) { return W1[(int64_t)r * dim + k] * gfin[k]; }, true,
-                              [&](int r) { return b1[r]; }, blob, bias);
-      g.x_off = (int64_t)b * dim;
-      g.o_off = (int64_t)b * hid;
-      m->mlp1.groups.push_back(g);
-      const auto& W2 = P(m, p + ".2.weight");
-      const auto& b2 = P(m, p + ".2.bias");
       const int din = m->dims[b];
-      auto src_row = [din](int r) { return (r & 1) ? din + (r >> 1) : (r >> 1); };
-      g = pack_group(2 * din, hid, [&](int r, int k) { return W2[(int64_t)src_row(r) * hid + k]; }, true,
-                     [&](int r) { return b2[src_row(r)]; }, blob, bias);
-      g.x_off = (int64_t)b * hid;
-      g.o_off = m->offs[b];
-      m->mlp2.groups.push_back(g);
+      for (int li = 0; li < m->n_lin; ++li) {
+        const auto& W = P(m, p + "." + std::to_string(2 * li) + ".weight");
+        const auto& bv = P(m, p + "." + std::to_string(2 * li) + ".bias");
+        const int K = li == 0 ? dim : hid;
+        const bool last = li == m->n_lin - 1;
+        TokGroup g;
+        if (!last) {
+          g = pack_group(hid, K, [&](int r, int k) { return W[(int64_t)r * K + k] * (li == 0 ? gfin[k] : 1.f); },
+                         true, [&](int r) { return bv[r]; }, blob, bias);
+          g.o_off = (int64_t)b * hid;
+        } else {
+          auto src_row = [din](int r) { return (r & 1) ? din + (r >> 1) : (r >> 1); };
+          g = pack_group(2 * din, K, [&](int r, int k) { return W[(int64_t)src_row(r) * K + k]; }, true,
+                         [&](int r) { return bv[src_row(r)]; }, blob, bias);
+          g.o_off = m->offs[b];
+        }
+        g.x_off = (int64_t)b * (li == 0 ? dim : hid);
+        m->mlp[li].groups.push_back(g);
+      }
     }
   if (m->d_w) (void)hipFree(m->d_w);
   if (m->d_bias) (void)hipFree(m->d_bias);
@@ -545,8 +615,43 @@ extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
     SESA_CHECK_HIP(hipMemcpyAsync(m->d_rope, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice, st));
   SESA_CHECK_HIP(hipStreamSynchronize(st));
   int rc = upload_groups(m->band);
-  if (!rc) rc = upload_groups(m->mlp1);
-  if (!rc) rc = upload_groups(m->mlp2);
+  for (auto& g : m->mlp)
+    if (!rc) rc = upload_groups(g);
+  if (!rc && c.mel) {
+    std::vector<float> aff;
+    m->norm_off.clear();
+    for (int i = 0; i < c.depth; ++i)
+      for (int j = 0; j < 2; ++j) {
+        const std::string tp = "layers." + std::to_string(i) + "." + std::to_string(j);
+        m->norm_off[tp] = (int64_t)aff.size();
+        const auto& gm = P(m, tp + ".norm.gamma");
+        aff.insert(aff.end(), gm.begin(), gm.end());
+      }
+    if (m->d_affine) (void)hipFree(m->d_affine);
+    m->d_affine = nullptr;
+    SESA_CHECK_HIP(hipMalloc(&m->d_affine, aff.size() * sizeof(float)));
+    SESA_CHECK_HIP(hipMemcpy(m->d_affine, aff.data(), aff.size() * sizeof(float), hipMemcpyHostToDevice));
+    // gathered feature j -> spectrum feature; CSR inverse for the scatter-average
+    std::vector<int> gidx(m->gfeat);
+    for (int p2 = 0; p2 < (int)m->fidx.size(); ++p2) {
+      gidx[2 * p2] = 2 * m->fidx[p2];
+      gidx[2 * p2 + 1] = 2 * m->fidx[p2] + 1;
+    }
+    std::vector<int> cnt(m->feat + 1, 0), ptr(m->feat + 1, 0), idx(m->gfeat);
+    for (int j = 0; j < m->gfeat; ++j) cnt[gidx[j]]++;
+    for (int f = 0; f < m->feat; ++f) ptr[f + 1] = ptr[f] + cnt[f];
+    std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+    for (int j = 0; j < m->gfeat; ++j) idx[fill[gidx[j]]++] = j;  // ascending j per feature
+    auto up = [&](int** d, const std::vector<int>& h) -> int {
+      if (*d) (void)hipFree(*d);
+      SESA_CHECK_HIP(hipMalloc(d, h.size() * sizeof(int)));
+      SESA_CHECK_HIP(hipMemcpy(*d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
+      return SESA_OK;
+    };
+    rc = up(&m->d_gidx, gidx);
+    if (!rc) rc = up(&m->d_inv_ptr, ptr);
+    if (!rc) rc = up(&m->d_inv_idx, idx);
+  }
   for (auto& L : m->layers) {
     if (!rc) rc = upload_groups(L.qkv);
     if (!rc) rc = upload_groups(L.out);
@@ -564,7 +669,7 @@ extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
 namespace {
 
 struct Plan {
-  size_t spec, x, qkv, ao, h, mask, frames, total;
+  size_t spec, xg, x, qkv, ao, h, h2, mask, maskg, frames, total;
 };
 
 Plan plan(const sesa_bsr* m, int B) {
@@ -573,11 +678,14 @@ Plan plan(const sesa_bsr* m, int B) {
   Plan p{};
   size_t off = 0;
   p.spec = off; off += al((size_t)B * m->T * m->feat);
+  p.xg = off; off += m->cfg.mel ? al((size_t)B * m->T * m->gfeat) : 0;
   p.x = off; off += al((size_t)tok * m->cfg.dim);
   p.qkv = off; off += al((size_t)tok * m->qkv_ld);
   p.ao = off; off += al((size_t)tok * m->inner);
   p.h = off; off += al((size_t)tok * std::max(m->ff, m->hidden));
+  p.h2 = off; off += m->n_lin >= 3 ? al((size_t)tok * m->hidden) : 0;
   p.mask = off; off += al((size_t)m->cfg.num_stems * B * m->T * m->feat);
+  p.maskg = off; off += m->cfg.mel ? al((size_t)m->cfg.num_stems * B * m->T * m->gfeat) : 0;
   p.frames = off; off += al((size_t)B * m->cfg.num_stems * m->cfg.audio_channels * m->T * kN);
   p.total = off;
   return p;
@@ -632,6 +740,9 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
   float* H = reinterpret_cast<float*>(ws + pl.h);
   float* MASK = reinterpret_cast<float*>(ws + pl.mask);
   float* FR = reinterpret_cast<float*>(ws + pl.frames);
+  float* XG = reinterpret_cast<float*>(ws + pl.xg);
+  float* H2 = reinterpret_cast<float*>(ws + pl.h2);
+  float* MASKG = reinterpret_cast<float*>(ws + pl.maskg);
   const int x3 = c.precision == SESA_PREC_BF16X3 ? 1 : 0;
   const int ch = c.audio_channels, dim = c.dim;
   const int T = m->T, nb = m->nb;
@@ -653,13 +764,23 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
     rc = launch_tok_gemm(a, x3, st);
     profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(gm, rows));
   };
+  const int64_t rowsBT = (int64_t)B * T;
+  const float* bs_in = spec;
+  if (c.mel) {  // gather the overlapping mel bands' (f, s, c) features (mel_band_roformer.py:522-528)
+    const int64_t n = rowsBT * m->gfeat;
+    hipLaunchKernelGGL(mel_gather_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, spec, m->feat,
+                       m->d_gidx, m->gfeat, rowsBT, XG);
+    SESA_CHECK_LAUNCH();
+    bs_in = XG;
+  }
   // band split: rows (b, t), groups over bands -> X rows (b, t, band)
   {
-    TokGemmArgs a = gemm_args(m, m->band, spec, m->feat, X, (int64_t)nb * dim, B * T);
+    TokGemmArgs a = gemm_args(m, m->band, bs_in, m->gfeat, X, (int64_t)nb * dim, B * T);
     a.rownorm = 1;
     gemm(a, m->band, B * T);
   }
-  for (auto& L : m->layers) {
+  for (size_t li = 0; li < m->layers.size(); ++li) {
+    const Layer& L = m->layers[li];
     // attention: QKV + gates (RMSNorm, rotary on q/k)
     {
       TokGemmArgs a = gemm_args(m, L.qkv, X, dim, QKV, m->qkv_ld, M);
@@ -718,26 +839,50 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
       gemm(a, L.ff2, M);
     }
     if (rc) return rc;
+    // Mel: Transformer.norm after the last layer of each (time / freq) transformer (:218, :226)
+    const bool stack_end = li + 1 == m->layers.size() || m->layers[li + 1].time != L.time ||
+                           m->layers[li + 1].prefix.substr(0, m->layers[li + 1].prefix.find(".layers.")) !=
+                               L.prefix.substr(0, L.prefix.find(".layers."));
+    if (c.mel && stack_end) {
+      const std::string tp = L.prefix.substr(0, L.prefix.find(".layers."));
+      hipLaunchKernelGGL(rownorm_kernel, dim3((unsigned)((Mtok + 3) / 4)), dim3(256), 0, st, X, Mtok, dim,
+                         m->d_affine + m->norm_off.at(tp));
+      SESA_CHECK_LAUNCH();
+    }
   }
-  // mask estimators (final RMSNorm folded into MLP1); per stem: MLP1 (tanh) then MLP2 (GLU)
+  // mask estimators, per stem: Linear (+Tanh) x (n_lin - 1), last Linear + GLU.  BS: final RMSNorm
+  // folded into the first Linear (rownorm).  Mel: GLU outputs land in the gathered layout and are
+  // scatter-averaged onto the spectrum features.
   for (int n = 0; n < c.num_stems && !rc; ++n) {
-    Gemm g1, g2;
-    g1.groups.assign(m->mlp1.groups.begin() + n * nb, m->mlp1.groups.begin() + (n + 1) * nb);
-    g2.groups.assign(m->mlp2.groups.begin() + n * nb, m->mlp2.groups.begin() + (n + 1) * nb);
-    TokGemmArgs a = gemm_args(m, m->mlp1, X, (int64_t)nb * dim, H, (int64_t)nb * m->hidden, B * T);
-    a.groups = m->mlp1.d_groups + n * nb;
-    a.n_groups = nb;
-    a.rownorm = 1;
-    a.act = TOK_ACT_TANH;
-    gemm(a, g1, B * T);
-    TokGemmArgs b = gemm_args(m, m->mlp2, H, (int64_t)nb * m->hidden, MASK + (int64_t)n * B * T * m->feat, m->feat,
-                              B * T);
-    b.groups = m->mlp2.d_groups + n * nb;
-    b.n_groups = nb;
-    b.glu = 1;
-    gemm(b, g2, B * T);
+    const float* hin = X;
+    int64_t hin_ld = (int64_t)nb * dim;
+    float* hbuf[2] = {H, H2};
+    for (int li = 0; li < m->n_lin && !rc; ++li) {
+      const Gemm& G = m->mlp[li];
+      Gemm gf;
+      gf.groups.assign(G.groups.begin() + n * nb, G.groups.begin() + (n + 1) * nb);
+      const bool last = li == m->n_lin - 1;
+      float* o = last ? (c.mel ? MASKG + (int64_t)n * rowsBT * m->gfeat : MASK + (int64_t)n * rowsBT * m->feat)
+                      : hbuf[li & 1];
+      const int64_t o_ld = last ? (c.mel ? m->gfeat : m->feat) : (int64_t)nb * m->hidden;
+      TokGemmArgs a = gemm_args(m, G, hin, hin_ld, o, o_ld, B * T);
+      a.groups = G.d_groups + n * nb;
+      a.n_groups = nb;
+      if (li == 0 && !c.mel) a.rownorm = 1;
+      if (last) a.glu = 1;
+      else a.act = TOK_ACT_TANH;
+      gemm(a, gf, B * T);
+      hin = o;
+      hin_ld = o_ld;
+    }
+    if (c.mel && !rc) {
+      const int64_t nn = rowsBT * m->feat;
+      hipLaunchKernelGGL(mel_scatter_avg_kernel, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, st,
+                         MASKG + (int64_t)n * rowsBT * m->gfeat, m->gfeat, m->d_inv_ptr, m->d_inv_idx, m->feat, rowsBT,
+                         MASK + (int64_t)n * rowsBT * m->feat);
+      SESA_CHECK_LAUNCH();
+    }
   }
-  if (rc) return rc;
   const int n_sig = B * c.num_stems * ch;
   tok = profile_begin(st);
   hipLaunchKernelGGL(bsr_istft_frames_kernel, dim3(T, n_sig), dim3(kFT), 0, st, spec, MASK, ch, c.num_stems, B, T, tb,
@@ -759,8 +904,11 @@ extern "C" int sesa_bsr_destroy(sesa_bsr* m) {
     if (g.d_groups) (void)hipFree(g.d_groups);
   };
   fr(m->band);
-  fr(m->mlp1);
-  fr(m->mlp2);
+  for (auto& g : m->mlp) fr(g);
+  if (m->d_gidx) (void)hipFree(m->d_gidx);
+  if (m->d_inv_ptr) (void)hipFree(m->d_inv_ptr);
+  if (m->d_inv_idx) (void)hipFree(m->d_inv_idx);
+  if (m->d_affine) (void)hipFree(m->d_affine);
   for (auto& L : m->layers) {
     fr(L.qkv);
     fr(L.out);

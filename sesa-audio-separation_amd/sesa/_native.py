@@ -25,7 +25,9 @@ class SesaBsrConfig(ctypes.Structure):
     _fields_ = [(n, c_int) for n in (
         "chunk_size", "audio_channels", "n_fft", "hop_length", "win_length", "dim", "depth", "heads", "dim_head",
         "time_transformer_depth", "freq_transformer_depth", "num_stems", "mask_estimator_depth",
-        "mlp_expansion_factor", "n_bands")] + [("freqs_per_bands", ctypes.POINTER(c_int)), ("precision", c_int)]
+        "mlp_expansion_factor", "n_bands")] + [("freqs_per_bands", ctypes.POINTER(c_int)), ("precision", c_int),
+                                               ("mel", c_int), ("n_freq_indices", c_int),
+                                               ("freq_indices", ctypes.POINTER(c_int))]
 
 
 # name -> (restype, argtypes); every symbol declared in include/sesa.h

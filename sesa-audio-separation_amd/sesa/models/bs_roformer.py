@@ -96,10 +96,17 @@ class BSRoformer:
         return out
 
     # ---- native handles ----
+    _mel = False
+    _freq_indices = ()
+
     def _config(self, chunk):
         fpb = (ctypes.c_int * len(self.freqs_per_bands))(*self.freqs_per_bands)
+        fidx = (ctypes.c_int * max(1, len(self._freq_indices)))(*self._freq_indices)
         c = N.SesaBsrConfig(chunk_size=int(chunk), n_bands=len(self.freqs_per_bands), freqs_per_bands=fpb,
-                            precision=N.SESA_PREC_BF16 if self.precision == "bf16" else N.SESA_PREC_BF16X3, **self._kw)
+                            precision=N.SESA_PREC_BF16 if self.precision == "bf16" else N.SESA_PREC_BF16X3,
+                            mel=1 if self._mel else 0, n_freq_indices=len(self._freq_indices), freq_indices=fidx,
+                            **self._kw)
+        self._keep = (fpb, fidx)   # ctypes arrays must outlive the create call
         return c, fpb
 
     def _create(self, chunk):

@@ -20,7 +20,7 @@ REFERENCE_MODEL_TYPES = (
     "bandit_v2", "scnet_unofficial", "scnet", "apollo", "bs_mamba2", "experimental_mdx23c_stht",
     "mel_band_roformer_experimental", "bs_roformer_experimental", "bs_roformer_custom", "scnet_tran", "scnet_masked",
     "conformer", "mel_band_conformer")
-NATIVE_MODEL_TYPES = ("mdx23c", "bs_roformer")
+NATIVE_MODEL_TYPES = ("mdx23c", "bs_roformer", "mel_band_roformer")
 
 
 def get_model_from_config(model_type: str, config_path: str):
@@ -29,6 +29,9 @@ def get_model_from_config(model_type: str, config_path: str):
     if model_type == "mdx23c":
         from .models.mdx23c import TFC_TDF_net
         model = TFC_TDF_net(config)
+    elif model_type == "mel_band_roformer":
+        from .models.mel_band_roformer import MelBandRoformer
+        model = MelBandRoformer(**dict(config.model))  # utils.py:101-103
     elif model_type == "bs_roformer":
         from .models.bs_roformer import BSRoformer
         model = BSRoformer(**dict(config.model))  # utils.py:104-106

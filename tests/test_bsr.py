@@ -112,3 +112,63 @@ def test_demix_matches_reference(golden, dev):
     assert prog == list(g["progress"])
     assert res["vocals"].shape == g["vocals"].shape
     assert rms(res["vocals"], g["vocals"]) <= RMS_GATE
+
+
+# ---------------- Mel-Band-Roformer (same native engine, mel = 1) ----------------
+def _mel_model(cfg_name, affine="random", precision="bf16x3"):
+    from oracle import mel_band_roformer as om
+    from sesa.utils import get_model_from_config
+    m, c = get_model_from_config("mel_band_roformer", os.path.join(CONFIGS, cfg_name))
+    sd = om.synth_params(om.load_cfg(os.path.join(CONFIGS, cfg_name)), affine)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    m.set_precision(precision)
+    return m, c
+
+
+@pytest.mark.parametrize("cfg_name,tag", [("config_mel_band_roformer_vocals.yaml", "vocals"),
+                                          ("config_mel_band_roformer_small.yaml", "small")])
+def test_mel_registry_matches_reference_state_dict(cfg_name, tag):
+    from sesa import _native as N
+    from sesa.utils import get_model_from_config
+    m, c = get_model_from_config("mel_band_roformer", os.path.join(CONFIGS, cfg_name))
+    with open(os.path.join(GOLDEN, f"params_mbr_{tag}.json")) as f:
+        ref = [(n, tuple(s)) for n, s in json.load(f)]
+    assert [(n, tuple(t.shape)) for n, t in m.named_parameters()] == ref
+    h = m._create(c.audio.chunk_size)
+    try:
+        names = []
+        for i in range(N.lib().sesa_bsr_num_params(h)):
+            nm = ctypes.c_char_p()
+            assert N.lib().sesa_bsr_param_info(h, i, ctypes.byref(nm), None) == 0
+            names.append(nm.value.decode())
+    finally:
+        N.lib().sesa_bsr_destroy(h)
+    assert names == [n for n, _ in ref]
+
+
+def test_mel_band_layout_matches_reference(golden):
+    g = golden("mbr_small.npz")
+    from sesa.utils import get_model_from_config
+    m, _ = get_model_from_config("mel_band_roformer", os.path.join(CONFIGS, "config_mel_band_roformer_small.yaml"))
+    assert np.array_equal(m.freq_indices.numpy(), g["freq_indices"])
+
+
+@pytest.mark.gpu
+def test_mel_forward_small_matches_reference(golden, dev):
+    g = golden("mbr_small.npz")
+    m, _ = _mel_model("config_mel_band_roformer_small.yaml", str(g["affine"]))
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    assert y.shape == g["y"].shape
+    err = rms(y, g["y"])
+    print(f"mel-band small forward rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    assert err <= RMS_GATE
+
+
+@pytest.mark.gpu
+def test_mel_forward_full_chunk_matches_reference(golden, dev):
+    g = golden("mbr_full_chunk.npz")
+    m, _ = _mel_model("config_mel_band_roformer_vocals.yaml", str(g["affine"]))
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"mel-band vocals full chunk rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    assert err <= RMS_GATE
