@@ -155,6 +155,36 @@ int sesa_bsr_forward(sesa_bsr* m, const float* x, int batch, float* out, void* w
 int sesa_bsr_destroy(sesa_bsr* m);
 
 /* ---------------------------------------------------------------------------------------
+ * SCNet (models/scnet/scnet.py:239-373 SCNet + models/scnet/separation.py).
+ * n_fft = win_size = 4096, conv_kernel 3, even num_dplayer, LSTM hidden (dims[-1] * expand, x2 on
+ * the odd dual-path layers) in {32, 64, 128, 256}.  Parameters are the reference state_dict() keys.
+ * band_sr is double so the split points match the reference's math.ceil(Fr * SR) (scnet.py:117-122).
+ */
+typedef struct sesa_scnet_config {
+  int chunk_size, audio_channels, n_sources;
+  int n_fft, hop_size, win_size, normalized;
+  int n_dims;
+  const int* dims;              /* host array [n_dims] (model.dims), copied by create          */
+  double band_sr[3];
+  int band_stride[3], band_kernel[3], conv_depths[3];
+  int compress, conv_kernel, num_dplayer, expand;
+  int precision;                /* SESA_PREC_*: the MFMA token GEMMs (LSTM input / output Linears) */
+} sesa_scnet_config;
+
+typedef struct sesa_scnet sesa_scnet;
+
+int sesa_scnet_create(const sesa_scnet_config* cfg, sesa_scnet** out);
+int sesa_scnet_num_params(const sesa_scnet* m);
+int sesa_scnet_param_info(const sesa_scnet* m, int i, const char** name, int64_t* numel);
+int sesa_scnet_set_param(sesa_scnet* m, const char* name, const float* host, int64_t numel);
+int sesa_scnet_finalize(sesa_scnet* m, void* stream);
+size_t sesa_scnet_workspace_size(const sesa_scnet* m, int batch);
+/* x [batch, audio_channels, chunk_size] -> out [batch, n_sources, audio_channels, chunk_size] */
+int sesa_scnet_forward(sesa_scnet* m, const float* x, int batch, float* out, void* workspace,
+                       size_t workspace_bytes, void* stream);
+int sesa_scnet_destroy(sesa_scnet* m);
+
+/* ---------------------------------------------------------------------------------------
  * Ensemble blend (ensemble.py:172-407, AudioEnsembleEngine.process_waveform / process_spectral /
  * run_ensemble's buffer loop).  Methods in the reference's --type order.
  *   x   [n_files][n_ch][L] fp32 (device; the inputs cut to the shortest, ensemble.py:304-306)
@@ -193,7 +223,9 @@ int sesa_blend_f32(const float* x, int n_files, int n_ch, int64_t L, int64_t buf
 #define SESA_KCLASS_ACT 7     /* act_split: norm + GELU + bf16 split pass (work = HBM bytes) */
 #define SESA_KCLASS_TOKGEMM 8 /* token-major Linear layers (transformer models)           */
 #define SESA_KCLASS_ATTN 9    /* flash attention (work = 4 L^2 d FLOP per sequence-head)    */
-#define SESA_KCLASS_COUNT 10
+#define SESA_KCLASS_LSTM 10   /* SCNet bi-LSTM recurrence (work = h W_hh^T FLOP)            */
+#define SESA_KCLASS_SIMT 11   /* SCNet fp32 convolutions / feature-conversion DFTs          */
+#define SESA_KCLASS_COUNT 12
 int sesa_profile_enable(int enable);   /* 1: start recording (clears previous records), 0: stop */
 int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work);
 

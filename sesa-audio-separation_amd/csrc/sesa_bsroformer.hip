@@ -249,32 +249,12 @@ __global__ void mel_scatter_avg_kernel(const float* __restrict__ mg, int G, cons
 }
 
 // ---------------------------------------------------------------------------------------------
-uint16_t f2bf(float f) {
-  uint32_t u;
-  memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-float bf2f(uint16_t h) {
-  uint32_t u = (uint32_t)h << 16;
-  float f;
-  memcpy(&f, &u, 4);
-  return f;
-}
-
 struct Param {
   std::string name;
   std::vector<int64_t> shape;
   int64_t numel = 0;
   std::vector<float> host;
   bool set = false;
-};
-
-struct Gemm {          // one packed (possibly grouped) GEMM
-  std::vector<TokGroup> groups;
-  TokGroup* d_groups = nullptr;
-  int n_tiles_n = 0;
 };
 
 struct Layer {         // one transformer layer (Attention + FeedForward)
@@ -328,51 +308,6 @@ int add_param(sesa_bsr* m, const std::string& name, std::vector<int64_t> shape) 
 
 const std::vector<float>& P(sesa_bsr* m, const std::string& name) { return m->params[m->by_name.at(name)].host; }
 
-// Pack W[n][k] (row accessor) of an N x K GEMM for one group; returns the TokGroup with w_off/b_off set.
-template <class RowFn, class BiasFn>
-TokGroup pack_group(int N, int K, RowFn row_val, bool has_bias, BiasFn bias_val, std::vector<uint16_t>& blob,
-                    std::vector<float>& bias) {
-  TokGroup g{};
-  g.K = K;
-  g.N = N;
-  g.w_off = (int64_t)blob.size();
-  const int nt = (N + kTokBN - 1) / kTokBN, nch = (K + kTokBK - 1) / kTokBK;
-  const int64_t img = (int64_t)kTokBN * kTokBK;
-  blob.resize(blob.size() + (size_t)nt * nch * 2 * img, 0);
-  uint16_t* base = blob.data() + g.w_off;
-  for (int t = 0; t < nt; ++t)
-    for (int kc = 0; kc < nch; ++kc) {
-      uint16_t* hi = base + ((int64_t)t * nch + kc) * 2 * img;
-      uint16_t* lo = hi + img;
-      for (int r = 0; r < kTokBN; ++r) {
-        const int n = t * kTokBN + r;
-        for (int kk = 0; kk < kTokBK; ++kk) {
-          const int k = kc * kTokBK + kk;
-          const float v = (n < N && k < K) ? row_val(n, k) : 0.f;
-          const int64_t o = (int64_t)r * kTokBK + (((kk >> 3) ^ ((r >> 2) & 3)) << 3) + (kk & 7);
-          const uint16_t h = f2bf(v);
-          hi[o] = h;
-          lo[o] = f2bf(v - bf2f(h));
-        }
-      }
-    }
-  g.b_off = -1;
-  if (has_bias) {
-    g.b_off = (int64_t)bias.size();
-    for (int n = 0; n < N; ++n) bias.push_back(bias_val(n));
-    while (bias.size() % 4) bias.push_back(0.f);
-  }
-  return g;
-}
-
-int upload_groups(Gemm& gm) {
-  if (gm.d_groups) (void)hipFree(gm.d_groups);
-  SESA_CHECK_HIP(hipMalloc(&gm.d_groups, gm.groups.size() * sizeof(TokGroup)));
-  SESA_CHECK_HIP(hipMemcpy(gm.d_groups, gm.groups.data(), gm.groups.size() * sizeof(TokGroup), hipMemcpyHostToDevice));
-  gm.n_tiles_n = 0;
-  for (auto& g : gm.groups) gm.n_tiles_n = std::max(gm.n_tiles_n, (g.N + kTokBN - 1) / kTokBN);
-  return SESA_OK;
-}
 
 }  // namespace
 }  // namespace sesa

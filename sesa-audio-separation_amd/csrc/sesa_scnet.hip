@@ -1,0 +1,1499 @@
+// SCNet (sparse compression network): parameter registry, weight packing, spectral front / back
+// end and the forward pass (gfx950).
+//
+// Reference: models/scnet/scnet.py:239-373 (SCNet; SDlayer :86-148, SUlayer :151-196, SDblock
+// :199-236, ConvolutionModule :15-52, FusionLayer :55-83) and models/scnet/separation.py
+// (DualPathRNN :37-86, FeatureConversion :6-34, SeparationNet :89-113).  Parameter names /
+// shapes are the reference state_dict keys, so released checkpoints load by name.
+//
+// Data layout: every activation is channels-last fp32 [B][F][T][C] (F = frequency rows, T = STFT
+// frames).  With F outermost, the SD layer's band outputs and the SU layer's trimmed band outputs
+// are contiguous F ranges of one buffer (torch.cat over F is free), a ConvolutionModule row
+// (b, f) is one contiguous [T][C] block, and the dual-path LSTMs read both of their sequence
+// families -- (b, t) -> f and (b, f) -> t -- as strided token rows of the same buffer.
+//
+// Kernels (all fp32 FMA unless noted):
+//   scn_stft_kernel         4096-point normalized rectangular-window STFT (2048-point complex
+//                           radix-4/2 Stockham FFT in LDS + real split), virtual right zero pad
+//   scn_sdconv_kernel       SD layer band conv (kernel k x 1, stride s x 1) into the band's F range
+//   scn_cm_in_kernel        ConvolutionModule head, one workgroup per (b, f) row: GroupNorm(1, C)
+//                           stats, normalise-on-load, conv1d k3 (weights in LDS), GLU
+//   scn_cm_out_kernel       ConvolutionModule tail per row: depthwise k3, GroupNorm(1, h), Swish,
+//                           1x1 conv, residual (+ the SD block's GELU after the last layer)
+//   scn_conv3x3_kernel      3x3 conv over (F, T), 4 x 32 positions x 64 output columns per
+//                           workgroup, 16-channel K chunks staged in LDS; FusionLayer: skip add on
+//                           load, repeated input folded into the weights, GLU in the epilogue
+//   scn_convtr_kernel       SU layer transposed band conv with the symmetric trim
+//   scn_gn_*                DualPathRNN GroupNorm(1, d) (fp64 statistics)
+//   tok_gemm (MFMA)         LSTM input projections (both directions, b_ih + b_hh) and the
+//                           Linear(2H -> d) + residual -- sesa_tokgemm.hip, bf16x3 in parity mode
+//   scn_lstm_kernel         bi-LSTM recurrence: one workgroup per (sequence block, direction),
+//                           h in LDS, c in registers, W_hh^T streamed from L2
+//   scn_rfft / scn_irfft    FeatureConversion as direct DFTs over T (norm="ortho")
+//   scn_istft_*             normalized inverse (c2r by_root_n), OLA / envelope, trim and crop
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sesa_common.hpp"
+#include "sesa_internal.hpp"
+#include "sesa_tokgemm.hpp"
+
+namespace sesa {
+namespace {
+
+constexpr int kSN = 4096;  // n_fft
+constexpr int kSH = 2048;  // complex FFT length
+constexpr int kST = 256;   // threads per workgroup
+
+struct ScnTables {
+  float2* tw = nullptr;   // exp(-2 pi i j / 2048), j < 2048
+  float2* twN = nullptr;  // exp(-2 pi i k / 4096), k <= 2048
+};
+std::mutex g_mu;
+std::vector<ScnTables> g_tabs;
+
+int get_tables(ScnTables* out) {
+  int dev = 0;
+  SESA_CHECK_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_mu);
+  if ((int)g_tabs.size() <= dev) g_tabs.resize(dev + 1);
+  ScnTables& t = g_tabs[dev];
+  if (!t.tw) {
+    std::vector<float2> a(kSH), b(kSH + 1);
+    for (int j = 0; j < kSH; ++j) {
+      const double ang = -2.0 * M_PI * j / kSH;
+      a[j] = make_float2((float)cos(ang), (float)sin(ang));
+    }
+    for (int k = 0; k <= kSH; ++k) {
+      const double ang = -2.0 * M_PI * k / kSN;
+      b[k] = make_float2((float)cos(ang), (float)sin(ang));
+    }
+    SESA_CHECK_HIP(hipMalloc(&t.tw, kSH * sizeof(float2)));
+    SESA_CHECK_HIP(hipMalloc(&t.twN, (kSH + 1) * sizeof(float2)));
+    SESA_CHECK_HIP(hipMemcpy(t.tw, a.data(), kSH * sizeof(float2), hipMemcpyHostToDevice));
+    SESA_CHECK_HIP(hipMemcpy(t.twN, b.data(), (kSH + 1) * sizeof(float2), hipMemcpyHostToDevice));
+  }
+  *out = t;
+  return SESA_OK;
+}
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+// 2048-point Stockham FFT in LDS: five radix-4 stages then one radix-2 stage (256 threads).
+template <bool INV>
+__device__ float2* fft2048(float2* x, float2* y, const float2* __restrict__ tw) {
+  int n = kSH, s = 1;
+#pragma unroll 1
+  for (int stage = 0; stage < 5; ++stage) {
+    const int m = n >> 2;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int bfly = threadIdx.x + r * kST;  // 512 butterflies per stage
+      const int q = bfly & (s - 1);
+      const int p = bfly >> __builtin_ctz(s);
+      const float2 a = x[q + s * p], b = x[q + s * (p + m)], c = x[q + s * (p + 2 * m)], d = x[q + s * (p + 3 * m)];
+      float2 w1 = tw[p * s], w2 = tw[2 * p * s], w3 = tw[3 * p * s];
+      if (INV) { w1 = cconj(w1); w2 = cconj(w2); w3 = cconj(w3); }
+      const float2 apc = cadd(a, c), amc = csub(a, c), bpd = cadd(b, d), bmd = csub(b, d);
+      const float2 jbmd = INV ? make_float2(-bmd.y, bmd.x) : make_float2(bmd.y, -bmd.x);
+      y[q + s * (4 * p + 0)] = cadd(apc, bpd);
+      y[q + s * (4 * p + 1)] = cmul(w1, cadd(amc, jbmd));
+      y[q + s * (4 * p + 2)] = cmul(w2, csub(apc, bpd));
+      y[q + s * (4 * p + 3)] = cmul(w3, csub(amc, jbmd));
+    }
+    float2* t = x; x = y; y = t;
+    n = m;
+    s <<= 2;
+  }
+  __syncthreads();  // n = 2, s = 1024: final radix-2 stage, unit twiddles
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = threadIdx.x + r * kST;
+    const float2 a = x[q], b = x[q + 1024];
+    y[q] = cadd(a, b);
+    y[q + 1024] = csub(a, b);
+  }
+  __syncthreads();
+  return y;
+}
+
+// x [B][ach][chunk] (right zero-padded to Lpad virtually, scnet.py:330-333) -> spec [B][F0][T][2*ach],
+// channel 2*s + (re, im) (scnet.py:343-348).  torch.stft: center, reflect, window = ones.
+__global__ void __launch_bounds__(kST) scn_stft_kernel(const float* __restrict__ x, int ach, int chunk, int Lpad,
+                                                       int hop, int T, float scale, ScnTables tb,
+                                                       float* __restrict__ spec) {
+  __shared__ float2 bufA[kSH];
+  __shared__ float2 bufB[kSH];
+  const int t = blockIdx.x;
+  const int sig = blockIdx.y;
+  const int b = sig / ach, s = sig - b * ach;
+  const float* xs = x + (int64_t)sig * chunk;
+  const int64_t base = (int64_t)t * hop - kSN / 2;
+  for (int m = threadIdx.x; m < kSH; m += kST) {
+    float v[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      int64_t pos = base + 2 * m + e;
+      if (pos < 0) pos = -pos;
+      if (pos >= Lpad) pos = 2 * (int64_t)(Lpad - 1) - pos;
+      v[e] = pos < chunk ? xs[pos] : 0.f;
+    }
+    bufA[m] = make_float2(v[0], v[1]);
+  }
+  const float2* Z = fft2048<false>(bufA, bufB, tb.tw);
+  const int C0 = 2 * ach;
+  for (int k = threadIdx.x; k <= kSH; k += kST) {
+    const float2 zk = Z[k & (kSH - 1)];
+    const float2 zm = cconj(Z[(kSH - k) & (kSH - 1)]);
+    const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y + zm.y));
+    const float2 D = csub(zk, zm);
+    const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
+    const float2 X = cadd(E, cmul(tb.twN[k], O));
+    *reinterpret_cast<float2*>(spec + (((int64_t)b * (kSH + 1) + k) * T + t) * C0 + 2 * s) =
+        make_float2(X.x * scale, X.y * scale);
+  }
+}
+
+// spec [B][F0][T][2*nsig] -> frames [B*nsig][T][4096] (c2r with scale, window = ones; scnet.py:364-368)
+__global__ void __launch_bounds__(kST) scn_istft_frames_kernel(const float* __restrict__ spec, int nsig, int T,
+                                                               float scale, ScnTables tb, float* __restrict__ fw) {
+  __shared__ float2 bufA[kSH];
+  __shared__ float2 bufB[kSH + 1];
+  const int t = blockIdx.x;
+  const int sg = blockIdx.y;
+  const int b = sg / nsig, m = sg - b * nsig;
+  const int C = 2 * nsig;
+  for (int k = threadIdx.x; k <= kSH; k += kST) {
+    float2 X = *reinterpret_cast<const float2*>(spec + (((int64_t)b * (kSH + 1) + k) * T + t) * C + 2 * m);
+    if (k == 0 || k == kSH) X.y = 0.f;  // C2R ignores the imaginary parts of DC and Nyquist
+    bufB[k] = X;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < kSH; k += kST) {
+    const float2 xk = bufB[k];
+    const float2 xm = cconj(bufB[kSH - k]);
+    const float2 E = make_float2(0.5f * (xk.x + xm.x), 0.5f * (xk.y + xm.y));
+    const float2 D = csub(xk, xm);
+    const float2 O = cmul(make_float2(0.5f * D.x, 0.5f * D.y), cconj(tb.twN[k]));
+    bufA[k] = make_float2(E.x - O.y, E.y + O.x);
+  }
+  const float2* z = fft2048<true>(bufA, bufB, tb.tw);
+  float2* o = reinterpret_cast<float2*>(fw + ((int64_t)sg * T + t) * kSN);
+  for (int k = threadIdx.x; k < kSH; k += kST) {
+    const float2 v = z[k];
+    o[k] = make_float2(v.x * scale, v.y * scale);
+  }
+}
+
+// overlap-add / sum(w^2) (rectangular window: the covering frame count), center trim, crop to chunk
+__global__ void scn_istft_ola_kernel(const float* __restrict__ fw, int T, int hop, int chunk, float* __restrict__ out) {
+  const int sg = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= chunk) return;
+  const int n = j + kSN / 2;
+  const int t_lo = n - kSN + 1 <= 0 ? 0 : (n - kSN + hop) / hop;
+  const int t_hi = min(n / hop, T - 1);
+  const float* f = fw + (int64_t)sg * T * kSN;
+  float acc = 0.f, env = 0.f;
+  for (int t = t_lo; t <= t_hi; ++t) {
+    acc += f[(int64_t)t * kSN + (n - t * hop)];
+    env += 1.f;
+  }
+  out[(int64_t)sg * chunk + j] = acc / env;
+}
+
+// ---- SD / SU band convolutions (scnet.py:114-148, :171-196) ---------------------------------
+struct BandConv {
+  int in_off, n_in, pad_left, stride, kern, n_out, out_off, dist;
+};
+
+// Y[b][out_off + fo][t][co] = bias + sum_{kk, ci} W[kk][ci][co] X[b][in_off + fo*s + kk - pad][t][ci]
+__global__ void scn_sdconv_kernel(const float* __restrict__ X, int Fin, int T, int Cin, const float* __restrict__ W,
+                                  const float* __restrict__ bias, BandConv bc, float* __restrict__ Y, int Fout,
+                                  int Cout, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int co = (int)(i % Cout);
+  int64_t r = i / Cout;
+  const int t = (int)(r % T);
+  r /= T;
+  const int fo = (int)(r % bc.n_out);
+  const int64_t b = r / bc.n_out;
+  float acc = bias[co];
+  for (int kk = 0; kk < bc.kern; ++kk) {
+    const int fi = fo * bc.stride + kk - bc.pad_left;
+    if (fi < 0 || fi >= bc.n_in) continue;
+    const float* xp = X + ((b * Fin + bc.in_off + fi) * T + t) * Cin;
+    const float* wp = W + (int64_t)kk * Cin * Cout + co;
+    for (int ci = 0; ci < Cin; ++ci) acc = fmaf(wp[(int64_t)ci * Cout], xp[ci], acc);
+  }
+  Y[((b * Fout + bc.out_off + fo) * T + t) * Cout + co] = acc;
+}
+
+// ConvTranspose2d (kern x 1, stride x 1) of the band rows, trimmed: out row fo <- full row fo + dist
+__global__ void scn_convtr_kernel(const float* __restrict__ X, int Fin, int T, int Cin, const float* __restrict__ W,
+                                  const float* __restrict__ bias, BandConv bc, float* __restrict__ Y, int Fout,
+                                  int Cout, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int co = (int)(i % Cout);
+  int64_t r = i / Cout;
+  const int t = (int)(r % T);
+  r /= T;
+  const int fo = (int)(r % bc.n_out);
+  const int64_t b = r / bc.n_out;
+  const int fp = fo + bc.dist;
+  float acc = bias[co];
+  for (int kk = 0; kk < bc.kern; ++kk) {
+    const int d = fp - kk;
+    if (d < 0 || d % bc.stride) continue;
+    const int fi = d / bc.stride;
+    if (fi >= bc.n_in) continue;
+    const float* xp = X + ((b * Fin + bc.in_off + fi) * T + t) * Cin;
+    const float* wp = W + (int64_t)kk * Cin * Cout + co;
+    for (int ci = 0; ci < Cin; ++ci) acc = fmaf(wp[(int64_t)ci * Cout], xp[ci], acc);
+  }
+  Y[((b * Fout + bc.out_off + fo) * T + t) * Cout + co] = acc;
+}
+
+// ---- ConvolutionModule (scnet.py:15-52), one workgroup per (b, f) row of [T][C] --------------
+struct CmArgs {
+  float* X;          // [B][F_all][T][C], rows f_off .. f_off + n_f of each item
+  int F_all, f_off, n_f, T, C, h;
+  const float *g1, *be1;   // GroupNorm(1, C) affine
+  const float* W1;         // [C][3][2h]
+  const float* b1;         // [2h]
+  float* U;                // [B * n_f][T][h]
+  const float *wdw, *bdw;  // [h][3], [h]
+  const float *g2, *be2;   // GroupNorm(1, h) affine
+  const float* W3;         // [h][C]
+  const float* b3;         // [C]
+  int gelu;                // SDblock F.gelu after the module's last layer (:229-234)
+};
+
+__device__ __forceinline__ void block_sum2(double& s, double& ss, double* red) {
+  for (int o = 32; o >= 1; o >>= 1) {
+    s += __shfl_xor(s, o);
+    ss += __shfl_xor(ss, o);
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) {
+    red[2 * w] = s;
+    red[2 * w + 1] = ss;
+  }
+  __syncthreads();
+  s = 0;
+  ss = 0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+    s += red[2 * i];
+    ss += red[2 * i + 1];
+  }
+}
+
+__global__ void __launch_bounds__(kST) scn_cm_in_kernel(CmArgs a) {
+  extern __shared__ __align__(16) float sm[];
+  const int C = a.C, h = a.h, T = a.T;
+  const int TT = 512 / h;
+  float* Ws = sm;                                    // [C][3][2h]
+  float* xs = Ws + 6 * h * C;                        // [TT + 2][C]
+  double* red = reinterpret_cast<double*>(xs + (TT + 2) * C);
+  const int row = blockIdx.x;
+  const int64_t b = row / a.n_f;
+  const int f = a.f_off + row % a.n_f;
+  const float* xr = a.X + ((b * a.F_all + f) * T) * C;
+  double s = 0, ss = 0;
+  for (int i = threadIdx.x; i < T * C; i += kST) {
+    const double v = xr[i];
+    s += v;
+    ss += v * v;
+  }
+  block_sum2(s, ss, red);
+  const double n = (double)T * C;
+  const double mu = s / n;
+  const double var = fmax(ss / n - mu * mu, 0.0);
+  const float mean = (float)mu, rstd = (float)(1.0 / sqrt(var + 1e-5));
+  for (int i = threadIdx.x; i < 6 * h * C; i += kST) Ws[i] = a.W1[i];
+  float* U = a.U + (int64_t)row * T * h;
+  for (int t0 = 0; t0 < T; t0 += TT) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < (TT + 2) * C; i += kST) {
+      const int tl = i / C, c = i - tl * C;
+      const int t = t0 - 1 + tl;
+      xs[i] = (t >= 0 && t < T) ? (xr[(int64_t)t * C + c] - mean) * rstd * a.g1[c] + a.be1[c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int q = threadIdx.x + r * kST;
+      const int j = q % h, tl = q / h;
+      const int t = t0 + tl;
+      if (t >= T) continue;
+      float ga = a.b1[j], gg = a.b1[j + h];
+#pragma unroll
+      for (int dt = 0; dt < 3; ++dt) {
+        const float* xrow = xs + (tl + dt) * C;
+        const float* w = Ws + dt * 2 * h + j;
+        for (int c = 0; c < C; ++c) {
+          const float xv = xrow[c];
+          ga = fmaf(w[c * 6 * h], xv, ga);
+          gg = fmaf(w[c * 6 * h + h], xv, gg);
+        }
+      }
+      U[(int64_t)t * h + j] = ga * sigm(gg);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kST) scn_cm_out_kernel(CmArgs a) {
+  extern __shared__ __align__(16) float sm[];
+  const int C = a.C, h = a.h, T = a.T;
+  float* Us = sm;              // [T][h]
+  float* Vs = Us + T * h;      // [T][h]
+  float* W3s = Vs + T * h;     // [h][C]
+  double* red = reinterpret_cast<double*>(W3s + h * C + ((h * C) & 1));
+  const int row = blockIdx.x;
+  const int64_t b = row / a.n_f;
+  const int f = a.f_off + row % a.n_f;
+  float* xr = a.X + ((b * a.F_all + f) * T) * C;
+  const float* U = a.U + (int64_t)row * T * h;
+  for (int i = threadIdx.x; i < T * h; i += kST) Us[i] = U[i];
+  for (int i = threadIdx.x; i < h * C; i += kST) W3s[i] = a.W3[i];
+  __syncthreads();
+  double s = 0, ss = 0;
+  for (int i = threadIdx.x; i < T * h; i += kST) {
+    const int t = i / h, j = i - t * h;
+    float v = a.bdw[j];
+    if (t > 0) v = fmaf(a.wdw[3 * j], Us[i - h], v);
+    v = fmaf(a.wdw[3 * j + 1], Us[i], v);
+    if (t < T - 1) v = fmaf(a.wdw[3 * j + 2], Us[i + h], v);
+    Vs[i] = v;
+    s += v;
+    ss += (double)v * v;
+  }
+  block_sum2(s, ss, red);
+  const double n = (double)T * h;
+  const double mu = s / n;
+  const double var = fmax(ss / n - mu * mu, 0.0);
+  const float mean = (float)mu, rstd = (float)(1.0 / sqrt(var + 1e-5));
+  for (int i = threadIdx.x; i < T * h; i += kST) {
+    const int j = i % h;
+    const float v = (Vs[i] - mean) * rstd * a.g2[j] + a.be2[j];
+    Vs[i] = v * sigm(v);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < T * C; i += kST) {
+    const int t = i / C, c = i - t * C;
+    float acc = a.b3[c];
+    const float* sv = Vs + t * h;
+    for (int j = 0; j < h; ++j) acc = fmaf(W3s[j * C + c], sv[j], acc);
+    float v = xr[i] + acc;
+    if (a.gelu) v = gelu_erf(v);
+    xr[i] = v;
+  }
+}
+
+__global__ void scn_gelu_rows_kernel(float* X, int F_all, int f_off, int n_f, int64_t row_elems, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int64_t row = i / row_elems, e = i - row * row_elems;
+  const int64_t b = row / n_f;
+  const int64_t f = f_off + row % n_f;
+  float* p = X + (b * F_all + f) * row_elems + e;
+  *p = gelu_erf(*p);
+}
+
+// ---- 3x3 convolution over (F, T), padding 1 (globalconv :215, FusionLayer :76) --------------
+struct C3Args {
+  const float* A;      // [B][F][T][Cin]
+  const float* S;      // nullable, added to A on load (FusionLayer x += skip)
+  int F, T, Cin;
+  const float* W;      // [9][Cin][ncols]
+  const float* bias;   // [ncols]
+  int ncols;
+  float* out;          // [B][F][T][c_store]
+  int c_store;
+  int glu;             // packed columns (a_2q, a_2q+1, g_2q, g_2q+1) -> out channels 2q, 2q+1
+};
+constexpr int kC3F = 4, kC3T = 32, kC3N = 64, kC3K = 16, kC3R = kC3T + 4;
+
+__global__ void __launch_bounds__(kST) scn_conv3x3_kernel(C3Args a) {
+  __shared__ __align__(16) float xs[kC3K][kC3F + 2][kC3R];
+  __shared__ __align__(16) float ws[9][kC3K][kC3N];
+  const int F = a.F, T = a.T, Cin = a.Cin;
+  const int ntt = (T + kC3T - 1) / kC3T;
+  const int t0 = (blockIdx.x % ntt) * kC3T, f0 = (blockIdx.x / ntt) * kC3F;
+  const int n0 = blockIdx.y * kC3N;
+  const int64_t b = blockIdx.z;
+  const int cg = threadIdx.x & 15, pg = threadIdx.x >> 4;
+  const int fl = pg >> 2, tg = pg & 3;
+  float acc[8][4];
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[p][q] = 0.f;
+  for (int ci0 = 0; ci0 < Cin; ci0 += kC3K) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kC3K * (kC3F + 2) * (kC3T + 2); i += kST) {
+      const int ci = i & (kC3K - 1);
+      const int r = i >> 4;
+      const int tt = r % (kC3T + 2), fr = r / (kC3T + 2);
+      const int f = f0 - 1 + fr, t = t0 - 1 + tt;
+      float v = 0.f;
+      if (f >= 0 && f < F && t >= 0 && t < T) {
+        const int64_t idx = ((b * F + f) * T + t) * Cin + ci0 + ci;
+        v = a.A[idx];
+        if (a.S) v += a.S[idx];
+      }
+      xs[ci][fr][tt] = v;
+    }
+    for (int i = threadIdx.x; i < 9 * kC3K * kC3N; i += kST) {
+      const int col = i & (kC3N - 1);
+      const int r = i >> 6;
+      const int ci = r & (kC3K - 1), tap = r >> 4;
+      ws[tap][ci][col] = (n0 + col < a.ncols) ? a.W[((int64_t)tap * Cin + ci0 + ci) * a.ncols + n0 + col] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int ci = 0; ci < kC3K; ++ci) {
+#pragma unroll
+      for (int df = 0; df < 3; ++df) {
+        const float* xr = &xs[ci][fl + df][8 * tg];
+        float xv[10];
+        const float4 x0 = *reinterpret_cast<const float4*>(xr);
+        const float4 x1 = *reinterpret_cast<const float4*>(xr + 4);
+        const float2 x2 = *reinterpret_cast<const float2*>(xr + 8);
+        xv[0] = x0.x; xv[1] = x0.y; xv[2] = x0.z; xv[3] = x0.w;
+        xv[4] = x1.x; xv[5] = x1.y; xv[6] = x1.z; xv[7] = x1.w;
+        xv[8] = x2.x; xv[9] = x2.y;
+#pragma unroll
+        for (int dt = 0; dt < 3; ++dt) {
+          const float4 w = *reinterpret_cast<const float4*>(&ws[df * 3 + dt][ci][4 * cg]);
+#pragma unroll
+          for (int p = 0; p < 8; ++p) {
+            const float xv_ = xv[p + dt];
+            acc[p][0] = fmaf(xv_, w.x, acc[p][0]);
+            acc[p][1] = fmaf(xv_, w.y, acc[p][1]);
+            acc[p][2] = fmaf(xv_, w.z, acc[p][2]);
+            acc[p][3] = fmaf(xv_, w.w, acc[p][3]);
+          }
+        }
+      }
+    }
+  }
+  const int f = f0 + fl;
+  if (f >= F) return;
+  const int col = n0 + 4 * cg;
+  if (col >= a.ncols) return;
+  float bv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bv[q] = col + q < a.ncols ? a.bias[col + q] : 0.f;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int t = t0 + 8 * tg + p;
+    if (t >= T) break;
+    float* o = a.out + ((b * F + f) * T + t) * a.c_store;
+    const float v0 = acc[p][0] + bv[0], v1 = acc[p][1] + bv[1], v2 = acc[p][2] + bv[2], v3 = acc[p][3] + bv[3];
+    if (a.glu) {
+      *reinterpret_cast<float2*>(o + col / 2) = make_float2(v0 * sigm(v2), v1 * sigm(v3));
+    } else {
+      o[col] = v0;
+      if (col + 1 < a.ncols) o[col + 1] = v1;
+      if (col + 2 < a.ncols) o[col + 2] = v2;
+      if (col + 3 < a.ncols) o[col + 3] = v3;
+    }
+  }
+}
+
+// ---- DualPathRNN GroupNorm(1, d) over (C, F, T) per item (separation.py:66, :77) -------------
+__global__ void scn_gn_stats_kernel(const float* __restrict__ X, int64_t n_item, double* __restrict__ stats) {
+  __shared__ double red[2 * (kST / 64)];
+  const int64_t b = blockIdx.y;
+  const float* x = X + b * n_item;
+  double s = 0, ss = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kST + threadIdx.x; i < n_item; i += (int64_t)gridDim.x * kST) {
+    const double v = x[i];
+    s += v;
+    ss += v * v;
+  }
+  block_sum2(s, ss, red);
+  if (threadIdx.x == 0) {
+    atomicAdd(&stats[2 * b], s);
+    atomicAdd(&stats[2 * b + 1], ss);
+  }
+}
+
+__global__ void scn_gn_apply_kernel(const float* __restrict__ X, int64_t n_item, int C, const double* __restrict__ stats,
+                                    const float* __restrict__ g, const float* __restrict__ be, float* __restrict__ Y,
+                                    int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int64_t b = i / n_item;
+  const int c = (int)(i % C);
+  const double mu = stats[2 * b] / (double)n_item;
+  const double var = fmax(stats[2 * b + 1] / (double)n_item - mu * mu, 0.0);
+  const float mean = (float)mu, rstd = (float)(1.0 / sqrt(var + 1e-5));
+  Y[i] = (X[i] - mean) * rstd * g[c] + be[c];
+}
+
+// ---- bi-LSTM recurrence (torch.nn.LSTM, batch_first, gate order i, f, g, o) -----------------
+// token row of (sequence s, position p) = (s / sdiv) * smul_a + (s % sdiv) * smul_b + p * pstride
+struct LstmArgs {
+  const float* G;     // [rows][g_ld]: x W_ih^T + b_ih + b_hh, direction d at column d * 4H
+  int64_t g_ld;
+  float* HO;          // [rows][ho_ld]: h, direction d at column d * H
+  int64_t ho_ld;
+  const float* Wt;    // [2][H][4H]  (W_hh transposed, k-major)
+  int H, L, n_seq, sdiv;
+  int64_t smul_a, smul_b, pstride;
+};
+
+template <int ST>
+__global__ void __launch_bounds__(kST) scn_lstm_kernel(LstmArgs a) {
+  extern __shared__ __align__(16) float hs[];  // [2][S][H]
+  const int H = a.H, H4 = 4 * H;
+  const int ngrp = kST / H;
+  const int S = ST * ngrp;
+  const int j = threadIdx.x % H, sg = threadIdx.x / H;
+  const int dir = blockIdx.y;
+  const int seq0 = blockIdx.x * S + sg * ST;
+  int64_t rowbase[ST];
+  bool ok[ST];
+  float c[ST];
+#pragma unroll
+  for (int u = 0; u < ST; ++u) {
+    const int s = seq0 + u;
+    ok[u] = s < a.n_seq;
+    rowbase[u] = ok[u] ? (int64_t)(s / a.sdiv) * a.smul_a + (int64_t)(s % a.sdiv) * a.smul_b : 0;
+    c[u] = 0.f;
+    hs[(sg * ST + u) * H + j] = 0.f;
+  }
+  const float* W = a.Wt + (int64_t)dir * H * H4 + j;
+  __syncthreads();
+  for (int step = 0; step < a.L; ++step) {
+    const int pos = dir ? a.L - 1 - step : step;
+    const float* hc = hs + (step & 1) * S * H + sg * ST * H;
+    float* hn = hs + ((step + 1) & 1) * S * H + sg * ST * H;
+    float acc[ST][4];
+#pragma unroll
+    for (int u = 0; u < ST; ++u) {
+      if (ok[u]) {
+        const float* gp = a.G + (rowbase[u] + (int64_t)pos * a.pstride) * a.g_ld + dir * H4 + j;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[u][g] = gp[g * H];
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[u][g] = 0.f;
+      }
+    }
+#pragma unroll 4
+    for (int k = 0; k < H; ++k) {
+      const float* wk = W + (int64_t)k * H4;
+      const float w0 = wk[0], w1 = wk[H], w2 = wk[2 * H], w3 = wk[3 * H];
+#pragma unroll
+      for (int u = 0; u < ST; ++u) {
+        const float hv = hc[u * H + k];
+        acc[u][0] = fmaf(w0, hv, acc[u][0]);
+        acc[u][1] = fmaf(w1, hv, acc[u][1]);
+        acc[u][2] = fmaf(w2, hv, acc[u][2]);
+        acc[u][3] = fmaf(w3, hv, acc[u][3]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < ST; ++u) {
+      const float ig = sigm(acc[u][0]), fg = sigm(acc[u][1]), gg = tanhf(acc[u][2]), og = sigm(acc[u][3]);
+      c[u] = fg * c[u] + ig * gg;
+      const float hv = og * tanhf(c[u]);
+      hn[u * H + j] = hv;
+      if (ok[u]) a.HO[(rowbase[u] + (int64_t)pos * a.pstride) * a.ho_ld + dir * H + j] = hv;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- FeatureConversion (separation.py:20-34): DFTs over T, norm = "ortho" -------------------
+// rfft: X [R][T][C] -> Y [R][K][2C] (real | imag), K = T/2 + 1.  tw[m] = (cos, sin)(2 pi m / T).
+__global__ void __launch_bounds__(kST) scn_rfft_kernel(const float* __restrict__ X, int T, int C,
+                                                       const float2* __restrict__ tw, float scale,
+                                                       float* __restrict__ Y) {
+  __shared__ __align__(16) float xs[32][64];
+  __shared__ float2 tws[1024];
+  const int K = T / 2 + 1;
+  const int64_t r = blockIdx.z;
+  const int k0 = blockIdx.x * 32, c0 = blockIdx.y * 64;
+  const int kq = threadIdx.x >> 5, cq = threadIdx.x & 31;
+  for (int i = threadIdx.x; i < T; i += kST) tws[i] = tw[i];
+  float are[4][2], aim[4][2];
+  int idx[4], stp[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    stp[i] = (k0 + kq + 8 * i) % T;
+    idx[i] = 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) are[i][e] = aim[i][e] = 0.f;
+  }
+  const float* xr = X + r * T * C;
+  for (int t0 = 0; t0 < T; t0 += 32) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 32 * 64; i += kST) {
+      const int tt = i >> 6, cc = i & 63;
+      const int t = t0 + tt, c = c0 + cc;
+      xs[tt][cc] = (t < T && c < C) ? xr[(int64_t)t * C + c] : 0.f;
+    }
+    __syncthreads();
+    const int nt = min(32, T - t0);
+    for (int tt = 0; tt < nt; ++tt) {
+      const float2 xv = *reinterpret_cast<const float2*>(&xs[tt][2 * cq]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float2 w = tws[idx[i]];
+        are[i][0] = fmaf(w.x, xv.x, are[i][0]);
+        are[i][1] = fmaf(w.x, xv.y, are[i][1]);
+        aim[i][0] = fmaf(-w.y, xv.x, aim[i][0]);
+        aim[i][1] = fmaf(-w.y, xv.y, aim[i][1]);
+        idx[i] += stp[i];
+        if (idx[i] >= T) idx[i] -= T;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + kq + 8 * i;
+    if (k >= K) continue;
+    float* yr = Y + (r * K + k) * 2 * C;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int c = c0 + 2 * cq + e;
+      if (c >= C) continue;
+      yr[c] = are[i][e] * scale;
+      yr[C + c] = aim[i][e] * scale;
+    }
+  }
+}
+
+// irfft: Y [R][K][2C] -> X [R][T][C], T = 2 (K - 1); imaginary parts of DC / Nyquist ignored.
+__global__ void __launch_bounds__(kST) scn_irfft_kernel(const float* __restrict__ Y, int K, int C,
+                                                        const float2* __restrict__ tw, float scale,
+                                                        float* __restrict__ X) {
+  __shared__ __align__(16) float ys[32][2][64];
+  __shared__ float2 tws[1024];
+  const int T = 2 * (K - 1);
+  const int64_t r = blockIdx.z;
+  const int t0 = blockIdx.x * 32, c0 = blockIdx.y * 64;
+  const int tq = threadIdx.x >> 5, cq = threadIdx.x & 31;
+  for (int i = threadIdx.x; i < T; i += kST) tws[i] = tw[i];
+  float acc[4][2];
+  int idx[4], stp[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    stp[i] = (t0 + tq + 8 * i) % T;
+    idx[i] = 0;
+    acc[i][0] = acc[i][1] = 0.f;
+  }
+  const float* yr = Y + r * K * 2 * C;
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 32 * 64; i += kST) {
+      const int kk = i >> 6, cc = i & 63;
+      const int k = k0 + kk, c = c0 + cc;
+      float re = 0.f, im = 0.f;
+      if (k < K && c < C) {
+        const bool edge = k == 0 || k == K - 1;
+        re = yr[(int64_t)k * 2 * C + c] * (edge ? 1.f : 2.f);
+        im = edge ? 0.f : 2.f * yr[(int64_t)k * 2 * C + C + c];
+      }
+      ys[kk][0][cc] = re;
+      ys[kk][1][cc] = im;
+    }
+    __syncthreads();
+    const int nk = min(32, K - k0);
+    for (int kk = 0; kk < nk; ++kk) {
+      const float2 re = *reinterpret_cast<const float2*>(&ys[kk][0][2 * cq]);
+      const float2 im = *reinterpret_cast<const float2*>(&ys[kk][1][2 * cq]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float2 w = tws[idx[i]];
+        acc[i][0] = fmaf(w.x, re.x, fmaf(-w.y, im.x, acc[i][0]));
+        acc[i][1] = fmaf(w.x, re.y, fmaf(-w.y, im.y, acc[i][1]));
+        idx[i] += stp[i];
+        if (idx[i] >= T) idx[i] -= T;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = t0 + tq + 8 * i;
+    if (t >= T) continue;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int c = c0 + 2 * cq + e;
+      if (c < C) X[(r * T + t) * C + c] = acc[i][e] * scale;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+struct Param {
+  std::string name;
+  std::vector<int64_t> shape;
+  int64_t numel = 0;
+  std::vector<float> host;
+  bool set = false;
+};
+
+struct CmLayer {  // float offsets into the packed fp32 blob
+  int64_t g1, be1, w1, b1, wdw, bdw, g2, be2, w3, b3;
+};
+
+struct Level {
+  int Fin, Fout, Cin, Cout, h, Cdec;  // Cdec: SU output channels
+  BandConv sd[3], su[3];
+  int64_t sd_w[3], sd_b[3], gc_w, gc_b, fu_w, fu_b, su_w[3], su_b[3];
+  std::vector<CmLayer> cm[3];
+};
+
+struct DpLayer {
+  int d, H;
+  Gemm ih[2], lin[2];
+  int64_t whh[2], gn_g[2], gn_b[2];
+};
+
+}  // namespace
+}  // namespace sesa
+
+struct sesa_scnet {
+  sesa_scnet_config cfg;
+  std::vector<int> dims;
+  int nl = 0, F0 = 0, T = 0, K = 0, Lpad = 0, padding = 0, nsig = 0;
+  std::vector<sesa::Level> lv;
+  std::vector<sesa::DpLayer> dp;
+  std::vector<sesa::Param> params;
+  std::map<std::string, int> by_name;
+  float* d_f32 = nullptr;     // packed fp32 weights (convs, norms, W_hh^T)
+  uint16_t* d_w = nullptr;    // token-GEMM bf16 hi/lo images
+  float* d_bias = nullptr;
+  float2* d_twT = nullptr;    // (cos, sin)(2 pi m / T)
+  bool finalized = false;
+};
+
+namespace sesa {
+namespace {
+
+void add_param(sesa_scnet* m, const std::string& name, std::vector<int64_t> shape) {
+  Param p;
+  p.name = name;
+  p.shape = shape;
+  p.numel = 1;
+  for (auto s : shape) p.numel *= s;
+  m->by_name[name] = (int)m->params.size();
+  m->params.push_back(std::move(p));
+}
+
+const std::vector<float>& P(sesa_scnet* m, const std::string& name) { return m->params[m->by_name.at(name)].host; }
+
+std::string S(int i) { return std::to_string(i); }
+
+// SDlayer split points (scnet.py:117-122): ceil(Fr * SR_low), ceil(Fr * (SR_low + SR_mid)), in double
+void splits(int Fr, const double* sr, int* s) {
+  s[0] = 0;
+  s[1] = (int)std::ceil(Fr * sr[0]);
+  s[2] = (int)std::ceil(Fr * (sr[0] + sr[1]));
+  s[3] = Fr;
+}
+
+struct Plan {
+  size_t spec, skip[4], bufA, bufB, bufN, U, G, HO, stats, frames, total;
+};
+
+size_t al(size_t floats) { return (floats * 4 + 255) / 256 * 256; }
+
+Plan plan(const sesa_scnet* m, int B) {
+  Plan p{};
+  size_t off = 0;
+  const int64_t T = m->T;
+  p.spec = off;
+  off += al((size_t)B * m->F0 * T * m->dims[0]);
+  size_t e = 0, u = 0;
+  for (int i = 0; i < m->nl; ++i) {
+    const Level& L = m->lv[i];
+    p.skip[i] = off;
+    off += al((size_t)B * L.Fout * T * L.Cout);
+    e = std::max(e, (size_t)B * L.Fout * T * L.Cout);
+    e = std::max(e, (size_t)B * L.Fin * T * L.Cdec);
+    u = std::max(u, (size_t)B * L.Fout * T * L.h);
+  }
+  const int Fn = m->lv[m->nl - 1].Fout, d = m->dims[m->nl];
+  e = std::max(e, (size_t)B * Fn * T * d);
+  e = std::max(e, (size_t)B * Fn * m->K * 2 * d);
+  size_t g = 0, ho = 0;
+  for (const DpLayer& L : m->dp) {
+    const size_t rows = (size_t)B * Fn * (L.d == d ? T : m->K);
+    g = std::max(g, rows * 8 * L.H);
+    ho = std::max(ho, rows * 2 * L.H);
+  }
+  p.bufA = off; off += al(e);
+  p.bufB = off; off += al(e);
+  p.bufN = off; off += al(e);
+  p.U = off; off += al(u);
+  p.G = off; off += al(g);
+  p.HO = off; off += al(ho);
+  p.stats = off; off += al((size_t)B * 4);
+  p.frames = off; off += al((size_t)B * m->nsig * T * kSN);
+  p.total = off;
+  return p;
+}
+
+size_t cm_in_lds(int C, int h) { return (size_t)(6 * h * C + (512 / h + 2) * C) * 4 + 16 * 8 + 16; }
+size_t cm_out_lds(int T, int C, int h) { return (size_t)(2 * T * h + h * C + 1) * 4 + 16 * 8 + 16; }
+
+double gemm_flops(const Gemm& gm, int64_t M) {
+  double f = 0;
+  for (auto& g : gm.groups) f += 2.0 * (double)M * g.N * g.K;
+  return f;
+}
+
+}  // namespace
+}  // namespace sesa
+
+using namespace sesa;
+
+extern "C" int sesa_scnet_create(const sesa_scnet_config* cfg, sesa_scnet** out) {
+  clear_error();
+  SESA_REQUIRE(cfg && out && cfg->dims && cfg->n_dims >= 2 && cfg->n_dims <= 5, SESA_ERR_INVALID,
+               "sesa_scnet_create: bad arguments");
+  const sesa_scnet_config& c = *cfg;
+  SESA_REQUIRE(c.n_fft == kSN && c.win_size == kSN, SESA_ERR_INVALID, "scnet: only nfft = win_size = 4096");
+  SESA_REQUIRE(c.hop_size > 0 && c.chunk_size > kSN / 2, SESA_ERR_INVALID, "scnet: bad hop_size / chunk_size");
+  SESA_REQUIRE(c.audio_channels >= 1 && c.audio_channels <= 2 && c.n_sources >= 1, SESA_ERR_INVALID,
+               "scnet: audio_channels 1 or 2, n_sources >= 1");
+  SESA_REQUIRE(c.dims[0] == 2 * c.audio_channels, SESA_ERR_INVALID, "scnet: dims[0] must be 2 * audio_channels");
+  SESA_REQUIRE(c.conv_kernel == 3, SESA_ERR_INVALID, "scnet: conv_kernel 3 only");
+  SESA_REQUIRE(c.num_dplayer >= 0 && c.num_dplayer % 2 == 0 && c.expand >= 1, SESA_ERR_INVALID,
+               "scnet: num_dplayer must be even (rfft/irfft pairs)");
+  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16, SESA_ERR_INVALID, "scnet: precision");
+  sesa_scnet* m = new sesa_scnet();
+  m->cfg = c;
+  m->dims.assign(c.dims, c.dims + c.n_dims);
+  m->cfg.dims = nullptr;
+  m->nl = c.n_dims - 1;
+  auto fail = [&](const char* msg, int v) {
+    delete m;
+    set_error("scnet: %s (%d)", msg, v);
+    return SESA_ERR_INVALID;
+  };
+  const int hop = c.hop_size;
+  int padding = hop - c.chunk_size % hop;
+  if ((c.chunk_size + padding) / hop % 2 == 0) padding += hop;
+  m->padding = padding;
+  m->Lpad = c.chunk_size + padding;
+  m->T = m->Lpad / hop + 1;
+  m->K = m->T / 2 + 1;
+  m->F0 = kSN / 2 + 1;
+  m->nsig = c.n_sources * c.audio_channels;
+  if (m->T % 2) return fail("odd frame count", m->T);
+  if (m->T > 1024) return fail("more than 1024 STFT frames per chunk (DFT twiddle table)", m->T);
+  // levels: SD geometry (scnet.py:114-148) and SU trims (:171-196)
+  int Fr = m->F0;
+  for (int i = 0; i < m->nl; ++i) {
+    Level L{};
+    L.Fin = Fr;
+    L.Cin = m->dims[i];
+    L.Cout = m->dims[i + 1];
+    L.h = (int)(L.Cout / (double)c.compress);
+    L.Cdec = i == 0 ? m->dims[0] * c.n_sources : m->dims[i];
+    int sp[4];
+    splits(Fr, c.band_sr, sp);
+    int fo = 0;
+    for (int b = 0; b < 3; ++b) {
+      BandConv& bc = L.sd[b];
+      bc.in_off = sp[b];
+      bc.n_in = sp[b + 1] - sp[b];
+      bc.stride = c.band_stride[b];
+      bc.kern = c.band_kernel[b];
+      if (bc.n_in <= 0 || bc.stride <= 0 || bc.kern <= 0) return fail("empty band", b);
+      const int tot = bc.stride == 1 ? bc.kern - bc.stride : (bc.stride - bc.n_in % bc.stride) % bc.stride;
+      bc.pad_left = tot / 2;
+      bc.n_out = (bc.n_in + tot - bc.kern) / bc.stride + 1;
+      if (bc.n_out <= 0) return fail("band shorter than its kernel", b);
+      bc.out_off = fo;
+      fo += bc.n_out;
+      BandConv& su = L.su[b];
+      su.in_off = bc.out_off;
+      su.n_in = bc.n_out;
+      su.stride = bc.stride;
+      su.kern = bc.kern;
+      const int full = (bc.n_out - 1) * bc.stride + bc.kern;
+      if (full < bc.n_in) return fail("transposed band conv shorter than the band", b);
+      su.dist = (full - bc.n_in) / 2;
+      su.n_out = bc.n_in;
+      su.out_off = bc.in_off;
+    }
+    L.Fout = fo;
+    if (L.h < 1 || (512 % L.h) != 0 || L.h > 64) return fail("ConvolutionModule hidden size must divide 512 and be <= 64", L.h);
+    if (L.Cout % 16 || L.Cout % 2) return fail("dims must be multiples of 16", L.Cout);
+    if (cm_in_lds(L.Cout, L.h) > 160 * 1024 || cm_out_lds(m->T, L.Cout, L.h) > 160 * 1024)
+      return fail("ConvolutionModule row does not fit in LDS", L.Cout);
+    m->lv.push_back(L);
+    Fr = fo;
+  }
+  const int dlast = m->dims[m->nl];
+  for (int i = 0; i < c.num_dplayer; ++i) {
+    DpLayer L{};
+    L.d = dlast * (i % 2 ? 2 : 1);
+    L.H = L.d * c.expand;
+    if (L.H != 32 && L.H != 64 && L.H != 128 && L.H != 256) return fail("LSTM hidden size must be 32/64/128/256", L.H);
+    m->dp.push_back(L);
+  }
+  // parameter registry, reference state_dict order (scnet.py:280-323)
+  for (int i = 0; i < m->nl; ++i) {
+    const Level& L = m->lv[i];
+    const std::string p = "encoder." + S(i);
+    for (int b = 0; b < 3; ++b) {
+      add_param(m, p + ".SDlayer.convs." + S(b) + ".weight", {L.Cout, L.Cin, c.band_kernel[b], 1});
+      add_param(m, p + ".SDlayer.convs." + S(b) + ".bias", {L.Cout});
+    }
+    for (int b = 0; b < 3; ++b)
+      for (int l = 0; l < std::abs(c.conv_depths[b]); ++l) {
+        const std::string q = p + ".conv_modules." + S(b) + ".layers." + S(l);
+        add_param(m, q + ".0.weight", {L.Cout});
+        add_param(m, q + ".0.bias", {L.Cout});
+        add_param(m, q + ".1.weight", {2 * L.h, L.Cout, 3});
+        add_param(m, q + ".1.bias", {2 * L.h});
+        add_param(m, q + ".3.weight", {L.h, 1, 3});
+        add_param(m, q + ".3.bias", {L.h});
+        add_param(m, q + ".4.weight", {L.h});
+        add_param(m, q + ".4.bias", {L.h});
+        add_param(m, q + ".6.weight", {L.Cout, L.h, 1});
+        add_param(m, q + ".6.bias", {L.Cout});
+      }
+    add_param(m, p + ".globalconv.weight", {L.Cout, L.Cout, 3, 3});
+    add_param(m, p + ".globalconv.bias", {L.Cout});
+  }
+  for (int j = 0; j < m->nl; ++j) {
+    const Level& L = m->lv[m->nl - 1 - j];
+    const std::string p = "decoder." + S(j);
+    add_param(m, p + ".0.conv.weight", {2 * L.Cout, 2 * L.Cout, 3, 3});
+    add_param(m, p + ".0.conv.bias", {2 * L.Cout});
+    for (int b = 0; b < 3; ++b) {
+      add_param(m, p + ".1.convtrs." + S(b) + ".weight", {L.Cout, L.Cdec, c.band_kernel[b], 1});
+      add_param(m, p + ".1.convtrs." + S(b) + ".bias", {L.Cdec});
+    }
+  }
+  for (int i = 0; i < c.num_dplayer; ++i) {
+    const DpLayer& L = m->dp[i];
+    const std::string p = "separation_net.dp_modules." + S(i);
+    for (int l = 0; l < 2; ++l)
+      for (const char* sfx : {"", "_reverse"}) {
+        const std::string q = p + ".lstm_layers." + S(l);
+        add_param(m, q + ".weight_ih_l0" + sfx, {4 * L.H, L.d});
+        add_param(m, q + ".weight_hh_l0" + sfx, {4 * L.H, L.H});
+        add_param(m, q + ".bias_ih_l0" + sfx, {4 * L.H});
+        add_param(m, q + ".bias_hh_l0" + sfx, {4 * L.H});
+      }
+    for (int l = 0; l < 2; ++l) {
+      add_param(m, p + ".linear_layers." + S(l) + ".weight", {L.d, 2 * L.H});
+      add_param(m, p + ".linear_layers." + S(l) + ".bias", {L.d});
+    }
+    for (int l = 0; l < 2; ++l) {
+      add_param(m, p + ".norm_layers." + S(l) + ".weight", {L.d});
+      add_param(m, p + ".norm_layers." + S(l) + ".bias", {L.d});
+    }
+  }
+  *out = m;
+  return SESA_OK;
+}
+
+extern "C" int sesa_scnet_num_params(const sesa_scnet* m) { return m ? (int)m->params.size() : 0; }
+
+extern "C" int sesa_scnet_param_info(const sesa_scnet* m, int i, const char** name, int64_t* numel) {
+  clear_error();
+  SESA_REQUIRE(m && i >= 0 && i < (int)m->params.size(), SESA_ERR_INVALID, "scnet param_info: index out of range");
+  if (name) *name = m->params[i].name.c_str();
+  if (numel) *numel = m->params[i].numel;
+  return SESA_OK;
+}
+
+extern "C" int sesa_scnet_set_param(sesa_scnet* m, const char* name, const float* host, int64_t numel) {
+  clear_error();
+  SESA_REQUIRE(m && name && host, SESA_ERR_INVALID, "scnet set_param: null argument");
+  auto it = m->by_name.find(name);
+  SESA_REQUIRE(it != m->by_name.end(), SESA_ERR_INVALID, "scnet set_param: unknown parameter '%s'", name);
+  Param& p = m->params[it->second];
+  SESA_REQUIRE(p.numel == numel, SESA_ERR_INVALID, "scnet set_param: '%s' expects %lld elements, got %lld", name,
+               (long long)p.numel, (long long)numel);
+  p.host.assign(host, host + numel);
+  p.set = true;
+  m->finalized = false;
+  return SESA_OK;
+}
+
+extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
+  clear_error();
+  SESA_REQUIRE(m, SESA_ERR_INVALID, "scnet finalize: null model");
+  for (auto& p : m->params)
+    SESA_REQUIRE(p.set, SESA_ERR_STATE, "scnet finalize: parameter '%s' was never set", p.name.c_str());
+  const sesa_scnet_config& c = m->cfg;
+  std::vector<float> f32;
+  auto put = [&](const std::vector<float>& v) {
+    const int64_t o = (int64_t)f32.size();
+    f32.insert(f32.end(), v.begin(), v.end());
+    while (f32.size() % 4) f32.push_back(0.f);
+    return o;
+  };
+  auto putp = [&](const std::string& n) { return put(P(m, n)); };
+  for (int i = 0; i < m->nl; ++i) {
+    Level& L = m->lv[i];
+    const std::string p = "encoder." + S(i);
+    for (int b = 0; b < 3; ++b) {  // [Cout][Cin][k][1] -> [k][Cin][Cout]
+      const auto& W = P(m, p + ".SDlayer.convs." + S(b) + ".weight");
+      const int k = L.sd[b].kern;
+      std::vector<float> w((size_t)k * L.Cin * L.Cout);
+      for (int co = 0; co < L.Cout; ++co)
+        for (int ci = 0; ci < L.Cin; ++ci)
+          for (int kk = 0; kk < k; ++kk) w[((size_t)kk * L.Cin + ci) * L.Cout + co] = W[((size_t)co * L.Cin + ci) * k + kk];
+      L.sd_w[b] = put(w);
+      L.sd_b[b] = putp(p + ".SDlayer.convs." + S(b) + ".bias");
+      L.cm[b].clear();
+      for (int l = 0; l < std::abs(c.conv_depths[b]); ++l) {
+        const std::string q = p + ".conv_modules." + S(b) + ".layers." + S(l);
+        CmLayer cl{};
+        const int C = L.Cout, h = L.h;
+        cl.g1 = putp(q + ".0.weight");
+        cl.be1 = putp(q + ".0.bias");
+        const auto& W1 = P(m, q + ".1.weight");  // [2h][C][3] -> [C][3][2h]
+        std::vector<float> w1((size_t)6 * h * C);
+        for (int o = 0; o < 2 * h; ++o)
+          for (int ci = 0; ci < C; ++ci)
+            for (int kk = 0; kk < 3; ++kk) w1[((size_t)ci * 3 + kk) * 2 * h + o] = W1[((size_t)o * C + ci) * 3 + kk];
+        cl.w1 = put(w1);
+        cl.b1 = putp(q + ".1.bias");
+        cl.wdw = putp(q + ".3.weight");
+        cl.bdw = putp(q + ".3.bias");
+        cl.g2 = putp(q + ".4.weight");
+        cl.be2 = putp(q + ".4.bias");
+        const auto& W3 = P(m, q + ".6.weight");  // [C][h][1] -> [h][C]
+        std::vector<float> w3((size_t)h * C);
+        for (int co = 0; co < C; ++co)
+          for (int j = 0; j < h; ++j) w3[(size_t)j * C + co] = W3[(size_t)co * h + j];
+        cl.w3 = put(w3);
+        cl.b3 = putp(q + ".6.bias");
+        L.cm[b].push_back(cl);
+      }
+    }
+    {  // globalconv [Cout][Cout][3][3] -> [9][Cin][Cout]
+      const auto& W = P(m, p + ".globalconv.weight");
+      const int C = L.Cout;
+      std::vector<float> w((size_t)9 * C * C);
+      for (int co = 0; co < C; ++co)
+        for (int ci = 0; ci < C; ++ci)
+          for (int tap = 0; tap < 9; ++tap) w[((size_t)tap * C + ci) * C + co] = W[((size_t)co * C + ci) * 9 + tap];
+      L.gc_w = put(w);
+      L.gc_b = putp(p + ".globalconv.bias");
+    }
+    const std::string dpfx = "decoder." + S(m->nl - 1 - i);
+    {  // FusionLayer: repeat(1, 2) folded (W[:, ci] + W[:, ci + C]); GLU column interleave
+      const auto& W = P(m, dpfx + ".0.conv.weight");
+      const auto& Bv = P(m, dpfx + ".0.conv.bias");
+      const int C = L.Cout, C2 = 2 * C;
+      std::vector<float> w((size_t)9 * C * C2), bias(C2);
+      auto src_col = [C](int col) { const int q = col >> 2, r = col & 3; return (r < 2 ? 0 : C) + 2 * q + (r & 1); };
+      for (int col = 0; col < C2; ++col) {
+        const int co = src_col(col);
+        bias[col] = Bv[co];
+        for (int ci = 0; ci < C; ++ci)
+          for (int tap = 0; tap < 9; ++tap)
+            w[((size_t)tap * C + ci) * C2 + col] =
+                W[((size_t)co * C2 + ci) * 9 + tap] + W[((size_t)co * C2 + ci + C) * 9 + tap];
+      }
+      L.fu_w = put(w);
+      L.fu_b = put(bias);
+    }
+    for (int b = 0; b < 3; ++b) {  // ConvTranspose2d [Cin][Cout][k][1] -> [k][Cin][Cout]
+      const auto& W = P(m, dpfx + ".1.convtrs." + S(b) + ".weight");
+      const int k = L.su[b].kern, Ci = L.Cout, Co = L.Cdec;
+      std::vector<float> w((size_t)k * Ci * Co);
+      for (int ci = 0; ci < Ci; ++ci)
+        for (int co = 0; co < Co; ++co)
+          for (int kk = 0; kk < k; ++kk) w[((size_t)kk * Ci + ci) * Co + co] = W[((size_t)ci * Co + co) * k + kk];
+      L.su_w[b] = put(w);
+      L.su_b[b] = putp(dpfx + ".1.convtrs." + S(b) + ".bias");
+    }
+  }
+  std::vector<uint16_t> blob;
+  std::vector<float> bias;
+  for (int i = 0; i < (int)m->dp.size(); ++i) {
+    DpLayer& L = m->dp[i];
+    const std::string p = "separation_net.dp_modules." + S(i);
+    const int H = L.H, d = L.d;
+    for (int l = 0; l < 2; ++l) {
+      const std::string q = p + ".lstm_layers." + S(l);
+      const auto& Wf = P(m, q + ".weight_ih_l0");
+      const auto& Wr = P(m, q + ".weight_ih_l0_reverse");
+      const auto& bif = P(m, q + ".bias_ih_l0");
+      const auto& bhf = P(m, q + ".bias_hh_l0");
+      const auto& bir = P(m, q + ".bias_ih_l0_reverse");
+      const auto& bhr = P(m, q + ".bias_hh_l0_reverse");
+      TokGroup g = pack_group(
+          8 * H, d,
+          [&](int n, int k) { return n < 4 * H ? Wf[(int64_t)n * d + k] : Wr[(int64_t)(n - 4 * H) * d + k]; }, true,
+          [&](int n) { return n < 4 * H ? bif[n] + bhf[n] : bir[n - 4 * H] + bhr[n - 4 * H]; }, blob, bias);
+      g.x_off = g.o_off = 0;
+      L.ih[l].groups = {g};
+      const auto& Wl = P(m, p + ".linear_layers." + S(l) + ".weight");
+      const auto& bl = P(m, p + ".linear_layers." + S(l) + ".bias");
+      g = pack_group(d, 2 * H, [&](int n, int k) { return Wl[(int64_t)n * 2 * H + k]; }, true,
+                     [&](int n) { return bl[n]; }, blob, bias);
+      g.x_off = g.o_off = 0;
+      L.lin[l].groups = {g};
+      std::vector<float> wt((size_t)2 * H * 4 * H);  // W_hh [4H][H] -> [dir][k][4H]
+      for (int dir = 0; dir < 2; ++dir) {
+        const auto& Wh = P(m, q + (dir ? ".weight_hh_l0_reverse" : ".weight_hh_l0"));
+        for (int n = 0; n < 4 * H; ++n)
+          for (int k = 0; k < H; ++k) wt[((size_t)dir * H + k) * 4 * H + n] = Wh[(size_t)n * H + k];
+      }
+      L.whh[l] = put(wt);
+      L.gn_g[l] = putp(p + ".norm_layers." + S(l) + ".weight");
+      L.gn_b[l] = putp(p + ".norm_layers." + S(l) + ".bias");
+    }
+  }
+  std::vector<float2> twT(m->T);
+  for (int i = 0; i < m->T; ++i) {
+    const double ang = 2.0 * M_PI * i / m->T;
+    twT[i] = make_float2((float)cos(ang), (float)sin(ang));
+  }
+  for (void* p : {(void*)m->d_f32, (void*)m->d_w, (void*)m->d_bias, (void*)m->d_twT})
+    if (p) (void)hipFree(p);
+  m->d_f32 = nullptr;
+  m->d_w = nullptr;
+  m->d_bias = nullptr;
+  m->d_twT = nullptr;
+  SESA_REQUIRE(hipMalloc(&m->d_f32, std::max<size_t>(f32.size(), 1) * 4) == hipSuccess, SESA_ERR_NOMEM,
+               "scnet finalize: hipMalloc weights");
+  SESA_REQUIRE(hipMalloc(&m->d_w, std::max<size_t>(blob.size(), 1) * 2) == hipSuccess, SESA_ERR_NOMEM,
+               "scnet finalize: hipMalloc gemm weights");
+  SESA_REQUIRE(hipMalloc(&m->d_bias, std::max<size_t>(bias.size(), 1) * 4) == hipSuccess, SESA_ERR_NOMEM,
+               "scnet finalize: hipMalloc bias");
+  SESA_REQUIRE(hipMalloc(&m->d_twT, twT.size() * sizeof(float2)) == hipSuccess, SESA_ERR_NOMEM,
+               "scnet finalize: hipMalloc twiddles");
+  hipStream_t st = as_stream(stream);
+  SESA_CHECK_HIP(hipMemcpyAsync(m->d_f32, f32.data(), f32.size() * 4, hipMemcpyHostToDevice, st));
+  if (!blob.empty()) SESA_CHECK_HIP(hipMemcpyAsync(m->d_w, blob.data(), blob.size() * 2, hipMemcpyHostToDevice, st));
+  if (!bias.empty()) SESA_CHECK_HIP(hipMemcpyAsync(m->d_bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice, st));
+  SESA_CHECK_HIP(hipMemcpyAsync(m->d_twT, twT.data(), twT.size() * sizeof(float2), hipMemcpyHostToDevice, st));
+  SESA_CHECK_HIP(hipStreamSynchronize(st));
+  for (auto& L : m->dp)
+    for (int l = 0; l < 2; ++l) {
+      int rc = upload_groups(L.ih[l]);
+      if (!rc) rc = upload_groups(L.lin[l]);
+      if (rc) return rc;
+    }
+  SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_in_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+  SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_out_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+  m->finalized = true;
+  return SESA_OK;
+}
+
+extern "C" size_t sesa_scnet_workspace_size(const sesa_scnet* m, int batch) {
+  if (!m || batch <= 0) return 0;
+  return plan(m, batch).total;
+}
+
+extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* out, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  clear_error();
+  SESA_REQUIRE(m && x && out && workspace && B > 0, SESA_ERR_INVALID, "scnet forward: bad arguments");
+  SESA_REQUIRE(m->finalized, SESA_ERR_STATE, "scnet forward: call sesa_scnet_finalize first");
+  const Plan pl = plan(m, B);
+  SESA_REQUIRE(workspace_bytes >= pl.total, SESA_ERR_INVALID, "scnet forward: workspace %zu < required %zu",
+               workspace_bytes, pl.total);
+  const sesa_scnet_config& c = m->cfg;
+  hipStream_t st = as_stream(stream);
+  char* ws = reinterpret_cast<char*>(workspace);
+  auto F32 = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
+  const float* Wb = m->d_f32;
+  const int T = m->T, K = m->K, F0 = m->F0, ach = c.audio_channels;
+  const int x3 = c.precision == SESA_PREC_BF16X3 ? 1 : 0;
+  ScnTables tb;
+  int rc = get_tables(&tb);
+  if (rc) return rc;
+  auto blocks = [](int64_t n) { return dim3((unsigned)((n + kST - 1) / kST)); };
+
+  // 1. STFT (scnet.py:335-348)
+  float* spec = F32(pl.spec);
+  {
+    void* tok = profile_begin(st);
+    hipLaunchKernelGGL(scn_stft_kernel, dim3(T, B * ach), dim3(kST), 0, st, x, ach, c.chunk_size, m->Lpad,
+                       c.hop_size, T, c.normalized ? 1.0f / 64.0f : 1.0f, tb, spec);
+    SESA_CHECK_LAUNCH();
+    profile_end(tok, st, SESA_KCLASS_STFT, 4.0 * B * ach * ((double)c.chunk_size + (double)T * F0 * 2));
+  }
+  float* bufA = F32(pl.bufA);
+  float* bufB = F32(pl.bufB);
+  float* bufN = F32(pl.bufN);
+  float* U = F32(pl.U);
+  // 2. encoder (scnet.py:356-361)
+  const float* cur = spec;
+  for (int i = 0; i < m->nl; ++i) {
+    const Level& L = m->lv[i];
+    float* skip = F32(pl.skip[i]);
+    void* tok = profile_begin(st);
+    double fl = 0;
+    for (int b = 0; b < 3; ++b) {
+      const BandConv& bc = L.sd[b];
+      const int64_t total = (int64_t)B * bc.n_out * T * L.Cout;
+      hipLaunchKernelGGL(scn_sdconv_kernel, blocks(total), dim3(kST), 0, st, cur, L.Fin, T, L.Cin, Wb + L.sd_w[b],
+                         Wb + L.sd_b[b], bc, skip, L.Fout, L.Cout, total);
+      SESA_CHECK_LAUNCH();
+      fl += 2.0 * total * L.Cin * bc.kern;
+    }
+    for (int b = 0; b < 3; ++b) {
+      const BandConv& bc = L.sd[b];
+      const int rows = B * bc.n_out;
+      if (L.cm[b].empty()) {
+        const int64_t total = (int64_t)rows * T * L.Cout;
+        hipLaunchKernelGGL(scn_gelu_rows_kernel, blocks(total), dim3(kST), 0, st, skip, L.Fout, bc.out_off, bc.n_out,
+                           (int64_t)T * L.Cout, total);
+        SESA_CHECK_LAUNCH();
+      }
+      for (size_t l = 0; l < L.cm[b].size(); ++l) {
+        const CmLayer& cl = L.cm[b][l];
+        CmArgs a{};
+        a.X = skip;
+        a.F_all = L.Fout;
+        a.f_off = bc.out_off;
+        a.n_f = bc.n_out;
+        a.T = T;
+        a.C = L.Cout;
+        a.h = L.h;
+        a.g1 = Wb + cl.g1;
+        a.be1 = Wb + cl.be1;
+        a.W1 = Wb + cl.w1;
+        a.b1 = Wb + cl.b1;
+        a.U = U;
+        a.wdw = Wb + cl.wdw;
+        a.bdw = Wb + cl.bdw;
+        a.g2 = Wb + cl.g2;
+        a.be2 = Wb + cl.be2;
+        a.W3 = Wb + cl.w3;
+        a.b3 = Wb + cl.b3;
+        a.gelu = l + 1 == L.cm[b].size();
+        hipLaunchKernelGGL(scn_cm_in_kernel, dim3(rows), dim3(kST), cm_in_lds(L.Cout, L.h), st, a);
+        SESA_CHECK_LAUNCH();
+        hipLaunchKernelGGL(scn_cm_out_kernel, dim3(rows), dim3(kST), cm_out_lds(T, L.Cout, L.h), st, a);
+        SESA_CHECK_LAUNCH();
+        fl += 2.0 * rows * T * (6.0 * L.h * L.Cout + 3.0 * L.h + (double)L.h * L.Cout);
+      }
+    }
+    {  // globalconv (3x3) -> bufA
+      C3Args a{};
+      a.A = skip;
+      a.F = L.Fout;
+      a.T = T;
+      a.Cin = L.Cout;
+      a.W = Wb + L.gc_w;
+      a.bias = Wb + L.gc_b;
+      a.ncols = L.Cout;
+      a.out = bufA;
+      a.c_store = L.Cout;
+      dim3 grid((unsigned)(((T + kC3T - 1) / kC3T) * ((L.Fout + kC3F - 1) / kC3F)), (unsigned)((L.Cout + kC3N - 1) / kC3N),
+                (unsigned)B);
+      hipLaunchKernelGGL(scn_conv3x3_kernel, grid, dim3(kST), 0, st, a);
+      SESA_CHECK_LAUNCH();
+      fl += 2.0 * B * L.Fout * T * L.Cout * L.Cout * 9;
+    }
+    profile_end(tok, st, SESA_KCLASS_SIMT, fl);
+    cur = bufA;
+  }
+  // 3. separation net (separation.py:107-113): X in bufA, [B][Fn][T][d]
+  const int Fn = m->lv[m->nl - 1].Fout;
+  float* X = bufA;
+  float* Y = bufB;
+  float* G = F32(pl.G);
+  float* HO = F32(pl.HO);
+  double* stats = reinterpret_cast<double*>(ws + pl.stats);
+  for (size_t i = 0; i < m->dp.size(); ++i) {
+    const DpLayer& L = m->dp[i];
+    const int Tc = (i % 2) ? K : T;  // frames (even layers) or rfft bins (odd layers)
+    const int d = L.d, H = L.H;
+    const int64_t rows = (int64_t)B * Fn * Tc;
+    const int64_t n_item = (int64_t)Fn * Tc * d;
+    SESA_REQUIRE(rows < (1ll << 31), SESA_ERR_INVALID, "scnet forward: batch too large");
+    for (int path = 0; path < 2; ++path) {
+      // GroupNorm(1, d) -> bufN
+      void* tok = profile_begin(st);
+      SESA_CHECK_HIP(hipMemsetAsync(stats, 0, (size_t)B * 2 * sizeof(double), st));
+      const unsigned gb = (unsigned)std::min<int64_t>((n_item + kST * 8 - 1) / (kST * 8), 512);
+      hipLaunchKernelGGL(scn_gn_stats_kernel, dim3(gb, B), dim3(kST), 0, st, X, n_item, stats);
+      SESA_CHECK_LAUNCH();
+      hipLaunchKernelGGL(scn_gn_apply_kernel, blocks(B * n_item), dim3(kST), 0, st, X, n_item, d, stats,
+                         Wb + L.gn_g[path], Wb + L.gn_b[path], bufN, (int64_t)B * n_item);
+      SESA_CHECK_LAUNCH();
+      profile_end(tok, st, SESA_KCLASS_ACT, 12.0 * B * n_item);
+      // input projection, both directions: G = XN W_ih^T + (b_ih + b_hh)
+      {
+        TokGemmArgs a{};
+        a.x = bufN;
+        a.x_ld = d;
+        a.out = G;
+        a.o_ld = 8 * H;
+        a.w = m->d_w;
+        a.bias = m->d_bias;
+        a.groups = L.ih[path].d_groups;
+        a.n_groups = 1;
+        a.n_tiles_n = L.ih[path].n_tiles_n;
+        a.M = (int)rows;
+        a.act = TOK_ACT_NONE;
+        void* t0 = profile_begin(st);
+        rc = launch_tok_gemm(a, x3, st);
+        profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(L.ih[path], rows));
+        if (rc) return rc;
+      }
+      // recurrence: path 0 = frequency path, sequences (b, t) over f; path 1 = time path, (b, f) over t
+      {
+        LstmArgs a{};
+        a.G = G;
+        a.g_ld = 8 * H;
+        a.HO = HO;
+        a.ho_ld = 2 * H;
+        a.Wt = Wb + L.whh[path];
+        a.H = H;
+        if (path == 0) {
+          a.L = Fn;
+          a.n_seq = B * Tc;
+          a.sdiv = Tc;
+          a.smul_a = (int64_t)Fn * Tc;
+          a.smul_b = 1;
+          a.pstride = Tc;
+        } else {
+          a.L = Tc;
+          a.n_seq = B * Fn;
+          a.sdiv = Fn;
+          a.smul_a = (int64_t)Fn * Tc;
+          a.smul_b = Tc;
+          a.pstride = 1;
+        }
+        const int ngrp = kST / H;
+        int ST = 8;
+        while (ST > 1 && (int64_t)((a.n_seq + ST * ngrp - 1) / (ST * ngrp)) * 2 < 512) ST >>= 1;
+        const int Sq = ST * ngrp;
+        dim3 grid((unsigned)((a.n_seq + Sq - 1) / Sq), 2);
+        const size_t lds = (size_t)2 * Sq * H * 4;
+        void* t0 = profile_begin(st);
+        switch (ST) {
+          case 8: hipLaunchKernelGGL(scn_lstm_kernel<8>, grid, dim3(kST), lds, st, a); break;
+          case 4: hipLaunchKernelGGL(scn_lstm_kernel<4>, grid, dim3(kST), lds, st, a); break;
+          case 2: hipLaunchKernelGGL(scn_lstm_kernel<2>, grid, dim3(kST), lds, st, a); break;
+          default: hipLaunchKernelGGL(scn_lstm_kernel<1>, grid, dim3(kST), lds, st, a); break;
+        }
+        SESA_CHECK_LAUNCH();
+        profile_end(t0, st, SESA_KCLASS_LSTM, 2.0 * rows * 2 * 4 * H * (double)H);
+      }
+      // Linear(2H -> d) + residual, in place
+      {
+        TokGemmArgs a{};
+        a.x = HO;
+        a.x_ld = 2 * H;
+        a.out = X;
+        a.o_ld = d;
+        a.residual = X;
+        a.w = m->d_w;
+        a.bias = m->d_bias;
+        a.groups = L.lin[path].d_groups;
+        a.n_groups = 1;
+        a.n_tiles_n = L.lin[path].n_tiles_n;
+        a.M = (int)rows;
+        a.act = TOK_ACT_NONE;
+        void* t0 = profile_begin(st);
+        rc = launch_tok_gemm(a, x3, st);
+        profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(L.lin[path], rows));
+        if (rc) return rc;
+      }
+    }
+    // FeatureConversion
+    void* tok = profile_begin(st);
+    const float scale = (float)(1.0 / std::sqrt((double)T));
+    if (i % 2 == 0) {
+      dim3 grid((unsigned)((K + 31) / 32), (unsigned)((d + 63) / 64), (unsigned)(B * Fn));
+      hipLaunchKernelGGL(scn_rfft_kernel, grid, dim3(kST), 0, st, X, T, d, m->d_twT, scale, Y);
+    } else {
+      const int Ch = d / 2;
+      dim3 grid((unsigned)((T + 31) / 32), (unsigned)((Ch + 63) / 64), (unsigned)(B * Fn));
+      hipLaunchKernelGGL(scn_irfft_kernel, grid, dim3(kST), 0, st, X, K, Ch, m->d_twT, scale, Y);
+    }
+    SESA_CHECK_LAUNCH();
+    profile_end(tok, st, SESA_KCLASS_SIMT, 4.0 * B * Fn * (double)K * T * (i % 2 ? d / 2 : d));
+    std::swap(X, Y);
+  }
+  // 4. decoder (scnet.py:363-366): X [B][F_{i+1}][T][C_{i+1}] -> [B][F_i][T][Cdec_i]
+  for (int j = 0; j < m->nl; ++j) {
+    const Level& L = m->lv[m->nl - 1 - j];
+    void* tok = profile_begin(st);
+    C3Args a{};
+    a.A = X;
+    a.S = F32(pl.skip[m->nl - 1 - j]);
+    a.F = L.Fout;
+    a.T = T;
+    a.Cin = L.Cout;
+    a.W = Wb + L.fu_w;
+    a.bias = Wb + L.fu_b;
+    a.ncols = 2 * L.Cout;
+    a.out = Y;
+    a.c_store = L.Cout;
+    a.glu = 1;
+    dim3 grid((unsigned)(((T + kC3T - 1) / kC3T) * ((L.Fout + kC3F - 1) / kC3F)), (unsigned)((2 * L.Cout + kC3N - 1) / kC3N),
+              (unsigned)B);
+    hipLaunchKernelGGL(scn_conv3x3_kernel, grid, dim3(kST), 0, st, a);
+    SESA_CHECK_LAUNCH();
+    double fl = 2.0 * B * L.Fout * T * 2.0 * L.Cout * 2.0 * L.Cout * 9;
+    for (int b = 0; b < 3; ++b) {
+      const BandConv& bc = L.su[b];
+      const int64_t total = (int64_t)B * bc.n_out * T * L.Cdec;
+      hipLaunchKernelGGL(scn_convtr_kernel, blocks(total), dim3(kST), 0, st, Y, L.Fout, T, L.Cout, Wb + L.su_w[b],
+                         Wb + L.su_b[b], bc, X, L.Fin, L.Cdec, total);
+      SESA_CHECK_LAUNCH();
+      fl += 2.0 * total * L.Cout * ((bc.kern + bc.stride - 1) / bc.stride);
+    }
+    profile_end(tok, st, SESA_KCLASS_SIMT, fl);
+  }
+  // 5. iSTFT (scnet.py:367-373)
+  {
+    void* tok = profile_begin(st);
+    float* FR = F32(pl.frames);
+    const float scale = c.normalized ? 2.0f / 64.0f : 2.0f / (float)kSN;
+    hipLaunchKernelGGL(scn_istft_frames_kernel, dim3(T, B * m->nsig), dim3(kST), 0, st, X, m->nsig, T, scale, tb, FR);
+    SESA_CHECK_LAUNCH();
+    hipLaunchKernelGGL(scn_istft_ola_kernel, dim3((c.chunk_size + kST - 1) / kST, B * m->nsig), dim3(kST), 0, st, FR, T,
+                       c.hop_size, c.chunk_size, out);
+    SESA_CHECK_LAUNCH();
+    profile_end(tok, st, SESA_KCLASS_ISTFT, 4.0 * B * m->nsig * ((double)T * F0 * 2 + (double)c.chunk_size));
+  }
+  return SESA_OK;
+}
+
+extern "C" int sesa_scnet_destroy(sesa_scnet* m) {
+  if (!m) return SESA_OK;
+  for (void* p : {(void*)m->d_f32, (void*)m->d_w, (void*)m->d_bias, (void*)m->d_twT})
+    if (p) (void)hipFree(p);
+  for (auto& L : m->dp)
+    for (int l = 0; l < 2; ++l) {
+      if (L.ih[l].d_groups) (void)hipFree(L.ih[l].d_groups);
+      if (L.lin[l].d_groups) (void)hipFree(L.lin[l].d_groups);
+    }
+  delete m;
+  return SESA_OK;
+}

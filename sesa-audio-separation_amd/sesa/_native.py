@@ -30,6 +30,14 @@ class SesaBsrConfig(ctypes.Structure):
                                                ("freq_indices", ctypes.POINTER(c_int))]
 
 
+class SesaScnetConfig(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("chunk_size", "audio_channels", "n_sources", "n_fft", "hop_size", "win_size",
+                                     "normalized", "n_dims")] + [
+        ("dims", ctypes.POINTER(c_int)), ("band_sr", ctypes.c_double * 3), ("band_stride", c_int * 3),
+        ("band_kernel", c_int * 3), ("conv_depths", c_int * 3), ("compress", c_int), ("conv_kernel", c_int),
+        ("num_dplayer", c_int), ("expand", c_int), ("precision", c_int)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/sesa.h
 SIGNATURES = {
     "sesa_version": (c_int, []),
@@ -57,6 +65,14 @@ SIGNATURES = {
     "sesa_bsr_workspace_size": (c_size_t, [c_void_p, c_int]),
     "sesa_bsr_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
     "sesa_bsr_destroy": (c_int, [c_void_p]),
+    "sesa_scnet_create": (c_int, [ctypes.POINTER(SesaScnetConfig), ctypes.POINTER(c_void_p)]),
+    "sesa_scnet_num_params": (c_int, [c_void_p]),
+    "sesa_scnet_param_info": (c_int, [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64)]),
+    "sesa_scnet_set_param": (c_int, [c_void_p, c_char_p, P_f32, c_int64]),
+    "sesa_scnet_finalize": (c_int, [c_void_p, c_void_p]),
+    "sesa_scnet_workspace_size": (c_size_t, [c_void_p, c_int]),
+    "sesa_scnet_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
+    "sesa_scnet_destroy": (c_int, [c_void_p]),
     "sesa_blend_workspace_size": (c_size_t, [c_int, c_int64]),
     "sesa_blend_f32": (c_int, [P_f32, c_int, c_int, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                c_void_p]),
@@ -66,7 +82,7 @@ SIGNATURES = {
 }
 
 KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6, "act": 7, "tokgemm": 8,
-          "attn": 9}
+          "attn": 9, "lstm": 10, "simt": 11}
 
 
 def profile_enable(on):

@@ -20,7 +20,7 @@ REFERENCE_MODEL_TYPES = (
     "bandit_v2", "scnet_unofficial", "scnet", "apollo", "bs_mamba2", "experimental_mdx23c_stht",
     "mel_band_roformer_experimental", "bs_roformer_experimental", "bs_roformer_custom", "scnet_tran", "scnet_masked",
     "conformer", "mel_band_conformer")
-NATIVE_MODEL_TYPES = ("mdx23c", "bs_roformer", "mel_band_roformer")
+NATIVE_MODEL_TYPES = ("mdx23c", "bs_roformer", "mel_band_roformer", "scnet")
 
 
 def get_model_from_config(model_type: str, config_path: str):
@@ -35,6 +35,9 @@ def get_model_from_config(model_type: str, config_path: str):
     elif model_type == "bs_roformer":
         from .models.bs_roformer import BSRoformer
         model = BSRoformer(**dict(config.model))  # utils.py:104-106
+    elif model_type == "scnet":
+        from .models.scnet import SCNet
+        model = SCNet(**dict(config.model))  # utils.py:119-121
     elif model_type in REFERENCE_MODEL_TYPES:
         raise NotImplementedError(f"model_type '{model_type}' has no MI355X-native implementation yet "
                                   f"(native: {', '.join(NATIVE_MODEL_TYPES)})")

@@ -61,7 +61,7 @@ def test_unknown_and_unported_model_types():
     with pytest.raises(ValueError):
         get_model_from_config("nope", os.path.join(CONFIGS, "config_mdx23c_small.yaml"))
     with pytest.raises(NotImplementedError):
-        get_model_from_config("scnet", os.path.join(CONFIGS, "config_mdx23c_small.yaml"))
+        get_model_from_config("htdemucs", os.path.join(CONFIGS, "config_mdx23c_small.yaml"))
 
 
 @pytest.mark.parametrize("name", sorted(os.listdir(GOLDEN)))

@@ -1,0 +1,159 @@
+"""SCNet on the native path.
+
+CPU (no device work): the oracle restatement (oracle/scnet.py) against the golden vectors of the
+real reference (tests/golden/make_golden_scnet.py); the Python and native parameter registries
+both equal the reference state_dict keys; unsupported configurations are refused.  GPU (marked
+``gpu``): the native forward / demix against the same golden vectors, per-sample RMS <= 1e-4
+(north_star gate) in bf16x3 (the fp32 SIMT kernels are exact fp32; only the LSTM input / output
+Linears run on MFMA); the bf16 throughput mode is measured and reported, not gated.
+"""
+import contextlib
+import ctypes
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import CONFIGS, GOLDEN, rms
+
+RMS_GATE = 1e-4
+
+
+def _cfg(name):
+    from oracle import scnet as osc
+    return osc.load_cfg(os.path.join(CONFIGS, name))
+
+
+def _model(cfg_name, affine="random", precision="bf16x3"):
+    from oracle import scnet as osc
+    from sesa.utils import get_model_from_config
+    m, c = get_model_from_config("scnet", os.path.join(CONFIGS, cfg_name))
+    sd = osc.synth_params(_cfg(cfg_name), affine)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    m.set_precision(precision)
+    return m, c
+
+
+@pytest.mark.parametrize("cfg_name,fx", [("config_scnet_small.yaml", "scnet_small.npz"),
+                                         ("config_musdb18_scnet.yaml", "scnet_full_chunk.npz")])
+def test_oracle_matches_reference(cfg_name, fx, golden):
+    from oracle import scnet as osc
+    g = golden(fx)
+    cfg = _cfg(cfg_name)
+    P = osc.to_torch(osc.synth_params(cfg, str(g["affine"])))
+    with torch.inference_mode():
+        y = osc.forward(P, cfg, torch.from_numpy(g["x"])).numpy()
+    assert y.shape == g["y"].shape
+    assert rms(y, g["y"]) <= 1e-6
+
+
+@pytest.mark.parametrize("cfg_name,tag", [("config_musdb18_scnet.yaml", "musdb"), ("config_scnet_small.yaml", "small")])
+def test_registry_matches_reference_state_dict(cfg_name, tag):
+    from sesa import _native as N
+    from sesa.utils import get_model_from_config
+    m, c = get_model_from_config("scnet", os.path.join(CONFIGS, cfg_name))
+    with open(os.path.join(GOLDEN, f"params_scnet_{tag}.json")) as f:
+        ref = [(n, tuple(s)) for n, s in json.load(f)]
+    assert [(n, tuple(t.shape)) for n, t in m.named_parameters()] == ref
+    h = m._create(c.audio.chunk_size)          # host-side plan only: no device allocation
+    try:
+        names = []
+        for i in range(N.lib().sesa_scnet_num_params(h)):
+            nm, numel = ctypes.c_char_p(), ctypes.c_int64()
+            assert N.lib().sesa_scnet_param_info(h, i, ctypes.byref(nm), ctypes.byref(numel)) == 0
+            names.append((nm.value.decode(), numel.value))
+    finally:
+        N.lib().sesa_scnet_destroy(h)
+    assert names == [(n, int(np.prod(s))) for n, s in ref]
+
+
+def test_create_rejects_unsupported():
+    from sesa import _native as N
+    dims = (ctypes.c_int * 4)(4, 32, 64, 128)
+    base = dict(chunk_size=485100, audio_channels=2, n_sources=4, n_fft=4096, hop_size=1024, win_size=4096,
+                normalized=1, n_dims=4, dims=dims, band_sr=(ctypes.c_double * 3)(0.175, 0.392, 0.433),
+                band_stride=(ctypes.c_int * 3)(1, 4, 16), band_kernel=(ctypes.c_int * 3)(3, 4, 16),
+                conv_depths=(ctypes.c_int * 3)(3, 2, 1), compress=4, conv_kernel=3, num_dplayer=6, expand=1,
+                precision=0)
+    for bad, msg in ((dict(num_dplayer=5), b"num_dplayer"), (dict(n_fft=2048), b"nfft"),
+                     (dict(conv_kernel=5), b"conv_kernel")):
+        c = N.SesaScnetConfig(**{**base, **bad})
+        h = ctypes.c_void_p()
+        assert N.lib().sesa_scnet_create(ctypes.byref(c), ctypes.byref(h)) == -1
+        assert msg in N.lib().sesa_last_error()
+    c = N.SesaScnetConfig(**base)
+    h = ctypes.c_void_p()
+    assert N.lib().sesa_scnet_create(ctypes.byref(c), ctypes.byref(h)) == 0
+    assert N.lib().sesa_scnet_workspace_size(h, 1) > 0
+    N.lib().sesa_scnet_destroy(h)
+
+
+def test_forward_refuses_cpu_tensor():
+    from sesa import _native as N
+    m, c = _model("config_scnet_small.yaml")
+    with pytest.raises(N.SesaError):
+        m(torch.zeros(1, 2, c.audio.chunk_size))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+@pytest.mark.gpu
+def test_forward_small_matches_reference(golden, dev):
+    g = golden("scnet_small.npz")
+    m, _ = _model("config_scnet_small.yaml", str(g["affine"]))
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"scnet small rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    assert y.shape == g["y"].shape and err <= RMS_GATE
+
+
+@pytest.mark.gpu
+def test_forward_small_bf16_reports_deviation(golden, dev):
+    g = golden("scnet_small.npz")
+    m, _ = _model("config_scnet_small.yaml", str(g["affine"]), precision="bf16")
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"scnet small bf16 rms {err:.3e} (reported, not gated)")
+    assert np.isfinite(err) and err < 1e-2
+
+
+@pytest.mark.gpu
+def test_forward_full_chunk_matches_reference(golden, dev):
+    g = golden("scnet_full_chunk.npz")
+    m, _ = _model("config_musdb18_scnet.yaml", str(g["affine"]))
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"scnet musdb full chunk rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    assert err <= RMS_GATE
+
+
+@pytest.mark.gpu
+def test_forward_batch_items_independent(golden, dev):
+    """Batch of 3 (two copies of item 0 around item 1): every item equals its own reference."""
+    g = golden("scnet_small.npz")
+    m, _ = _model("config_scnet_small.yaml", str(g["affine"]))
+    x = np.stack([g["x"][0], g["x"][1], g["x"][0]])
+    y = m(torch.from_numpy(x).to(dev)).cpu().numpy()
+    for i, j in enumerate((0, 1, 0)):
+        assert rms(y[i], g["y"][j]) <= RMS_GATE
+
+
+@pytest.mark.gpu
+def test_demix_matches_reference(golden, dev):
+    from sesa.demix import demix_pytorch_optimized
+    g = golden("demix_scnet_small.npz")
+    m, c = _model("config_scnet_small.yaml", "random")
+    with contextlib.redirect_stdout(io.StringIO()) as out:
+        res = demix_pytorch_optimized(c, m, g["mix"], dev)
+    prog = [ln for ln in out.getvalue().splitlines() if ln.startswith("[SESA_PROGRESS]")]
+    assert prog == list(g["progress"])
+    for k in c.training.instruments:
+        assert res[k].shape == g[f"stem_{k}"].shape
+        assert rms(res[k], g[f"stem_{k}"]) <= RMS_GATE
