@@ -41,7 +41,18 @@ MODELS = {
                "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)"),
     "bs_roformer": ("config_bs_roformer_vocals.yaml", 7.6429e12, "tokgemm",
                     "tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)"),
+    # SCNet: FlopCounterMode on oracle/scnet.py (pinned to the reference, LSTM matmuls written out):
+    # conv 118.3 + LSTM input proj 128.4 + recurrence 128.4 + Linear 32.1 GFLOP per 485100-sample chunk
+    "scnet": ("config_musdb18_scnet.yaml", 4.072e11, "lstm",
+              "scn_lstm_kernel (bi-LSTM recurrence, fp32 FMA, W_hh^T streamed from L2)"),
 }
+METRIC = {"mdx23c": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X",
+          "bs_roformer": "separated-audio sec/sec (RTF), BS-Roformer 44.1kHz stereo, MI355X",
+          "scnet": "separated-audio sec/sec (RTF), SCNet 44.1kHz stereo, MI355X"}
+WORKLOAD = {"mdx23c": "mdx23c_tfc_tdf_v3 vocals config",
+            "bs_roformer": "bs_roformer (viperx 1297: dim 512, depth 12, 8x64 heads, 62 bands) vocals config",
+            "scnet": "scnet musdb18 config (dims 4/32/64/128, 6 dual-path bi-LSTM layers, 4 sources)"}
+EXEC_BATCH = {"mdx23c": 16, "bs_roformer": 4, "scnet": 16}
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
 
 
@@ -60,6 +71,11 @@ def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chu
             cfg = yaml.safe_load(f)
         params = om.to_torch_params(synth_state_dict(om.param_shapes(cfg)))
         fwd = om.forward
+    elif model_name == "scnet":
+        from oracle import scnet as osc
+        cfg = osc.load_cfg(cfg_path)
+        params = osc.to_torch(osc.synth_params(cfg))
+        fwd = osc.forward
     else:
         from oracle import bs_roformer as ob
         cfg = ob.load_cfg(cfg_path)
@@ -75,7 +91,7 @@ def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chu
     return {"value": round(track_seconds / (per_chunk * n_chunks_track), 4), "unit": "separated-audio sec/sec",
             "cores": threads, "kind": "port",
             "sample": f"{sample_chunks} of {n_chunks_track} chunks of the same 4-min track, full-width {model_name} "
-                      f"vocals config, oracle/{'mdx23c' if model_name == 'mdx23c' else 'bs_roformer'}.py PyTorch-CPU "
+                      f"config, oracle/{model_name}.py PyTorch-CPU "
                       f"fp32, {per_chunk:.2f} s/chunk, "
                       f"extrapolated per chunk (OLA <1% of CPU time, SURVEY §6)"}
 
@@ -109,20 +125,25 @@ def main():
 
     cfg_name, flop_per_chunk, kclass, kdesc = MODELS[args.model]
     cfg_path = os.path.join(CFG_DIR, cfg_name)
-    exec_batch = args.exec_batch or (16 if args.model == "mdx23c" else 4)
+    exec_batch = args.exec_batch or EXEC_BATCH[args.model]
     model, cfg = get_model_from_config(args.model, cfg_path)
     if args.model == "mdx23c":
         model.load_state_dict(synth_state_dict(model), strict=True)   # random-init weights (no checkpoint offline)
     else:
         import zlib
         sd = {}
-        for name, shape in model.param_shapes():                      # name-keyed random init, PyTorch bounds
-            t = model.state_dict()[name]
-            if name.endswith("freqs") or name.endswith("gamma"):
-                sd[name] = t
+        shapes = dict(model.param_shapes())
+        defaults = model.state_dict()
+        for name, shape in shapes.items():                            # name-keyed random init, PyTorch bounds
+            wname = name[:-5] + ".weight" if name.endswith(".bias") else name.replace("bias_", "weight_")
+            if len(shape) >= 2:
+                fan_in = int(np.prod(shape[1:]))
+            elif "bias" in name and wname in shapes and len(shapes[wname]) >= 2:
+                fan_in = int(np.prod(shapes[wname][1:]))
+            else:                                                     # rotary freqs, norm gammas / betas
+                sd[name] = defaults[name]
                 continue
             rng = np.random.Generator(np.random.PCG64(zlib.crc32(name.encode()) ^ 0x5E5A))
-            fan_in = shape[1] if len(shape) == 2 else dict(model.param_shapes())[name[:-5] + ".weight"][1]
             b = 1.0 / np.sqrt(fan_in)
             sd[name] = torch.from_numpy(rng.uniform(-b, b, size=shape).astype(np.float32))
         model.load_state_dict(sd, strict=True)
@@ -179,11 +200,9 @@ def main():
     value = args.track_seconds * args.steps / elapsed
     if rank == 0:
         C, ov = int(cfg.audio.chunk_size), int(cfg.inference.num_overlap)
-        wl = ("mdx23c_tfc_tdf_v3 vocals config" if args.model == "mdx23c" else
-              "bs_roformer (viperx 1297: dim 512, depth 12, 8x64 heads, 62 bands) vocals config")
+        wl = WORKLOAD[args.model]
         line = {
-            "metric": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X"
-                      if args.model == "mdx23c" else "separated-audio sec/sec (RTF), BS-Roformer 44.1kHz stereo, MI355X",
+            "metric": METRIC[args.model],
             "value": round(value, 3), "unit": "separated-audio sec/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
@@ -202,7 +221,7 @@ def main():
                                  "launches": alaunch, "avg_launch_ms": round(ams / max(alaunch, 1), 4)}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.model, cfg_path, n_chunks, args.track_seconds,
-                                                args.cpu_sample_chunks or (2 if args.model == "mdx23c" else 1))
+                                                args.cpu_sample_chunks or (1 if args.model == "bs_roformer" else 2))
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
