@@ -52,7 +52,7 @@ METRIC = {"mdx23c": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4
 WORKLOAD = {"mdx23c": "mdx23c_tfc_tdf_v3 vocals config",
             "bs_roformer": "bs_roformer (viperx 1297: dim 512, depth 12, 8x64 heads, 62 bands) vocals config",
             "scnet": "scnet musdb18 config (dims 4/32/64/128, 6 dual-path bi-LSTM layers, 4 sources)"}
-EXEC_BATCH = {"mdx23c": 16, "bs_roformer": 4, "scnet": 16}
+EXEC_BATCH = {"mdx23c": 16, "bs_roformer": 4, "scnet": 48}
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
 
 

@@ -624,6 +624,37 @@ __global__ void __launch_bounds__(kST) scn_lstm_kernel(LstmArgs a) {
   }
 }
 
+// Launch-time choice of ST (sequences per thread; S = ST * 256 / H per workgroup): every
+// workgroup re-reads all of W_hh^T (4 H^2 floats) from L2 per step, so small S multiplies L2
+// traffic while large S serialises FMAs on few CUs.  Model per step: max(L2 bytes / 20 TB/s,
+// resident-wave rounds x S * 4H * H FMA / (128 FMA/clk * 2.4 GHz)); pick the smallest.
+void launch_lstm(const LstmArgs& a, hipStream_t st) {
+  const int H = a.H;
+  int best = 1;
+  double best_t = 1e30;
+  for (int ST = 1; ST <= 16; ST *= 2) {
+    const int S = ST * (kST / H);
+    const double n_wg = 2.0 * ((a.n_seq + S - 1) / S);
+    const double l2 = n_wg * 16.0 * H * H / 20e12;
+    const double comp = std::ceil(n_wg / 256.0) * (double)S * 4.0 * H * H / (128.0 * 2.4e9);
+    const double t = std::max(l2, comp);
+    if (t < best_t * 0.97) {
+      best_t = t;
+      best = ST;
+    }
+  }
+  const int Sq = best * (kST / H);
+  dim3 grid((unsigned)((a.n_seq + Sq - 1) / Sq), 2);
+  const size_t lds = (size_t)2 * Sq * H * 4;
+  switch (best) {
+    case 16: hipLaunchKernelGGL(scn_lstm_kernel<16>, grid, dim3(kST), lds, st, a); break;
+    case 8: hipLaunchKernelGGL(scn_lstm_kernel<8>, grid, dim3(kST), lds, st, a); break;
+    case 4: hipLaunchKernelGGL(scn_lstm_kernel<4>, grid, dim3(kST), lds, st, a); break;
+    case 2: hipLaunchKernelGGL(scn_lstm_kernel<2>, grid, dim3(kST), lds, st, a); break;
+    default: hipLaunchKernelGGL(scn_lstm_kernel<1>, grid, dim3(kST), lds, st, a); break;
+  }
+}
+
 // ---- FeatureConversion (separation.py:20-34): DFTs over T, norm = "ortho" -------------------
 // rfft: X [R][T][C] -> Y [R][K][2C] (real | imag), K = T/2 + 1.  tw[m] = (cos, sin)(2 pi m / T).
 __global__ void __launch_bounds__(kST) scn_rfft_kernel(const float* __restrict__ X, int T, int C,
@@ -1387,19 +1418,8 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
           a.smul_b = Tc;
           a.pstride = 1;
         }
-        const int ngrp = kST / H;
-        int ST = 8;
-        while (ST > 1 && (int64_t)((a.n_seq + ST * ngrp - 1) / (ST * ngrp)) * 2 < 512) ST >>= 1;
-        const int Sq = ST * ngrp;
-        dim3 grid((unsigned)((a.n_seq + Sq - 1) / Sq), 2);
-        const size_t lds = (size_t)2 * Sq * H * 4;
         void* t0 = profile_begin(st);
-        switch (ST) {
-          case 8: hipLaunchKernelGGL(scn_lstm_kernel<8>, grid, dim3(kST), lds, st, a); break;
-          case 4: hipLaunchKernelGGL(scn_lstm_kernel<4>, grid, dim3(kST), lds, st, a); break;
-          case 2: hipLaunchKernelGGL(scn_lstm_kernel<2>, grid, dim3(kST), lds, st, a); break;
-          default: hipLaunchKernelGGL(scn_lstm_kernel<1>, grid, dim3(kST), lds, st, a); break;
-        }
+        launch_lstm(a, st);
         SESA_CHECK_LAUNCH();
         profile_end(t0, st, SESA_KCLASS_LSTM, 2.0 * rows * 2 * 4 * H * (double)H);
       }
