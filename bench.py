@@ -46,13 +46,19 @@ MODELS = {
     "scnet": ("config_musdb18_scnet.yaml", 4.072e11, "lstm",
               "scn_lstm_kernel (bi-LSTM recurrence, fp32 FMA, W_hh^T streamed from L2)"),
 }
-METRIC = {"mdx23c": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X",
+# ensemble (BASELINE configs[4]): the three members' vocals stems, blended on the device
+ENSEMBLE = ("mdx23c", "bs_roformer", "scnet")
+MODELS["ensemble"] = (None, sum(MODELS[m][1] for m in ENSEMBLE), None, None)
+METRIC = {"ensemble": "separated-audio sec/sec (RTF), ensemble mdx23c + bs_roformer + scnet (vocals, avg_wave), MI355X",
+          "mdx23c": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X",
           "bs_roformer": "separated-audio sec/sec (RTF), BS-Roformer 44.1kHz stereo, MI355X",
           "scnet": "separated-audio sec/sec (RTF), SCNet 44.1kHz stereo, MI355X"}
-WORKLOAD = {"mdx23c": "mdx23c_tfc_tdf_v3 vocals config",
+WORKLOAD = {"ensemble": "ensemble.py flow: mdx23c vocals + bs_roformer vocals + scnet musdb18, vocals stems "
+                        "blended (sesa_blend_f32)",
+            "mdx23c": "mdx23c_tfc_tdf_v3 vocals config",
             "bs_roformer": "bs_roformer (viperx 1297: dim 512, depth 12, 8x64 heads, 62 bands) vocals config",
             "scnet": "scnet musdb18 config (dims 4/32/64/128, 6 dual-path bi-LSTM layers, 4 sources)"}
-EXEC_BATCH = {"mdx23c": 16, "bs_roformer": 4, "scnet": 48}
+EXEC_BATCH = {"ensemble": 0, "mdx23c": 16, "bs_roformer": 4, "scnet": 48}
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
 
 
@@ -96,6 +102,41 @@ def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chu
                       f"extrapolated per chunk (OLA <1% of CPU time, SURVEY §6)"}
 
 
+def build_model(name, precision):
+    """Native model of the named workload with name-keyed random-init weights (no checkpoint offline)."""
+    from sesa.utils import get_model_from_config
+    from sesa.weights import synth_state_dict
+    cfg_path = os.path.join(CFG_DIR, MODELS[name][0])
+    model, cfg = get_model_from_config(name, cfg_path)
+    if name == "mdx23c":
+        model.load_state_dict(synth_state_dict(model), strict=True)
+    else:
+        import zlib
+        sd = {}
+        shapes = dict(model.param_shapes())
+        defaults = model.state_dict()
+        for pname, shape in shapes.items():                           # PyTorch default-init bounds
+            wname = pname[:-5] + ".weight" if pname.endswith(".bias") else pname.replace("bias_", "weight_")
+            if len(shape) >= 2:
+                fan_in = int(np.prod(shape[1:]))
+            elif "bias" in pname and wname in shapes and len(shapes[wname]) >= 2:
+                fan_in = int(np.prod(shapes[wname][1:]))
+            else:                                                     # rotary freqs, norm gammas / betas
+                sd[pname] = defaults[pname]
+                continue
+            rng = np.random.Generator(np.random.PCG64(zlib.crc32(pname.encode()) ^ 0x5E5A))
+            b = 1.0 / np.sqrt(fan_in)
+            sd[pname] = torch.from_numpy(rng.uniform(-b, b, size=shape).astype(np.float32))
+        model.load_state_dict(sd, strict=True)
+    model.set_precision(precision)
+    return model, cfg, cfg_path
+
+
+KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)",
+         "tokgemm": "tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)",
+         "lstm": "scn_lstm_kernel (bi-LSTM recurrence, fp32 FMA, W_hh^T streamed from L2)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -103,9 +144,10 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"])
-    ap.add_argument("--exec-batch", type=int, default=0, help="chunks per forward (0: 16 mdx23c / 4 bs_roformer)")
+    ap.add_argument("--exec-batch", type=int, default=0, help="chunks per forward (0: per-model default)")
     ap.add_argument("--track-seconds", type=float, default=240.0)
-    ap.add_argument("--cpu-sample-chunks", type=int, default=0, help="0: 2 (mdx23c) / 1 (bs_roformer)")
+    ap.add_argument("--cpu-sample-chunks", type=int, default=0, help="0: 2 (1 for bs_roformer)")
+    ap.add_argument("--blend", default="avg_wave", help="ensemble blend method (ensemble.py --type)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -119,44 +161,27 @@ def main():
 
     from sesa import _native
     from sesa.demix import chunk_plan
+    from sesa.ensemble import ensemble_separate
     from sesa.parallel import demix_sharded
-    from sesa.utils import get_model_from_config
-    from sesa.weights import synth_state_dict
 
-    cfg_name, flop_per_chunk, kclass, kdesc = MODELS[args.model]
-    cfg_path = os.path.join(CFG_DIR, cfg_name)
-    exec_batch = args.exec_batch or EXEC_BATCH[args.model]
-    model, cfg = get_model_from_config(args.model, cfg_path)
-    if args.model == "mdx23c":
-        model.load_state_dict(synth_state_dict(model), strict=True)   # random-init weights (no checkpoint offline)
-    else:
-        import zlib
-        sd = {}
-        shapes = dict(model.param_shapes())
-        defaults = model.state_dict()
-        for name, shape in shapes.items():                            # name-keyed random init, PyTorch bounds
-            wname = name[:-5] + ".weight" if name.endswith(".bias") else name.replace("bias_", "weight_")
-            if len(shape) >= 2:
-                fan_in = int(np.prod(shape[1:]))
-            elif "bias" in name and wname in shapes and len(shapes[wname]) >= 2:
-                fan_in = int(np.prod(shapes[wname][1:]))
-            else:                                                     # rotary freqs, norm gammas / betas
-                sd[name] = defaults[name]
-                continue
-            rng = np.random.Generator(np.random.PCG64(zlib.crc32(name.encode()) ^ 0x5E5A))
-            b = 1.0 / np.sqrt(fan_in)
-            sd[name] = torch.from_numpy(rng.uniform(-b, b, size=shape).astype(np.float32))
-        model.load_state_dict(sd, strict=True)
-    model.set_precision(args.precision)
+    names = list(ENSEMBLE) if args.model == "ensemble" else [args.model]
+    members = [build_model(nm, args.precision) for nm in names]
+    batches = [args.exec_batch or EXEC_BATCH[nm] for nm in names]
     n = int(round(args.track_seconds * SR))
     rng = np.random.default_rng(0)
     mix = (0.1 * rng.standard_normal((2, n))).astype(np.float32)
     mix_d = torch.from_numpy(mix).to(dev)
-    n_chunks = sum(len(b[0]) for b in chunk_plan(n, cfg.audio.chunk_size, cfg.inference.num_overlap,
-                                                    cfg.inference.batch_size)[3])
+    chunks = [sum(len(b[0]) for b in chunk_plan(n, cfg.audio.chunk_size, cfg.inference.num_overlap,
+                                                 cfg.inference.batch_size)[3]) for _, cfg, _ in members]
+    n_chunks = sum(chunks)
+    path_flop = sum(c * MODELS[nm][1] for c, nm in zip(chunks, names))
 
     def step():
-        return demix_sharded(cfg, model, mix_d, dev, rank=rank, world=world, exec_batch=exec_batch)
+        if args.model == "ensemble":
+            return ensemble_separate([(cfg, m) for m, cfg, _ in members], mix_d, "vocals", args.blend, rank=rank,
+                                     world=world, exec_batch=batches)[0]
+        m, cfg, _ = members[0]
+        return demix_sharded(cfg, m, mix_d, dev, rank=rank, world=world, exec_batch=batches[0])
 
     for _ in range(args.warmup):
         step()
@@ -180,48 +205,68 @@ def main():
         elapsed = float(t.item())
     assert torch.isfinite(est).all().item()
 
+    # dominant kernel class: the model's own, or (ensemble) the class with the most kernel time
+    if args.model == "ensemble":
+        kclass = max(("conv3x3", "tokgemm", "lstm"), key=lambda k: _native.profile_read(k)[0])
+    else:
+        kclass = MODELS[args.model][2]
     ms, launches, work = _native.profile_read(kclass)
     passes = 3 if args.precision == "bf16x3" else 1
     achieved = work / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-    peak = BF16_DENSE_TFLOPS / passes
+    if kclass == "lstm":  # fp32 FMA on the vector ALUs: 157.3 TF/s dense fp32 vector (MI355X_MICROARCH.md)
+        peak, note = 157.3, "157.3 TF/s fp32 vector ALU peak (the recurrence runs as fp32 FMA)"
+    else:
+        peak = BF16_DENSE_TFLOPS / passes
+        note = f"2.5 PF/s dense bf16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
     traffic = None
     pmc = os.path.join(REPO, "profiles", f"pmc_{kclass}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic,
-            "kernel": kdesc,
+            "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": KDESC[kclass],
             "launches": launches, "avg_launch_ms": round(ms / max(launches, 1), 4),
-            "flop_per_launch": round(work / max(launches, 1)),
-            "peak_note": f"2.5 PF/s dense bf16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"}
-    path_tflops = n_chunks * flop_per_chunk * args.steps / elapsed / 1e12
+            "flop_per_launch": round(work / max(launches, 1)), "peak_note": note}
+    path_tflops = path_flop * args.steps / elapsed / 1e12
 
     value = args.track_seconds * args.steps / elapsed
     if rank == 0:
-        C, ov = int(cfg.audio.chunk_size), int(cfg.inference.num_overlap)
-        wl = WORKLOAD[args.model]
+        desc = []
+        for nm, (_, cfg, _), c, eb in zip(names, members, chunks, batches):
+            desc.append(f"{WORKLOAD[nm]} (C={int(cfg.audio.chunk_size)}, overlap {int(cfg.inference.num_overlap)}, "
+                        f"{c} chunks, exec batch {eb})")
+        if args.model == "ensemble":
+            desc = [WORKLOAD["ensemble"] + f" [{args.blend}]: " + "; ".join(desc)]
         line = {
             "metric": METRIC[args.model],
             "value": round(value, 3), "unit": "separated-audio sec/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic: 0.1*N(0,1) stereo mix (seed 0), name-keyed random-init weights",
-            "config": {"workload": f"{wl}, {args.track_seconds:.0f} s 44.1 kHz stereo track chunked (C={C}, "
-                                   f"overlap {ov}, {n_chunks} chunks), mix resident in HBM",
-                       "model": args.model, "chunks": n_chunks, "exec_batch": exec_batch,
+            "config": {"workload": f"{desc[0]}, {args.track_seconds:.0f} s 44.1 kHz stereo track chunked, "
+                                   f"mix resident in HBM",
+                       "model": args.model, "chunks": n_chunks,
+                       "exec_batch": batches[0] if len(batches) == 1 else batches,
                        "parallelism": f"chunk-shard x{world} + RCCL all_gather" if world > 1 else "1 GPU",
                        "path_tflops_algorithmic": round(path_tflops, 2)},
             "roofline": roof,
         }
-        if args.model == "bs_roformer":
+        if "bs_roformer" in names:
             ams, alaunch, awork = _native.profile_read("attn")
             line["attention"] = {"kernel": "attn_kernel (flash, S^T = K Q^T, bf16x3 MFMA)",
                                  "achieved_tflops": round(awork / (ams * 1e-3) / 1e12, 2) if ams > 0 else 0.0,
                                  "launches": alaunch, "avg_launch_ms": round(ams / max(alaunch, 1), 4)}
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.model, cfg_path, n_chunks, args.track_seconds,
-                                                args.cpu_sample_chunks or (1 if args.model == "bs_roformer" else 2))
+            parts = [cpu_baseline(nm, cp, c, args.track_seconds,
+                                  args.cpu_sample_chunks or (1 if nm in ("bs_roformer",) or len(names) > 1 else 2))
+                     for nm, (_, _, cp), c in zip(names, members, chunks)]
+            if len(parts) == 1:
+                line["cpu_baseline"] = parts[0]
+            else:  # the members run one after another: wall times add
+                line["cpu_baseline"] = {
+                    "value": round(args.track_seconds / sum(args.track_seconds / p["value"] for p in parts), 4),
+                    "unit": "separated-audio sec/sec", "cores": parts[0]["cores"], "kind": "port",
+                    "sample": " + ".join(p["sample"] for p in parts) + "; member wall times summed"}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1,0 +1,76 @@
+"""Multi-model ensemble on the device (BASELINE configs[4]: mdx23c + bs_roformer + scnet, stem blend).
+
+``sesa.ensemble.ensemble_separate`` runs each member's chunked separation (sesa/parallel.py,
+world 1 here) and blends the members' vocals stems with ``sesa_blend_f32``.  The oracle
+composition is the GUI flow restated on the CPU: oracle/demix.py (inference_pytorch.py:55-186) per
+member with the members' oracle forwards, then oracle/ensemble.py's blend (ensemble.py:258-407).
+Reduced configs, random weights, a 2.5 s mix.  Gate: per-sample RMS <= 1e-4 (north_star).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from conftest import CONFIGS, rms
+
+MEMBERS = (("mdx23c", "config_mdx23c_small.yaml"), ("bs_roformer", "config_bs_roformer_small.yaml"),
+           ("scnet", "config_scnet_small.yaml"))
+
+
+def _oracle_member(kind, cfg_name):
+    from oracle import bs_roformer as ob
+    from oracle import mdx23c as om
+    from oracle import scnet as osc
+    from oracle.weights import synth_state_dict
+    path = os.path.join(CONFIGS, cfg_name)
+    if kind == "mdx23c":
+        with open(path) as f:
+            cfg = yaml.safe_load(f)
+        raw = synth_state_dict(om.param_shapes(cfg), "random")
+        P = om.to_torch_params(raw)
+        return cfg, raw, lambda x: om.forward(P, cfg, x)
+    if kind == "bs_roformer":
+        cfg = ob.load_cfg(path)
+        raw = ob.synth_params(cfg, "random")
+        P = ob.to_torch(raw)
+        return cfg, raw, lambda x: ob.forward(P, cfg, x)
+    cfg = osc.load_cfg(path)
+    raw = osc.synth_params(cfg, "random")
+    P = osc.to_torch(raw)
+    return cfg, raw, lambda x: osc.forward(P, cfg, x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["avg_wave", "median_fft"])
+def test_ensemble_separate_matches_oracle_composition(method):
+    from oracle import demix as odm
+    from oracle import ensemble as oen
+    from sesa.ensemble import ensemble_separate
+    from sesa.utils import get_model_from_config
+    dev = torch.device("cuda:0")
+    mix = (0.1 * np.random.default_rng(5).standard_normal((2, 110250))).astype(np.float32)
+    members, ref_stems = [], []
+    for kind, cfg_name in MEMBERS:
+        cfg, raw, fwd = _oracle_member(kind, cfg_name)
+        with torch.inference_mode():
+            ref_stems.append(odm.demix(cfg, fwd, mix)["vocals"])
+        m, c = get_model_from_config(kind, os.path.join(CONFIGS, cfg_name))
+        m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in raw.items()}, strict=True)
+        members.append((c, m))
+    out, stems = ensemble_separate(members, torch.from_numpy(mix).to(dev), "vocals", method, rank=0, world=1,
+                                   exec_batch=4)
+    for i, r in enumerate(ref_stems):
+        assert rms(stems[i].cpu().numpy(), r) <= 1e-4, i
+    ref = oen.blend(np.stack(ref_stems), method)
+    assert out.shape == ref.shape
+    assert rms(out.cpu().numpy(), ref) <= 1e-4
+
+
+def test_ensemble_separate_rejects_missing_stem():
+    from sesa.ensemble import ensemble_separate
+    from sesa.utils import get_model_from_config
+    m, c = get_model_from_config("scnet", os.path.join(CONFIGS, "config_scnet_small.yaml"))
+    with pytest.raises(ValueError):
+        ensemble_separate([(c, m)], torch.zeros(2, 100), "guitar")
