@@ -4,7 +4,9 @@ Per MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7: FETCH_SIZE and WRIT
 in SEPARATE passes (TCC slots), both in KiB; on gfx950 FETCH_SIZE reports exactly half of the bytes
 of a wide coalesced streaming read, so it is doubled before comparing with byte counts.
 
-usage: python tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> <kernel-substring> [out.json]
+usage: python tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> <kernel-substring[|substring...]> [out.json]
+(a dispatch matches if its name contains any of the '|'-separated substrings: one kernel CLASS, as
+bench.py's roofline times it)
 """
 import csv
 import glob
@@ -34,8 +36,9 @@ def read_counter(d, counter):
 def main(fetch_dir, write_dir, substr, out=None):
     f, fn = read_counter(fetch_dir, "FETCH_SIZE")
     w, wn = read_counter(write_dir, "WRITE_SIZE")
-    fk = [v for k, v in f.items() if substr in fn[k]]
-    wk = [v for k, v in w.items() if substr in wn[k]]
+    subs = substr.split("|")
+    fk = [v for k, v in f.items() if any(s in fn[k] for s in subs)]
+    wk = [v for k, v in w.items() if any(s in wn[k] for s in subs)]
     if not fk or not wk:
         raise SystemExit(f"no dispatches matching {substr!r}")
     fetch_kib = sum(fk) / len(fk)
