@@ -251,6 +251,16 @@ def main():
                        "path_tflops_algorithmic": round(path_tflops, 2)},
             "roofline": roof,
         }
+        # north_star evidence: HBM GB/s of the streaming kernels (STFT / iSTFT / chunk gather + OLA),
+        # algorithmic bytes / event-timed kernel time, against the 8 TB/s HBM3E peak
+        hbm = {}
+        for kc in ("stft", "istft", "ola"):
+            kms, kn, kbytes = _native.profile_read(kc)
+            if kn:
+                gbs = kbytes / (kms * 1e-3) / 1e9
+                hbm[kc] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / 8000.0, 4), "launches": kn,
+                           "avg_launch_ms": round(kms / kn, 4), "bytes_per_launch": round(kbytes / kn)}
+        line["hbm_kernels"] = {"peak_gbs": 8000.0, **hbm}
         if "bs_roformer" in names:
             ams, alaunch, awork = _native.profile_read("attn")
             line["attention"] = {"kernel": "attn_kernel (flash, S^T = K Q^T, bf16x3 MFMA)",

@@ -225,7 +225,8 @@ int sesa_blend_f32(const float* x, int n_files, int n_ch, int64_t L, int64_t buf
 #define SESA_KCLASS_ATTN 9    /* flash attention (work = 4 L^2 d FLOP per sequence-head)    */
 #define SESA_KCLASS_LSTM 10   /* SCNet bi-LSTM recurrence (work = h W_hh^T FLOP)            */
 #define SESA_KCLASS_SIMT 11   /* SCNet fp32 convolutions / feature-conversion DFTs          */
-#define SESA_KCLASS_COUNT 12
+#define SESA_KCLASS_OLA 12    /* chunk gather / overlap-add / finalize (work = HBM bytes)     */
+#define SESA_KCLASS_COUNT 13
 int sesa_profile_enable(int enable);   /* 1: start recording (clears previous records), 0: stop */
 int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work);
 

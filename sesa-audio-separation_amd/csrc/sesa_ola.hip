@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "sesa_common.hpp"
+#include "sesa_internal.hpp"
 
 namespace sesa {
 namespace {
@@ -137,9 +138,11 @@ extern "C" int sesa_chunk_gather_f32(const float* mix, int n_ch, int64_t L, int6
       tab.seg[j] = (L_pad - s) < chunk ? (L_pad - s) : chunk;
     }
     dim3 grid((unsigned)grid_for(chunk, 256), (unsigned)n);
+    void* tok = profile_begin(as_stream(stream));
     hipLaunchKernelGGL(chunk_gather_kernel, grid, dim3(256), 0, as_stream(stream), mix, n_ch, L, border, L_pad, tab,
                        n, chunk, out + (int64_t)base * n_ch * chunk);
     SESA_CHECK_LAUNCH();
+    profile_end(tok, as_stream(stream), SESA_KCLASS_OLA, 8.0 * n * n_ch * (double)chunk);  // read + write
   }
   return SESA_OK;
 }
@@ -166,10 +169,15 @@ extern "C" int sesa_ola_accumulate_f32(const float* y, int n_chunks, int n_out_c
       lo = s < lo ? s : lo;
       hi = s + sl > hi ? s + sl : hi;
     }
+    double seg_sum = 0;
+    for (int j = 0; j < n; ++j) seg_sum += (double)tab.seg[j];
+    void* tok = profile_begin(as_stream(stream));
     hipLaunchKernelGGL(ola_accumulate_kernel, dim3(grid_for(hi - lo, 256)), dim3(256), 0, as_stream(stream),
                        y + (int64_t)base * n_out_ch * chunk, n, n_out_ch, chunk, tab, lo, hi - lo, window, result,
                        counter, L_pad);
     SESA_CHECK_LAUNCH();
+    // algorithmic bytes: y read once + result / counter span read and written once
+    profile_end(tok, as_stream(stream), SESA_KCLASS_OLA, 4.0 * n_out_ch * seg_sum + 8.0 * (n_out_ch + 1) * (double)(hi - lo));
   }
   return SESA_OK;
 }
@@ -182,8 +190,10 @@ extern "C" int sesa_ola_finalize_f32(const float* result, const float* counter, 
   const int64_t L_out = L_pad - 2 * border;
   if (L_out == 0) return SESA_OK;  // empty track (the reference returns empty stems)
   SESA_REQUIRE(result && counter && out, SESA_ERR_INVALID, "sesa_ola_finalize_f32: null pointer");
+  void* tok = profile_begin(as_stream(stream));
   hipLaunchKernelGGL(ola_finalize_kernel, dim3(grid_for(L_out, 256)), dim3(256), 0, as_stream(stream), result,
                      counter, n_out_ch, L_pad, border, L_out, out);
   SESA_CHECK_LAUNCH();
+  profile_end(tok, as_stream(stream), SESA_KCLASS_OLA, 4.0 * (double)L_out * (2 * n_out_ch + 1));
   return SESA_OK;
 }
