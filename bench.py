@@ -58,7 +58,9 @@ WORKLOAD = {"ensemble": "ensemble.py flow: mdx23c vocals + bs_roformer vocals + 
             "mdx23c": "mdx23c_tfc_tdf_v3 vocals config",
             "bs_roformer": "bs_roformer (viperx 1297: dim 512, depth 12, 8x64 heads, 62 bands) vocals config",
             "scnet": "scnet musdb18 config (dims 4/32/64/128, 6 dual-path bi-LSTM layers, 4 sources)"}
-EXEC_BATCH = {"ensemble": 0, "mdx23c": 16, "bs_roformer": 4, "scnet": 48}
+# chunks per forward: at most this many, balanced so a rank's last forward is not a small remainder
+# (169 chunks at N=1 -> 3 forwards of 57; 22 per rank at N=8 -> one forward of 22)
+EXEC_BATCH = {"ensemble": 0, "mdx23c": 64, "bs_roformer": 4, "scnet": 48}
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
 
 
@@ -166,7 +168,6 @@ def main():
 
     names = list(ENSEMBLE) if args.model == "ensemble" else [args.model]
     members = [build_model(nm, args.precision) for nm in names]
-    batches = [args.exec_batch or EXEC_BATCH[nm] for nm in names]
     n = int(round(args.track_seconds * SR))
     rng = np.random.default_rng(0)
     mix = (0.1 * rng.standard_normal((2, n))).astype(np.float32)
@@ -174,6 +175,12 @@ def main():
     chunks = [sum(len(b[0]) for b in chunk_plan(n, cfg.audio.chunk_size, cfg.inference.num_overlap,
                                                  cfg.inference.batch_size)[3]) for _, cfg, _ in members]
     n_chunks = sum(chunks)
+
+    def balanced(cap, total):
+        local = -(-total // world)
+        return max(1, -(-local // max(1, -(-local // cap))))
+
+    batches = [args.exec_batch or balanced(EXEC_BATCH[nm], c) for nm, c in zip(names, chunks)]
     path_flop = sum(c * MODELS[nm][1] for c, nm in zip(chunks, names))
 
     def step():
