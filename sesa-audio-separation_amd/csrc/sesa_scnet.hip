@@ -221,42 +221,54 @@ struct BandConv {
 };
 
 // Y[b][out_off + fo][t][co] = bias + sum_{kk, ci} W[kk][ci][co] X[b][in_off + fo*s + kk - pad][t][ci]
+// One thread = 4 consecutive output channels of one (b, fo, t): float4 weight loads, each input
+// value feeds 4 FMAs (Cout % 4 == 0, checked at create).  `total` counts (position, channel quad).
 __global__ void scn_sdconv_kernel(const float* __restrict__ X, int Fin, int T, int Cin, const float* __restrict__ W,
                                   const float* __restrict__ bias, BandConv bc, float* __restrict__ Y, int Fout,
                                   int Cout, int64_t total) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int co = (int)(i % Cout);
-  int64_t r = i / Cout;
+  const int C4 = Cout >> 2;
+  const int co = (int)(i % C4) * 4;
+  int64_t r = i / C4;
   const int t = (int)(r % T);
   r /= T;
   const int fo = (int)(r % bc.n_out);
   const int64_t b = r / bc.n_out;
-  float acc = bias[co];
+  float4 acc = *reinterpret_cast<const float4*>(bias + co);
   for (int kk = 0; kk < bc.kern; ++kk) {
     const int fi = fo * bc.stride + kk - bc.pad_left;
     if (fi < 0 || fi >= bc.n_in) continue;
     const float* xp = X + ((b * Fin + bc.in_off + fi) * T + t) * Cin;
     const float* wp = W + (int64_t)kk * Cin * Cout + co;
-    for (int ci = 0; ci < Cin; ++ci) acc = fmaf(wp[(int64_t)ci * Cout], xp[ci], acc);
+    for (int ci = 0; ci < Cin; ++ci) {
+      const float xv = xp[ci];
+      const float4 w = *reinterpret_cast<const float4*>(wp + (int64_t)ci * Cout);
+      acc.x = fmaf(w.x, xv, acc.x);
+      acc.y = fmaf(w.y, xv, acc.y);
+      acc.z = fmaf(w.z, xv, acc.z);
+      acc.w = fmaf(w.w, xv, acc.w);
+    }
   }
-  Y[((b * Fout + bc.out_off + fo) * T + t) * Cout + co] = acc;
+  *reinterpret_cast<float4*>(Y + ((b * Fout + bc.out_off + fo) * T + t) * Cout + co) = acc;
 }
 
 // ConvTranspose2d (kern x 1, stride x 1) of the band rows, trimmed: out row fo <- full row fo + dist
+// (same thread shape as scn_sdconv_kernel)
 __global__ void scn_convtr_kernel(const float* __restrict__ X, int Fin, int T, int Cin, const float* __restrict__ W,
                                   const float* __restrict__ bias, BandConv bc, float* __restrict__ Y, int Fout,
                                   int Cout, int64_t total) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int co = (int)(i % Cout);
-  int64_t r = i / Cout;
+  const int C4 = Cout >> 2;
+  const int co = (int)(i % C4) * 4;
+  int64_t r = i / C4;
   const int t = (int)(r % T);
   r /= T;
   const int fo = (int)(r % bc.n_out);
   const int64_t b = r / bc.n_out;
   const int fp = fo + bc.dist;
-  float acc = bias[co];
+  float4 acc = *reinterpret_cast<const float4*>(bias + co);
   for (int kk = 0; kk < bc.kern; ++kk) {
     const int d = fp - kk;
     if (d < 0 || d % bc.stride) continue;
@@ -264,9 +276,16 @@ __global__ void scn_convtr_kernel(const float* __restrict__ X, int Fin, int T, i
     if (fi >= bc.n_in) continue;
     const float* xp = X + ((b * Fin + bc.in_off + fi) * T + t) * Cin;
     const float* wp = W + (int64_t)kk * Cin * Cout + co;
-    for (int ci = 0; ci < Cin; ++ci) acc = fmaf(wp[(int64_t)ci * Cout], xp[ci], acc);
+    for (int ci = 0; ci < Cin; ++ci) {
+      const float xv = xp[ci];
+      const float4 w = *reinterpret_cast<const float4*>(wp + (int64_t)ci * Cout);
+      acc.x = fmaf(w.x, xv, acc.x);
+      acc.y = fmaf(w.y, xv, acc.y);
+      acc.z = fmaf(w.z, xv, acc.z);
+      acc.w = fmaf(w.w, xv, acc.w);
+    }
   }
-  Y[((b * Fout + bc.out_off + fo) * T + t) * Cout + co] = acc;
+  *reinterpret_cast<float4*>(Y + ((b * Fout + bc.out_off + fo) * T + t) * Cout + co) = acc;
 }
 
 // ---- ConvolutionModule (scnet.py:15-52), one workgroup per (b, f) row of [T][C] --------------
@@ -974,7 +993,7 @@ extern "C" int sesa_scnet_create(const sesa_scnet_config* cfg, sesa_scnet** out)
     }
     L.Fout = fo;
     if (L.h < 1 || (512 % L.h) != 0 || L.h > 64) return fail("ConvolutionModule hidden size must divide 512 and be <= 64", L.h);
-    if (L.Cout % 16 || L.Cout % 2) return fail("dims must be multiples of 16", L.Cout);
+    if (L.Cout % 16 || L.Cdec % 4) return fail("dims must be multiples of 16 (decoder output channels of 4)", L.Cout);
     if (cm_in_lds(L.Cout, L.h) > 160 * 1024 || cm_out_lds(m->T, L.Cout, L.h) > 160 * 1024)
       return fail("ConvolutionModule row does not fit in LDS", L.Cout);
     m->lv.push_back(L);
@@ -1286,11 +1305,11 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     double fl = 0;
     for (int b = 0; b < 3; ++b) {
       const BandConv& bc = L.sd[b];
-      const int64_t total = (int64_t)B * bc.n_out * T * L.Cout;
+      const int64_t total = (int64_t)B * bc.n_out * T * (L.Cout / 4);
       hipLaunchKernelGGL(scn_sdconv_kernel, blocks(total), dim3(kST), 0, st, cur, L.Fin, T, L.Cin, Wb + L.sd_w[b],
                          Wb + L.sd_b[b], bc, skip, L.Fout, L.Cout, total);
       SESA_CHECK_LAUNCH();
-      fl += 2.0 * total * L.Cin * bc.kern;
+      fl += 2.0 * total * 4 * L.Cin * bc.kern;
     }
     for (int b = 0; b < 3; ++b) {
       const BandConv& bc = L.sd[b];
@@ -1482,11 +1501,11 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     double fl = 2.0 * B * L.Fout * T * 2.0 * L.Cout * 2.0 * L.Cout * 9;
     for (int b = 0; b < 3; ++b) {
       const BandConv& bc = L.su[b];
-      const int64_t total = (int64_t)B * bc.n_out * T * L.Cdec;
+      const int64_t total = (int64_t)B * bc.n_out * T * (L.Cdec / 4);
       hipLaunchKernelGGL(scn_convtr_kernel, blocks(total), dim3(kST), 0, st, Y, L.Fout, T, L.Cout, Wb + L.su_w[b],
                          Wb + L.su_b[b], bc, X, L.Fin, L.Cdec, total);
       SESA_CHECK_LAUNCH();
-      fl += 2.0 * total * L.Cout * ((bc.kern + bc.stride - 1) / bc.stride);
+      fl += 2.0 * total * 4 * L.Cout * ((bc.kern + bc.stride - 1) / bc.stride);
     }
     profile_end(tok, st, SESA_KCLASS_SIMT, fl);
   }

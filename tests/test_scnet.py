@@ -157,3 +157,20 @@ def test_demix_matches_reference(golden, dev):
     for k in c.training.instruments:
         assert res[k].shape == g[f"stem_{k}"].shape
         assert rms(res[k], g[f"stem_{k}"]) <= RMS_GATE
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L", [30001, 2049 * 3])
+def test_forward_odd_lengths_match_oracle(dev, L):
+    """Lengths that are not a multiple of the hop (scnet.py:330-333 right pad + crop), against the
+    pinned oracle restatement on the same input."""
+    from oracle import scnet as osc
+    cfg = _cfg("config_scnet_small.yaml")
+    m, _ = _model("config_scnet_small.yaml")
+    P = osc.to_torch(osc.synth_params(cfg, "random"))
+    x = (0.1 * np.random.default_rng(L).standard_normal((1, 2, L))).astype(np.float32)
+    with torch.inference_mode():
+        ref = osc.forward(P, cfg, torch.from_numpy(x)).numpy()
+    y = m(torch.from_numpy(x).to(dev)).cpu().numpy()
+    assert y.shape == ref.shape == (1, 4, 2, L)
+    assert rms(y, ref) <= RMS_GATE
