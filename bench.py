@@ -136,7 +136,7 @@ def build_model(name, precision):
 
 KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)",
          "tokgemm": "tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)",
-         "lstm": "scn_lstm_kernel (bi-LSTM recurrence, fp32 FMA, W_hh^T streamed from L2)"}
+         "lstm": "scn_lstm_mfma_kernel (bi-LSTM recurrence, bf16x3 v_mfma_f32_32x32x16_bf16)"}
 
 
 def main():
@@ -220,11 +220,10 @@ def main():
     ms, launches, work = _native.profile_read(kclass)
     passes = 3 if args.precision == "bf16x3" else 1
     achieved = work / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-    if kclass == "lstm":  # fp32 FMA on the vector ALUs: 157.3 TF/s dense fp32 vector (MI355X_MICROARCH.md)
-        peak, note = 157.3, "157.3 TF/s fp32 vector ALU peak (the recurrence runs as fp32 FMA)"
-    else:
-        peak = BF16_DENSE_TFLOPS / passes
-        note = f"2.5 PF/s dense bf16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
+    peak = BF16_DENSE_TFLOPS / passes
+    note = f"2.5 PF/s dense bf16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
+    if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
+        peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
     traffic = None
     pmc = os.path.join(REPO, "profiles", f"pmc_{kclass}.json")
     if os.path.exists(pmc):

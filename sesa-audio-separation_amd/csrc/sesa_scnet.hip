@@ -27,17 +27,22 @@
 //   scn_gn_*                DualPathRNN GroupNorm(1, d) (fp64 statistics)
 //   tok_gemm (MFMA)         LSTM input projections (both directions, b_ih + b_hh) and the
 //                           Linear(2H -> d) + residual -- sesa_tokgemm.hip, bf16x3 in parity mode
-//   scn_lstm_kernel         bi-LSTM recurrence: one workgroup per (sequence block, direction),
-//                           h in LDS, c in registers, W_hh^T streamed from L2
+//   scn_lstm_mfma_kernel    bi-LSTM recurrence on MFMA (bf16x3): one workgroup per (32 sequences,
+//                           direction), a wave per 32 hidden units x 4 gates (lane-local cell
+//                           update), h as the LDS A operand, W_hh fragments register-resident
+//                           (H <= 128) or streamed (H = 256), c in registers
+//   scn_lstm_kernel         fp32-FMA recurrence (A/B comparison path)
 //   scn_rfft / scn_irfft    FeatureConversion as direct DFTs over T (norm="ortho")
 //   scn_istft_*             normalized inverse (c2r by_root_n), OLA / envelope, trim and crop
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "sesa_common.hpp"
@@ -643,6 +648,136 @@ __global__ void __launch_bounds__(kST) scn_lstm_kernel(LstmArgs a) {
   }
 }
 
+// MFMA recurrence (bf16x3): one workgroup = 32 sequences of one direction, NW = H / 32 waves; wave w
+// owns hidden units 32w .. 32w + 31 for all four gates, so the cell update is lane-local:
+//   gates[32 seq][4H] = h[32][H] . W_hh^T  as v_mfma_f32_32x32x16_bf16 (h and W split hi/lo, 3 passes)
+// h (bf16 hi/lo) lives in LDS as the A operand; W_hh's B fragments are pre-packed per lane
+// ([dir][w][k-step][gate][hi, lo][64 lanes][8]) and streamed from L2 with a PF-deep register ring;
+// the next step's input-projection gates are prefetched under the MFMAs.  c stays in registers.
+// compact gate nonlinearities for the MFMA recurrence (abs. error ~1e-7, far below the bf16x3
+// product error and the 1e-4 gate): one v_exp_f32 + one v_rcp_f32 each
+__device__ __forceinline__ float sigm_f(float v) { return __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
+__device__ __forceinline__ float tanh_f(float v) {
+  const float t = __expf(-2.0f * fabsf(v));
+  return copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), v);
+}
+
+__device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int NW, int PF>
+__global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, const uint16_t* __restrict__ Wf) {
+  constexpr int H = 32 * NW, H4 = 4 * H, KS = H / 16, RS = H + 8;
+  extern __shared__ __align__(16) uint16_t lsa[];
+  uint16_t* Ahi = lsa;            // [32 seq][RS]
+  uint16_t* Alo = lsa + 32 * RS;
+  int64_t* rowb = reinterpret_cast<int64_t*>(lsa + 64 * RS);  // [32] token row of (seq, position 0); -1 = none
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int dir = blockIdx.y;
+  const int s0 = blockIdx.x * 32;
+  const int j = 32 * w + l32;
+  float c[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) c[r] = 0.f;
+  for (int i = threadIdx.x; i < 64 * RS; i += 64 * NW) lsa[i] = 0;  // h_0 = 0 (hi and lo)
+  if (threadIdx.x < 32) {
+    const int sq = s0 + threadIdx.x;
+    rowb[threadIdx.x] = sq < a.n_seq ? (int64_t)(sq / a.sdiv) * a.smul_a + (int64_t)(sq % a.sdiv) * a.smul_b : -1;
+  }
+  // H <= 128: the compiler keeps the whole W_hh slice of a wave in registers across steps (<= 256);
+  // H = 256 (512 per wave) streams it from L2 every step: `volatile` stops that hoisting.
+  constexpr bool STREAM = NW >= 8;
+  using WP = typename std::conditional<STREAM, const volatile bf16x8*, const bf16x8*>::type;
+  WP wb = reinterpret_cast<WP>(Wf) + (int64_t)(dir * NW + w) * KS * 4 * 2 * 64 + lane;
+  __syncthreads();
+  for (int step = 0; step < a.L; ++step) {
+    const int pos = dir ? a.L - 1 - step : step;
+    // input-projection gates: issued now, added after the MFMAs (their latency hides under them);
+    // the streamed-W variant (H = 256) loads them after the MFMAs (register budget of 2 waves/SIMD)
+    float gv[4][16];
+    auto load_g = [&]() {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t rb = rowb[(r & 3) + 8 * (r >> 2) + 4 * hh];
+        const float* gp = a.G + (rb >= 0 ? (rb + (int64_t)pos * a.pstride) * a.g_ld + dir * H4 + j : 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gv[q][r] = rb >= 0 ? gp[q * H] : 0.f;
+      }
+    };
+    if constexpr (!STREAM) load_g();
+    f32x16 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+    bf16x8 bh[PF][4], bl[PF][4];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bh[p][q] = wb[((p * 4 + q) * 2 + 0) * 64];
+        bl[p][q] = wb[((p * 4 + q) * 2 + 1) * 64];
+      }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int slot = ks % PF;
+      const int ao = l32 * RS + 16 * ks + 8 * hh;
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ahi + ao);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Alo + ao);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[q] = mfma_bf16(al, bh[slot][q], acc[q]);
+        acc[q] = mfma_bf16(ah, bl[slot][q], acc[q]);
+        acc[q] = mfma_bf16(ah, bh[slot][q], acc[q]);
+      }
+      if (ks + PF < KS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          bh[slot][q] = wb[(((ks + PF) * 4 + q) * 2 + 0) * 64];
+          bl[slot][q] = wb[(((ks + PF) * 4 + q) * 2 + 1) * 64];
+        }
+      }
+      if constexpr (STREAM) asm volatile("" ::: "memory");  // keep the prefetch depth at PF k-steps
+    }
+    if constexpr (STREAM) load_g();
+    __syncthreads();  // every wave has read h_{t-1}
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int sl = (r & 3) + 8 * (r >> 2) + 4 * hh;
+      const float ig = sigm_f(acc[0][r] + gv[0][r]), fg = sigm_f(acc[1][r] + gv[1][r]);
+      const float gg = tanh_f(acc[2][r] + gv[2][r]), og = sigm_f(acc[3][r] + gv[3][r]);
+      c[r] = fg * c[r] + ig * gg;
+      const float hv = og * tanh_f(c[r]);
+      __bf16 hi, lo;
+      split_bf16(hv, hi, lo);
+      Ahi[sl * RS + j] = __builtin_bit_cast(uint16_t, hi);
+      Alo[sl * RS + j] = __builtin_bit_cast(uint16_t, lo);
+      const int64_t rb = rowb[sl];
+      if (rb >= 0) a.HO[(rb + (int64_t)pos * a.pstride) * a.ho_ld + dir * H + j] = hv;
+    }
+    __syncthreads();  // h_t visible
+  }
+}
+
+template <int NW>
+void launch_lstm_mfma_t(const LstmArgs& a, const uint16_t* Wf, hipStream_t st) {
+  constexpr int PF = 2;
+  const size_t lds = (size_t)64 * (32 * NW + 8) * 2 + 32 * 8;
+  dim3 grid((unsigned)((a.n_seq + 31) / 32), 2);
+  hipLaunchKernelGGL((scn_lstm_mfma_kernel<NW, PF>), grid, dim3(64 * NW), lds, st, a, Wf);
+}
+
+void launch_lstm_mfma(const LstmArgs& a, const uint16_t* Wf, hipStream_t st) {
+  switch (a.H) {
+    case 32: launch_lstm_mfma_t<1>(a, Wf, st); break;
+    case 64: launch_lstm_mfma_t<2>(a, Wf, st); break;
+    case 128: launch_lstm_mfma_t<4>(a, Wf, st); break;
+    default: launch_lstm_mfma_t<8>(a, Wf, st); break;
+  }
+}
+
 // Launch-time choice of ST (sequences per thread; S = ST * 256 / H per workgroup): every
 // workgroup re-reads all of W_hh^T (4 H^2 floats) from L2 per step, so small S multiplies L2
 // traffic while large S serialises FMAs on few CUs.  Model per step: max(L2 bytes / 20 TB/s,
@@ -819,6 +954,7 @@ struct DpLayer {
   int d, H;
   Gemm ih[2], lin[2];
   int64_t whh[2], gn_g[2], gn_b[2];
+  int64_t whh_frag[2];  // uint16 offset of the MFMA B fragments (d_w blob)
 };
 
 }  // namespace
@@ -869,6 +1005,14 @@ struct Plan {
 };
 
 size_t al(size_t floats) { return (floats * 4 + 255) / 256 * 256; }
+
+// Recurrence kernel choice (measured on MI355X, musdb18 config, 4-min track): bf16x3 MFMA for every
+// H (325.7x real-time) beats MFMA for H <= 128 only (307.6x) and the fp32-FMA kernel (280.8x).
+// SESA_LSTM_MFMA=0: fp32 everywhere; =1: MFMA for H <= 128 only (A/B comparisons).
+bool lstm_mfma_on(int H) {
+  static const int mode = getenv("SESA_LSTM_MFMA") ? atoi(getenv("SESA_LSTM_MFMA")) : 2;
+  return mode == 2 || (mode == 1 && H <= 128);
+}
 
 Plan plan(const sesa_scnet* m, int B) {
   Plan p{};
@@ -1215,6 +1359,28 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
           for (int k = 0; k < H; ++k) wt[((size_t)dir * H + k) * 4 * H + n] = Wh[(size_t)n * H + k];
       }
       L.whh[l] = put(wt);
+      {  // B fragments of W_hh for scn_lstm_mfma_kernel: [dir][w][ks][gate][hi, lo][64 lanes][8]
+        const int NW = H / 32, KS = H / 16;
+        L.whh_frag[l] = (int64_t)blob.size();
+        blob.resize(blob.size() + (size_t)2 * NW * KS * 4 * 2 * 64 * 8, 0);
+        uint16_t* f = blob.data() + L.whh_frag[l];
+        for (int dir = 0; dir < 2; ++dir) {
+          const auto& Wh = P(m, q + (dir ? ".weight_hh_l0_reverse" : ".weight_hh_l0"));
+          for (int w = 0; w < NW; ++w)
+            for (int ks = 0; ks < KS; ++ks)
+              for (int g4 = 0; g4 < 4; ++g4)
+                for (int ln = 0; ln < 64; ++ln)
+                  for (int e = 0; e < 8; ++e) {
+                    const int n = g4 * H + 32 * w + (ln & 31);
+                    const int k = 16 * ks + 8 * (ln >> 5) + e;
+                    const float v = Wh[(size_t)n * H + k];
+                    const uint16_t hb = f2bf(v);
+                    const size_t base = ((((((size_t)dir * NW + w) * KS + ks) * 4 + g4) * 2) * 64 + ln) * 8 + e;
+                    f[base] = hb;
+                    f[base + 64 * 8] = f2bf(v - bf2f(hb));
+                  }
+        }
+      }
       L.gn_g[l] = putp(p + ".norm_layers." + S(l) + ".weight");
       L.gn_b[l] = putp(p + ".norm_layers." + S(l) + ".bias");
     }
@@ -1438,7 +1604,8 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
           a.pstride = 1;
         }
         void* t0 = profile_begin(st);
-        launch_lstm(a, st);
+        if (lstm_mfma_on(H)) launch_lstm_mfma(a, m->d_w + L.whh_frag[path], st);
+        else launch_lstm(a, st);
         SESA_CHECK_LAUNCH();
         profile_end(t0, st, SESA_KCLASS_LSTM, 2.0 * rows * 2 * 4 * H * (double)H);
       }
