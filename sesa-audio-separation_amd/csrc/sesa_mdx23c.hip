@@ -264,6 +264,7 @@ struct Fwd {
   int x3;
   char* ws;
   size_t off = 0;        // float region bump offset (bytes)
+  size_t peak = 0;       // high-water mark of `off` (block temporaries are released, see stack())
   size_t stats_off = 0;  // stats region bump offset (bytes), relative to stats_base
   char* stats_base = nullptr;
   size_t stats_cap = 0;
@@ -274,7 +275,8 @@ struct Fwd {
   float* buf(int64_t nfloat) {
     float* p = dry ? nullptr : reinterpret_cast<float*>(ws + off);
     off += ((size_t)nfloat * 4 + 255) & ~(size_t)255;
-    if (!dry && off > float_cap && !rc) {
+    peak = off > peak ? off : peak;
+    if (!dry && peak > float_cap && !rc) {
       set_error("mdx23c forward: workspace plan overflow (%zu > %zu)", off, float_cap);
       rc = SESA_ERR_STATE;  // every later launch is skipped
     }
@@ -376,7 +378,8 @@ struct Fwd {
       const Block& bk = s.blocks[i];
       const int c = bk.c;
       const int64_t plane = (int64_t)B * L.T * L.F * c;
-      float* S = buf(plane);  // block output
+      float* S = buf(plane);  // block output (outlives the block: next block's input / skip)
+      const size_t mark = off;  // everything below is dead once S is written
       float* H = buf(plane);
       float* U = buf(tdf_u_floats((int64_t)B * L.T * c, L.F / bnf));  // tiled U^T (sesa_tapgemm.hip)
       double* st_h1 = stats(c);
@@ -396,6 +399,7 @@ struct Fwd {
            &xs);
       x0 = Tensor{S, st_out, c};
       x1 = Tensor{};
+      off = mark;  // release H, U and the act_split planes (stream order keeps reuse safe)
     }
     return x0;
   }
@@ -421,7 +425,9 @@ struct Fwd {
       Tensor y = stack(m->enc[l], xt, Tensor{}, L);
       skips.push_back(y);
       Tensor d{buf((int64_t)B * L1.T * L1.F * L1.c), stats(L1.c), L1.c};
+      const size_t mark = off;
       conv(m->down[l], act(y, Tensor{}, &m->down_norm[l], L.T, L.F), L.T, L.F, L1.T, L1.F, d.p, nullptr, d.st, 0);
+      off = mark;
       xt = d;
     }
     xt = stack(m->bottleneck, xt, Tensor{}, m->lv[n]);
@@ -431,7 +437,9 @@ struct Fwd {
       const Level& L1 = m->lv[l + 1];
       Tensor upt{buf((int64_t)B * L.T * L.F * L.c), stats(L.c), L.c};
       // Upscale: GEMM over the level-(l+1) positions, N = 4*c_l, scattered to 2x2 outputs
+      const size_t mark = off;
       conv(m->up[i], act(xt, Tensor{}, &m->up_norm[i], L1.T, L1.F), L1.T, L1.F, L1.T, L1.F, upt.p, nullptr, upt.st, 0);
+      off = mark;
       xt = stack(m->dec[i], upt, skips[l], L);
     }
     // x = x * first_conv_out; x = final_conv(cat([mix, x]))
@@ -601,7 +609,7 @@ namespace {
 void plan_sizes(sesa_mdx23c* m, int batch, size_t* float_bytes, size_t* stats_bytes) {
   Fwd f{m, nullptr, true, batch, m->cfg.precision == SESA_PREC_BF16X3 ? 1 : 0, nullptr};
   f.run(nullptr, nullptr);
-  *float_bytes = f.off;
+  *float_bytes = f.peak;
   *stats_bytes = f.stats_off;
 }
 }  // namespace
