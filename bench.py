@@ -260,7 +260,7 @@ def main():
         # north_star evidence: HBM GB/s of the streaming kernels (STFT / iSTFT / chunk gather + OLA),
         # algorithmic bytes / event-timed kernel time, against the 8 TB/s HBM3E peak
         hbm = {}
-        for kc in ("stft", "istft", "ola"):
+        for kc in ("stft", "istft", "ola", "act"):  # act: act_split (norm + GELU + bf16 hi/lo), 8 B/element
             kms, kn, kbytes = _native.profile_read(kc)
             if kn:
                 gbs = kbytes / (kms * 1e-3) / 1e9

@@ -66,6 +66,33 @@ __device__ __forceinline__ float gelu_erf(float v) {
   return v * phi;
 }
 
+// gelu_erf on two values at once: the same sequence of fmas on float2, which gfx950 issues as
+// packed v_pk_fma_f32 / v_pk_mul_f32 (half the VALU issue slots of the scalar form; the rcp / exp2
+// stay per component).  Used by the HBM-streaming act_split pass, where the scalar form made the
+// kernel issue-bound below the HBM rate.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 v) {
+  const f32x2 z = __builtin_elementwise_abs(v) * 0.70710678118654752440f;
+  const f32x2 d = __builtin_elementwise_fma(z, f32x2{0.5f, 0.5f}, f32x2{1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 p = {0.17087277f, 0.17087277f};
+  p = __builtin_elementwise_fma(p, t, f32x2{-0.82215223f, -0.82215223f});
+  p = __builtin_elementwise_fma(p, t, f32x2{1.48851587f, 1.48851587f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-1.13520398f, -1.13520398f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.27886807f, 0.27886807f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-0.18628806f, -0.18628806f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.09678418f, 0.09678418f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.37409196f, 0.37409196f});
+  p = __builtin_elementwise_fma(p, t, f32x2{1.00002368f, 1.00002368f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-1.26551223f, -1.26551223f});
+  const f32x2 a = __builtin_elementwise_fma(-z, z, p) * 1.4426950408889634f;
+  const f32x2 e = t * f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])};
+  const f32x2 one_minus = __builtin_elementwise_fma(e, f32x2{-0.5f, -0.5f}, f32x2{1.0f, 1.0f});
+  const f32x2 half = e * 0.5f;
+  const f32x2 phi = {v[0] >= 0.f ? one_minus[0] : half[0], v[1] >= 0.f ? one_minus[1] : half[1]};
+  return v * phi;
+}
+
 // Split an fp32 value into bf16 hi + bf16 lo (v ~= hi + lo to ~2^-17 relative).
 __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   hi = (__bf16)v;

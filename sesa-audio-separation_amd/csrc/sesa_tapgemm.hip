@@ -76,7 +76,7 @@ __device__ __forceinline__ Src pick_src(const GemmIn& in, int s) {
 
 // Per-channel affine (scale, shift) of the consumer's InstanceNorm, from the producer's sums.
 __device__ void build_affine(const GemmIn& in, int b, float* sc, float* sh) {
-  for (int c = threadIdx.x; c < in.C_in; c += kThreads) {
+  for (int c = threadIdx.x; c < in.C_in; c += blockDim.x) {  // (act_split launches < kThreads threads)
     const int s = c < in.C_split ? 0 : 1;
     const Src src = pick_src(in, s);
     const int cl = c - (s ? in.C_split : 0);
@@ -1050,37 +1050,71 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
 // act_split: one pass over a normalised tensor, writing the bf16 hi/lo operand planes of its
 // consumer (InstanceNorm affine + exact GELU applied once per element instead of once per
 // consuming tile).  HBM-bound: reads 4 B, writes 2 + 2 B per element.
+// Thread layout: blockDim = groups * lanes_pos (groups = C / 8); thread (pl, g) owns the fixed
+// 8-channel group g, so its 8 (scale, shift) pairs live in registers, and walks positions
+// pl, pl + lanes_pos, ... of the block's range -- consecutive threads still cover consecutive
+// 32-B pieces of a row (coalesced), with no per-item index division or LDS affine reads.  Four
+// positions' loads are issued before any is transformed; the GELU runs on packed float2 pairs.
+constexpr int kActUnroll = 4;
 __global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t n_pos, int pos_per_block,
                                                              uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
-  __shared__ float sc[kMaxCin], sh[kMaxCin];
+  __shared__ float sc_s[kMaxCin], sh_s[kMaxCin];
   const int b = blockIdx.y;
-  build_affine(in, b, sc, sh);
+  build_affine(in, b, sc_s, sh_s);
   __syncthreads();
   const int C = in.C_in;
-  const int groups = C / 8;  // 8 channels per thread-item (C % 16 == 0)
-  const int64_t p0 = (int64_t)blockIdx.x * pos_per_block;
-  const int64_t np = (n_pos - p0) < pos_per_block ? (n_pos - p0) : pos_per_block;
-  const int64_t items = np * groups;
-  for (int64_t e = threadIdx.x; e < items; e += kThreads) {
-    const int64_t p = p0 + e / groups;
-    const int c = (int)(e % groups) * 8;
-    const int s = c < in.C_split ? 0 : 1;
-    const Src src = pick_src(in, s);
-    const int cl = c - (s ? in.C_split : 0);
-    const f32x4* xp = reinterpret_cast<const f32x4*>(src.ptr + ((int64_t)b * n_pos + p) * src.C + cl);
-    const f32x4 x0 = xp[0], x1 = xp[1];
-    float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-    __bf16 h8[8], l8[8];
+  const int groups = C >> 3;  // 8 channels per thread (C % 16 == 0)
+  const int lanes_pos = (int)blockDim.x / groups;
+  const int g = (int)threadIdx.x % groups;
+  const int pl = (int)threadIdx.x / groups;
+  if (pl >= lanes_pos) return;
+  const int c = g * 8;
+  const int s = c < in.C_split ? 0 : 1;
+  const Src src = pick_src(in, s);
+  const int cl = c - (s ? in.C_split : 0);
+  const bool act = src.mode == SRC_NORM_GELU;
+  f32x2 sc[4], sh[4];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float y = src.mode == SRC_NORM_GELU ? gelu_erf(v[q] * sc[c + q] + sh[c + q]) : v[q];
-      split_bf16(y, h8[q], l8[q]);
+  for (int q = 0; q < 4; ++q) {
+    sc[q] = f32x2{sc_s[c + 2 * q], sc_s[c + 2 * q + 1]};
+    sh[q] = f32x2{sh_s[c + 2 * q], sh_s[c + 2 * q + 1]};
+  }
+  const int64_t p_begin = (int64_t)blockIdx.x * pos_per_block + pl;
+  const int64_t p_end = (int64_t)(blockIdx.x + 1) * pos_per_block < n_pos ? (int64_t)(blockIdx.x + 1) * pos_per_block
+                                                                           : n_pos;
+  const float* xbase = src.ptr + (int64_t)b * n_pos * src.C + cl;
+  const int64_t obase = (int64_t)b * n_pos * C + c;
+  for (int64_t p0 = p_begin; p0 < p_end; p0 += (int64_t)kActUnroll * lanes_pos) {
+    f32x4 x[kActUnroll][2];
+#pragma unroll
+    for (int u = 0; u < kActUnroll; ++u) {
+      const int64_t p = p0 + (int64_t)u * lanes_pos;
+      if (p < p_end) {
+        const f32x4* xp = reinterpret_cast<const f32x4*>(xbase + p * src.C);
+        x[u][0] = __builtin_nontemporal_load(xp);
+        x[u][1] = __builtin_nontemporal_load(xp + 1);
+      }
     }
-    const int64_t o = ((int64_t)b * n_pos + p) * C + c;
-    *reinterpret_cast<uint4*>(hi + o) =
-        make_uint4(pack2(h8[0], h8[1]), pack2(h8[2], h8[3]), pack2(h8[4], h8[5]), pack2(h8[6], h8[7]));
-    *reinterpret_cast<uint4*>(lo + o) =
-        make_uint4(pack2(l8[0], l8[1]), pack2(l8[2], l8[3]), pack2(l8[4], l8[5]), pack2(l8[6], l8[7]));
+#pragma unroll
+    for (int u = 0; u < kActUnroll; ++u) {
+      const int64_t p = p0 + (int64_t)u * lanes_pos;
+      if (p >= p_end) continue;
+      f32x2 v[4] = {f32x2{x[u][0][0], x[u][0][1]}, f32x2{x[u][0][2], x[u][0][3]}, f32x2{x[u][1][0], x[u][1][1]},
+                    f32x2{x[u][1][2], x[u][1][3]}};
+      uint32_t hw[4], lw[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x2 y = act ? gelu_erf2(__builtin_elementwise_fma(v[q], sc[q], sh[q])) : v[q];
+        __bf16 h0, l0, h1, l1;
+        split_bf16(y[0], h0, l0);
+        split_bf16(y[1], h1, l1);
+        hw[q] = pack2(h0, h1);
+        lw[q] = pack2(l0, l1);
+      }
+      const int64_t o = obase + p * C;
+      *reinterpret_cast<uint4*>(hi + o) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+      *reinterpret_cast<uint4*>(lo + o) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+    }
   }
 }
 
@@ -1178,9 +1212,12 @@ int tdf_block_rows(int M) { return M > 128 ? 256 : M > 64 ? 128 : M > 32 ? 64 : 
 int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st) {
   SESA_REQUIRE(in.C_in % 16 == 0 && in.C_split % 8 == 0 && in.C_in <= kMaxCin, SESA_ERR_INVALID,
                "act_split: C %d must be a multiple of 16 (<= %d)", in.C_in, kMaxCin);
-  const int ppb = (int)((16384 + in.C_in - 1) / in.C_in);  // ~16K elements per block
+  // blockDim = groups * lanes_pos (every thread owns one 8-channel group); ~32 positions per thread
+  const int groups = in.C_in / 8;
+  const int lanes_pos = groups >= kThreads ? 1 : kThreads / groups;
+  const int ppb = lanes_pos * 32;
   dim3 grid((unsigned)((n_pos + ppb - 1) / ppb), (unsigned)batch);
-  hipLaunchKernelGGL(act_split_kernel, grid, dim3(kThreads), 0, st, in, n_pos, ppb, hi, lo);
+  hipLaunchKernelGGL(act_split_kernel, grid, dim3((unsigned)(groups * lanes_pos)), 0, st, in, n_pos, ppb, hi, lo);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }
