@@ -72,6 +72,13 @@ int sesa_istft_f32(const float* spec, int n_sig, int dim_f, int frames, int n_ff
 int sesa_chunk_gather_f32(const float* mix, int n_ch, int64_t L, int64_t border,
                           const int64_t* starts, int n_chunks, int chunk, float* out, void* stream);
 
+/* sesa_chunk_gather_constant_f32 -- utils.py:371-380 + :413-418 (utils.demix demucs mode, model_type
+ *   'htdemucs'): out[j] = zero_pad_C( mix[:, starts[j] : starts[j]+C] ) -- no border pad, and every
+ *   short chunk is padded with zeros ('constant') whatever its length.  Same layouts as above.
+ */
+int sesa_chunk_gather_constant_f32(const float* mix, int n_ch, int64_t L, const int64_t* starts,
+                                   int n_chunks, int chunk, float* out, void* stream);
+
 /* sesa_ola_accumulate_f32 -- inference_pytorch.py:151-159.  For chunk j (in order):
  *   result[:, s_j : s_j+n_j] += y[j, :, :n_j] * window[:n_j];  counter[s_j : s_j+n_j] += window[:n_j]
  * with fp32 multiply-then-add rounding and chunk-order summation exactly as the reference.

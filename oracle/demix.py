@@ -99,6 +99,42 @@ def demix(cfg, model, mix, batch_size=None, num_instruments=None, instruments=No
     return {k: v for k, v in zip(instruments, est)}
 
 
+def demix_demucs_mode(cfg, model, mix):
+    """utils.demix with model_type 'htdemucs' (utils.py:371-380, :408-445, :471-477) restated:
+    C = training.samplerate * training.segment, step = C // num_overlap, no border pad and no
+    fades; chunk i..i+C zero-padded to C ('constant' whatever its length, :413-418); batches of
+    inference.batch_size; result += y[:seg], counter += 1.0 in chunk order; result / counter,
+    NaN -> 0.  Returns the bare array for a single instrument, else {instrument: [2, L]}."""
+    C = int(cfg["training"]["samplerate"] * cfg["training"]["segment"])
+    step = C // cfg["inference"]["num_overlap"]
+    bs = cfg["inference"]["batch_size"]
+    instruments = list(cfg["training"]["instruments"])
+    ni = len(instruments)
+    mix = np.asarray(mix, np.float32)
+    L = mix.shape[-1]
+    result = np.zeros((ni,) + mix.shape, np.float32)
+    counter = np.zeros((ni,) + mix.shape, np.float32)
+    i, batch, locs = 0, [], []
+    while i < L:
+        part = mix[:, i:i + C]
+        n = part.shape[-1]
+        batch.append(np.pad(part, ((0, 0), (0, C - n))))
+        locs.append((i, n))
+        i += step
+        if len(batch) >= bs or i >= L:
+            y = model(torch.from_numpy(np.stack(batch))).detach().cpu().numpy().astype(np.float32)
+            for j, (s, n) in enumerate(locs):
+                result[..., s:s + n] += y[j, ..., :n]
+                counter[..., s:s + n] += 1.0
+            batch, locs = [], []
+    with np.errstate(divide="ignore", invalid="ignore"):
+        est = result / counter
+    np.nan_to_num(est, copy=False, nan=0.0)
+    if ni <= 1:
+        return est
+    return {k: v for k, v in zip(instruments, est)}
+
+
 def normalize_audio(audio):
     """utils.normalize_audio (utils.py:199-217)."""
     mono = audio.mean(0)

@@ -37,11 +37,11 @@ __device__ __forceinline__ int64_t reflect_idx(int64_t p, int64_t n) {
 
 __global__ void chunk_gather_kernel(const float* __restrict__ mix, int n_ch, int64_t L, int64_t border,
                                     int64_t L_pad, ChunkTable tab, int n_chunks, int chunk,
-                                    float* __restrict__ out) {
+                                    int tail_constant, float* __restrict__ out) {
   const int j = blockIdx.y;  // chunk
   const int64_t s = tab.start[j];
   const int64_t seg = tab.seg[j];  // valid length inside the padded mix (<= chunk)
-  const bool reflect_tail = seg > chunk / 2;
+  const bool reflect_tail = !tail_constant && seg > chunk / 2;  // demucs mode: always 'constant'
   for (int c = 0; c < n_ch; ++c) {
     const float* src = mix + (int64_t)c * L;
     float* dst = out + ((int64_t)j * n_ch + c) * chunk;
@@ -119,8 +119,9 @@ int grid_for(int64_t n, int block) {
 
 using namespace sesa;
 
-extern "C" int sesa_chunk_gather_f32(const float* mix, int n_ch, int64_t L, int64_t border, const int64_t* starts,
-                                     int n_chunks, int chunk, float* out, void* stream) {
+namespace {
+int chunk_gather(const float* mix, int n_ch, int64_t L, int64_t border, const int64_t* starts, int n_chunks, int chunk,
+                 int tail_constant, float* out, void* stream) {
   clear_error();
   SESA_REQUIRE(mix && out && starts && n_ch > 0 && L > 0 && chunk > 0, SESA_ERR_INVALID,
                "sesa_chunk_gather_f32: bad arguments");
@@ -140,11 +141,23 @@ extern "C" int sesa_chunk_gather_f32(const float* mix, int n_ch, int64_t L, int6
     dim3 grid((unsigned)grid_for(chunk, 256), (unsigned)n);
     void* tok = profile_begin(as_stream(stream));
     hipLaunchKernelGGL(chunk_gather_kernel, grid, dim3(256), 0, as_stream(stream), mix, n_ch, L, border, L_pad, tab,
-                       n, chunk, out + (int64_t)base * n_ch * chunk);
+                       n, chunk, tail_constant, out + (int64_t)base * n_ch * chunk);
     SESA_CHECK_LAUNCH();
     profile_end(tok, as_stream(stream), SESA_KCLASS_OLA, 8.0 * n * n_ch * (double)chunk);  // read + write
   }
   return SESA_OK;
+}
+}  // namespace
+
+extern "C" int sesa_chunk_gather_f32(const float* mix, int n_ch, int64_t L, int64_t border, const int64_t* starts,
+                                     int n_chunks, int chunk, float* out, void* stream) {
+  return chunk_gather(mix, n_ch, L, border, starts, n_chunks, chunk, 0, out, stream);
+}
+
+// utils.demix demucs mode (utils.py:371-380, :413-418): no border pad, every short tail zero-padded
+extern "C" int sesa_chunk_gather_constant_f32(const float* mix, int n_ch, int64_t L, const int64_t* starts,
+                                              int n_chunks, int chunk, float* out, void* stream) {
+  return chunk_gather(mix, n_ch, L, 0, starts, n_chunks, chunk, 1, out, stream);
 }
 
 extern "C" int sesa_ola_accumulate_f32(const float* y, int n_chunks, int n_out_ch, int chunk, const int64_t* starts,

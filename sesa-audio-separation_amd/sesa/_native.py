@@ -46,6 +46,7 @@ SIGNATURES = {
     "sesa_istft_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "sesa_istft_f32": (c_int, [P_f32, c_int, c_int, c_int, c_int, c_int, P_f32, c_void_p, c_void_p]),
     "sesa_chunk_gather_f32": (c_int, [P_f32, c_int, c_int64, c_int64, P_i64, c_int, c_int, P_f32, c_void_p]),
+    "sesa_chunk_gather_constant_f32": (c_int, [P_f32, c_int, c_int64, P_i64, c_int, c_int, P_f32, c_void_p]),
     "sesa_ola_accumulate_f32": (c_int, [P_f32, c_int, c_int, c_int, P_i64, P_i64, P_f32, P_f32, P_f32, c_int64,
                                         c_void_p]),
     "sesa_ola_finalize_f32": (c_int, [P_f32, P_f32, c_int, c_int64, c_int64, P_f32, c_void_p]),

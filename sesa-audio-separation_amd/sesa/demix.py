@@ -136,6 +136,45 @@ def demix_device(config, model, mix, device, exec_batch=None, progress=True, chu
     return est.reshape(ni, n_ch, L)
 
 
+def demucs_chunk_plan(L, chunk_size, num_overlap):
+    """Chunk list of utils.demix demucs mode (utils.py:371-375, :408-420): starts 0, step, ...
+    while < L, no border pad; returns [(start, seg_len)]."""
+    step = chunk_size // num_overlap
+    return [(i, min(chunk_size, L - i)) for i in range(0, L, step)]
+
+
+def demix_device_demucs(config, model, mix, device, exec_batch=None):
+    """utils.demix demucs mode (utils.py:371-380, :408-445; taken for model_type 'htdemucs'):
+    C = training.samplerate * training.segment, step = C // num_overlap, no fades and no border
+    pad, every chunk zero-padded to C, result += y[:seg], counter += 1, then result / counter with
+    nan_to_num.  The reference's batch grouping does not change the result here (no per-batch
+    window), so chunks run in groups of ``exec_batch``.  Returns the device tensor [n_instr, 2, L]."""
+    C = int(config.training.samplerate * config.training.segment)
+    ov = int(config.inference.num_overlap)
+    ni = len(config.training.instruments)
+    if isinstance(mix, torch.Tensor):
+        mix_d = mix.to(device=device, dtype=torch.float32).contiguous()
+    else:
+        mix_d = torch.from_numpy(np.ascontiguousarray(mix, dtype=np.float32)).to(device, non_blocking=False)
+    n_ch, L = mix_d.shape
+    if L == 0:
+        return torch.zeros(ni, n_ch, 0, device=device, dtype=torch.float32)
+    plan = demucs_chunk_plan(L, C, ov)
+    E = exec_batch or getattr(model, "exec_batch", None) or 8
+    ones = torch.ones(C, device=device, dtype=torch.float32)
+    result = torch.zeros(ni * n_ch, L, device=device, dtype=torch.float32)
+    counter = torch.zeros(L, device=device, dtype=torch.float32)
+    xbuf = None
+    for pos in range(0, len(plan), E):
+        group = plan[pos:pos + E]
+        if xbuf is None or xbuf.shape[0] != len(group):
+            xbuf = torch.empty(len(group), n_ch, C, device=device, dtype=torch.float32)
+        ops.chunk_gather_constant(mix_d, [g[0] for g in group], C, out=xbuf)
+        y = model(xbuf).reshape(len(group), ni * n_ch, C)
+        ops.ola_accumulate(y, [g[0] for g in group], [g[1] for g in group], ones, result, counter)
+    return ops.ola_finalize(result, counter, 0).reshape(ni, n_ch, L)
+
+
 def demix_pytorch_optimized(config, backend, mix, device, pbar=False):
     """inference_pytorch.demix_pytorch_optimized (:55-186): same signature and return value."""
     dev = torch.device(device) if not isinstance(device, torch.device) else device

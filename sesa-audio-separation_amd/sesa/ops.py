@@ -79,6 +79,17 @@ def chunk_gather(mix, border, starts, chunk, out=None):
     return out
 
 
+def chunk_gather_constant(mix, starts, chunk, out=None):
+    """utils.py:413-418 in demucs mode: no border pad, short chunks zero-padded -> [n_chunks, n_ch, chunk]."""
+    mix = _dev_f32(mix, "sesa chunk_gather_constant")
+    n_ch, L = mix.shape
+    if out is None:
+        out = torch.empty(len(starts), n_ch, chunk, device=mix.device, dtype=torch.float32)
+    N.check(N.lib().sesa_chunk_gather_constant_f32(mix.data_ptr(), n_ch, L, N.i64_array(starts), len(starts), chunk,
+                                                   out.data_ptr(), _stream()), "sesa_chunk_gather_constant_f32")
+    return out
+
+
 def ola_accumulate(y, starts, seg_lens, window, result, counter):
     """inference_pytorch.py:151-159 (in place on result/counter)."""
     y = _dev_f32(y, "sesa ola_accumulate")

@@ -64,10 +64,20 @@ def _as_backend(model, device):
 
 
 def demix(config, model, mix, device, model_type: str = "generic", pbar: bool = False):
-    """utils.demix generic mode.  (The 'htdemucs' demucs mode has no native model yet.)"""
-    if model_type == "htdemucs":
-        raise NotImplementedError("demucs-mode demix needs the htdemucs model, not implemented natively yet")
+    """utils.demix (utils.py:330-477).  Generic mode: the device chunker with fades and border pad.
+    model_type 'htdemucs' selects the reference's demucs mode (C = samplerate * segment, no fades,
+    no border pad, zero-padded tails, counter += 1) and returns a bare array when the config has
+    a single instrument, a dict otherwise (:471-477).  The demucs-mode chunker is model-agnostic;
+    the HTDemucs network itself has no native engine yet."""
     dev = torch.device(device) if not isinstance(device, torch.device) else device
+    if model_type == "htdemucs":
+        from .demix import demix_device_demucs
+        m = _as_backend(model, dev) if isinstance(model, torch.nn.Module) else model
+        est = demix_device_demucs(config, m, mix, dev).cpu().numpy()
+        instruments = list(config.training.instruments)
+        if len(instruments) <= 1:
+            return est
+        return {k: v for k, v in zip(instruments, est)}
     est = demix_device(config, _as_backend(model, dev), mix, dev, progress=False).cpu().numpy()
     return {k: v for k, v in zip(prefer_target_instrument(config), est)}
 
