@@ -192,6 +192,46 @@ int sesa_scnet_forward(sesa_scnet* m, const float* x, int batch, float* out, voi
 int sesa_scnet_destroy(sesa_scnet* m);
 
 /* ---------------------------------------------------------------------------------------
+ * HTDemucs (models/demucs4ht.py:28-693 HTDemucs, cac), the hybrid
+ * time / frequency U-Net with the cross-domain transformer.  Replaces HTDemucs.forward
+ * (:548-693) for use_train_segment=False: _spec (:427-446), _magnitude (:459-468), the branch
+ * normalisation, HEncLayer / HDecLayer / DConv (third-party demucs.hdemucs / demucs.demucs,
+ * restated), the CrossTransformerEncoder (demucs.transformer, restated), _mask (:470-481) and
+ * _ispec (:448-457).  Supported: stereo, cac, num_subbands 1, no multi_freqs, wiener_iters 0,
+ * nfft 4096, kernel 8 / stride 4, rewrite, no GroupNorm in the U-Net layers (norm_starts >=
+ * depth), every encoder level a frequency level (no branch merge), sinusoidal embeddings,
+ * dense attention, norm_first + norm_out + LayerScale (the released htdemucs configs).
+ * Parameters are the reference state_dict() keys.
+ */
+typedef struct sesa_htdemucs_config {
+  int chunk_size;                       /* samples per forward item (samplerate * segment)       */
+  int audio_channels, n_sources;
+  int channels, channels_time, growth, nfft, depth;
+  int kernel_size, stride, context, context_enc;
+  int norm_starts, rewrite, cac, num_subbands;
+  int dconv_mode, dconv_depth, dconv_comp;
+  int bottom_channels;
+  int t_layers, t_heads, t_norm_in, t_norm_first, t_norm_out, t_layer_scale, t_gelu, t_cross_first;
+  double t_hidden_scale, freq_emb, emb_scale, t_max_period, t_weight_pos_embed;
+  int precision;                        /* SESA_PREC_*: the MFMA GEMMs (convs, transformer)      */
+} sesa_htdemucs_config;
+
+typedef struct sesa_htdemucs sesa_htdemucs;
+
+int sesa_htdemucs_create(const sesa_htdemucs_config* cfg, sesa_htdemucs** out);
+int sesa_htdemucs_num_params(const sesa_htdemucs* m);
+int sesa_htdemucs_param_info(const sesa_htdemucs* m, int i, const char** name, int64_t* numel);
+/* Shape of the i-th parameter: writes ndim (<= 4) and dims[0 .. ndim). */
+int sesa_htdemucs_param_shape(const sesa_htdemucs* m, int i, int64_t* dims, int* ndim);
+int sesa_htdemucs_set_param(sesa_htdemucs* m, const char* name, const float* host, int64_t numel);
+int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream);
+size_t sesa_htdemucs_workspace_size(const sesa_htdemucs* m, int batch);
+/* x [batch, audio_channels, chunk_size] -> out [batch, n_sources, audio_channels, chunk_size] */
+int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int batch, float* out, void* workspace,
+                          size_t workspace_bytes, void* stream);
+int sesa_htdemucs_destroy(sesa_htdemucs* m);
+
+/* ---------------------------------------------------------------------------------------
  * Ensemble blend (ensemble.py:172-407, AudioEnsembleEngine.process_waveform / process_spectral /
  * run_ensemble's buffer loop).  Methods in the reference's --type order.
  *   x   [n_files][n_ch][L] fp32 (device; the inputs cut to the shortest, ensemble.py:304-306)
@@ -233,7 +273,8 @@ int sesa_blend_f32(const float* x, int n_files, int n_ch, int64_t L, int64_t buf
 #define SESA_KCLASS_LSTM 10   /* SCNet bi-LSTM recurrence (work = h W_hh^T FLOP)            */
 #define SESA_KCLASS_SIMT 11   /* SCNet fp32 convolutions / feature-conversion DFTs          */
 #define SESA_KCLASS_OLA 12    /* chunk gather / overlap-add / finalize (work = HBM bytes)     */
-#define SESA_KCLASS_COUNT 13
+#define SESA_KCLASS_HCONV 13  /* HTDemucs implicit-GEMM convolutions (tok_gemm conv mode)    */
+#define SESA_KCLASS_COUNT 14
 int sesa_profile_enable(int enable);   /* 1: start recording (clears previous records), 0: stop */
 int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work);
 

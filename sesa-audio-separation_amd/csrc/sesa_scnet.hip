@@ -47,93 +47,18 @@
 
 #include "sesa_common.hpp"
 #include "sesa_internal.hpp"
+#include "sesa_fft2048.hpp"
 #include "sesa_tokgemm.hpp"
 
 namespace sesa {
 namespace {
 
-constexpr int kSN = 4096;  // n_fft
-constexpr int kSH = 2048;  // complex FFT length
-constexpr int kST = 256;   // threads per workgroup
-
-struct ScnTables {
-  float2* tw = nullptr;   // exp(-2 pi i j / 2048), j < 2048
-  float2* twN = nullptr;  // exp(-2 pi i k / 4096), k <= 2048
-};
-std::mutex g_mu;
-std::vector<ScnTables> g_tabs;
-
-int get_tables(ScnTables* out) {
-  int dev = 0;
-  SESA_CHECK_HIP(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(g_mu);
-  if ((int)g_tabs.size() <= dev) g_tabs.resize(dev + 1);
-  ScnTables& t = g_tabs[dev];
-  if (!t.tw) {
-    std::vector<float2> a(kSH), b(kSH + 1);
-    for (int j = 0; j < kSH; ++j) {
-      const double ang = -2.0 * M_PI * j / kSH;
-      a[j] = make_float2((float)cos(ang), (float)sin(ang));
-    }
-    for (int k = 0; k <= kSH; ++k) {
-      const double ang = -2.0 * M_PI * k / kSN;
-      b[k] = make_float2((float)cos(ang), (float)sin(ang));
-    }
-    SESA_CHECK_HIP(hipMalloc(&t.tw, kSH * sizeof(float2)));
-    SESA_CHECK_HIP(hipMalloc(&t.twN, (kSH + 1) * sizeof(float2)));
-    SESA_CHECK_HIP(hipMemcpy(t.tw, a.data(), kSH * sizeof(float2), hipMemcpyHostToDevice));
-    SESA_CHECK_HIP(hipMemcpy(t.twN, b.data(), (kSH + 1) * sizeof(float2), hipMemcpyHostToDevice));
-  }
-  *out = t;
-  return SESA_OK;
-}
-
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+constexpr int kSN = kFft4096;  // n_fft
+constexpr int kSH = kFft2048;  // complex FFT length
+constexpr int kST = kFftThreads;   // threads per workgroup
+using ScnTables = Fft2048Tables;
+inline int get_tables(ScnTables* out) { return get_fft2048_tables(out); }
 __device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + expf(-v)); }
-
-// 2048-point Stockham FFT in LDS: five radix-4 stages then one radix-2 stage (256 threads).
-template <bool INV>
-__device__ float2* fft2048(float2* x, float2* y, const float2* __restrict__ tw) {
-  int n = kSH, s = 1;
-#pragma unroll 1
-  for (int stage = 0; stage < 5; ++stage) {
-    const int m = n >> 2;
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int bfly = threadIdx.x + r * kST;  // 512 butterflies per stage
-      const int q = bfly & (s - 1);
-      const int p = bfly >> __builtin_ctz(s);
-      const float2 a = x[q + s * p], b = x[q + s * (p + m)], c = x[q + s * (p + 2 * m)], d = x[q + s * (p + 3 * m)];
-      float2 w1 = tw[p * s], w2 = tw[2 * p * s], w3 = tw[3 * p * s];
-      if (INV) { w1 = cconj(w1); w2 = cconj(w2); w3 = cconj(w3); }
-      const float2 apc = cadd(a, c), amc = csub(a, c), bpd = cadd(b, d), bmd = csub(b, d);
-      const float2 jbmd = INV ? make_float2(-bmd.y, bmd.x) : make_float2(bmd.y, -bmd.x);
-      y[q + s * (4 * p + 0)] = cadd(apc, bpd);
-      y[q + s * (4 * p + 1)] = cmul(w1, cadd(amc, jbmd));
-      y[q + s * (4 * p + 2)] = cmul(w2, csub(apc, bpd));
-      y[q + s * (4 * p + 3)] = cmul(w3, csub(amc, jbmd));
-    }
-    float2* t = x; x = y; y = t;
-    n = m;
-    s <<= 2;
-  }
-  __syncthreads();  // n = 2, s = 1024: final radix-2 stage, unit twiddles
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int q = threadIdx.x + r * kST;
-    const float2 a = x[q], b = x[q + 1024];
-    y[q] = cadd(a, b);
-    y[q + 1024] = csub(a, b);
-  }
-  __syncthreads();
-  return y;
-}
 
 // x [B][ach][chunk] (right zero-padded to Lpad virtually, scnet.py:330-333) -> spec [B][F0][T][2*ach],
 // channel 2*s + (re, im) (scnet.py:343-348).  torch.stft: center, reflect, window = ones.
@@ -161,12 +86,7 @@ __global__ void __launch_bounds__(kST) scn_stft_kernel(const float* __restrict__
   const float2* Z = fft2048<false>(bufA, bufB, tb.tw);
   const int C0 = 2 * ach;
   for (int k = threadIdx.x; k <= kSH; k += kST) {
-    const float2 zk = Z[k & (kSH - 1)];
-    const float2 zm = cconj(Z[(kSH - k) & (kSH - 1)]);
-    const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y + zm.y));
-    const float2 D = csub(zk, zm);
-    const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
-    const float2 X = cadd(E, cmul(tb.twN[k], O));
+    const float2 X = rfft_bin(Z, tb.twN, k);
     *reinterpret_cast<float2*>(spec + (((int64_t)b * (kSH + 1) + k) * T + t) * C0 + 2 * s) =
         make_float2(X.x * scale, X.y * scale);
   }
@@ -187,14 +107,7 @@ __global__ void __launch_bounds__(kST) scn_istft_frames_kernel(const float* __re
     bufB[k] = X;
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < kSH; k += kST) {
-    const float2 xk = bufB[k];
-    const float2 xm = cconj(bufB[kSH - k]);
-    const float2 E = make_float2(0.5f * (xk.x + xm.x), 0.5f * (xk.y + xm.y));
-    const float2 D = csub(xk, xm);
-    const float2 O = cmul(make_float2(0.5f * D.x, 0.5f * D.y), cconj(tb.twN[k]));
-    bufA[k] = make_float2(E.x - O.y, E.y + O.x);
-  }
+  for (int k = threadIdx.x; k < kSH; k += kST) bufA[k] = irfft_pack(bufB, tb.twN, k);
   const float2* z = fft2048<true>(bufA, bufB, tb.tw);
   float2* o = reinterpret_cast<float2*>(fw + ((int64_t)sg * T + t) * kSN);
   for (int k = threadIdx.x; k < kSH; k += kST) {

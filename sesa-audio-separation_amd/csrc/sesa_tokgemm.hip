@@ -57,7 +57,7 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf
 // double-buffered (2 x 64 KB) with ONE barrier per 32-wide K chunk (48 MFMAs per wave per barrier): iteration k runs the MFMAs of
 // stage k&1, writes chunk k+1 (already in registers) to the other stage and issues the global loads
 // of chunk k+2.  The body is straight-line (clamped addresses, validity applied at store time).
-template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB>
+template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB, bool CONV>
 __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a) {
   constexpr int BN = kTokBN, BK = kTokBK;
   static_assert((NT / 64) == (BM / (32 * MI)) * WN && BN == WN * NI * 32, "tile");
@@ -67,6 +67,7 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
   constexpr int STAGE = 2 * A_BYTES + 2 * W_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE];
   __shared__ float rs[BM];
+  __shared__ int orow_base[CONV ? BM : 1], orow_i1[CONV ? BM : 1];  // transposed-conv output rows
 
   const TokGroup g = a.groups[blockIdx.y];
   const int n_tile = blockIdx.x % a.n_tiles_n;
@@ -94,15 +95,28 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
   constexpr int RS = NT / 8;
   const int arow0 = tid >> 3, akq = (tid & 7) * 4;
   f32x4 areg[AI];
+  f32x4 a2reg[CONV ? AI : 1];
   float ss[AI];
   const float* xrow[AI];
   bool rok[AI];
+  // CONV: per-row input grid origin (b Q1, i1 s1, i2 s2) and per-chunk validity
+  int rb1[CONV ? AI : 1], ri1[CONV ? AI : 1], ri2[CONV ? AI : 1];
+  bool aval[CONV ? AI : 1];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     ss[i] = 0.f;
     const int m = m0 + arow0 + RS * i;
     rok[i] = m < a.M;
     xrow[i] = a.x + (int64_t)(rok[i] ? m : a.M - 1) * a.x_ld + g.x_off;
+    if constexpr (CONV) {
+      const int mm = rok[i] ? m : 0;
+      const int i2 = mm % a.geo.P2, t = mm / a.geo.P2;
+      const int i1 = t % a.geo.P1, b = t / a.geo.P1;
+      rb1[i] = b * a.geo.Q1;
+      ri1[i] = i1 * a.geo.s1;
+      ri2[i] = i2 * a.geo.s2;
+      aval[i] = false;
+    }
   }
   bool kok = true;
   constexpr int W16 = (X3 ? 2 : 1) * W_BYTES / 16;
@@ -119,8 +133,22 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
     const int k = kc * BK + akq;
     kok = k < g.K;  // K % 4 == 0 (host check): a quad is wholly in or out
     const int kc_ = kok ? k : 0;
+    if constexpr (CONV) {
+      // Cin % 4 == 0 (host check): a quad lies inside one tap
+      const int tap = kc_ / a.geo.Cin, c = kc_ - tap * a.geo.Cin;
+      const int d1 = a.geo.d1[tap], d2 = a.geo.d2[tap];
 #pragma unroll
-    for (int i = 0; i < AI; ++i) areg[i] = *reinterpret_cast<const f32x4*>(xrow[i] + kc_);
+      for (int i = 0; i < AI; ++i) {
+        const int j1 = ri1[i] + d1, j2 = ri2[i] + d2;
+        aval[i] = rok[i] && kok && j1 >= 0 && j1 < a.geo.Q1 && j2 >= 0 && j2 < a.geo.Q2;
+        const int64_t off = aval[i] ? ((int64_t)(rb1[i] + j1) * a.geo.Q2 + j2) * a.x_ld + g.x_off + c : 0;
+        areg[i] = *reinterpret_cast<const f32x4*>(a.x + off);
+        if (a.geo.x2) a2reg[i] = *reinterpret_cast<const f32x4*>(a.geo.x2 + off);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) areg[i] = *reinterpret_cast<const f32x4*>(xrow[i] + kc_);
+    }
   };
   // count: 1 when this store is a real chunk (0 for the clamped repeat past the end: no RMS sum)
   auto store_chunk = [&](char* stg, float count) {
@@ -134,11 +162,15 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int row = arow0 + RS * i;
-      const bool ok = rok[i] && kok;
+      bool ok = rok[i] && kok;
+      if constexpr (CONV) ok = aval[i];
       __bf16 hi[4], lo[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float v = ok ? areg[i][q] : 0.f;
+        float v = ok ? areg[i][q] : 0.f;
+        if constexpr (CONV) {
+          if (a.geo.x2 && ok) v += a2reg[i][q];
+        }
         ss[i] = fmaf(v * count, v, ss[i]);
         split_bf16(v, hi[q], lo[q]);
       }
@@ -220,6 +252,21 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
     __syncthreads();
   }
 
+  const bool tconv = CONV && a.geo.phases > 1;
+  if constexpr (CONV) {
+    if (a.geo.phases > 1) {
+      for (int r = tid; r < BM; r += NT) {
+        const int m = min(m0 + r, a.M - 1);
+        const int i2 = m % a.geo.P2, t = m / a.geo.P2;
+        const int i1 = t % a.geo.P1, b = t / a.geo.P1;
+        orow_i1[r] = i1 * a.geo.phases - a.geo.opad;
+        orow_base[r] = (b * a.geo.O1 + orow_i1[r]) * a.geo.P2 + i2;
+      }
+      __syncthreads();
+    }
+  }
+  const int n_ph = tconv ? g.N / a.geo.phases : g.N;
+
   // ---- epilogue, one 32x32 block at a time (compile-time block indices: acc stays in VGPRs):
   // scale, bias, activation, rotary / GLU, then residual loads (all before any store: residual may
   // alias out), then stores ----
@@ -241,6 +288,7 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
         x += bias;
         if (a.act == TOK_ACT_GELU) x = gelu_erf(x);
         else if (a.act == TOK_ACT_TANH) x = tanhf(x);
+        else if (a.act == TOK_ACT_RELU) x = fmaxf(x, 0.f);
         const float partner = __shfl_xor(x, 1);  // column n ^ 1, same row
         if (rot) {
           const int m = m0 + ml;
@@ -252,19 +300,33 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
         v[r] = x;
       }
       const int rb = m0 + (wm * MI + i) * 32 + 4 * h;
+      // output row of tile row ml (identity unless transposed conv), validity, column
+      const int ph = tconv ? n / n_ph : 0;
+      const int ncol = tconv ? n - ph * n_ph : n;
+      auto orow = [&](int r, bool& ok) -> int64_t {
+        const int m = rb + (r & 3) + 8 * (r >> 2);
+        ok = m < a.M;
+        if (!tconv) return m;
+        const int ml = m - m0;
+        const int i1 = orow_i1[ml] + ph;
+        ok = ok && i1 >= 0 && i1 < a.geo.O1;
+        return (int64_t)orow_base[ml] + (int64_t)ph * a.geo.P2;
+      };
       if (a.residual && n_ok) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = rb + (r & 3) + 8 * (r >> 2);
-          if (m < a.M) v[r] += a.residual[(int64_t)m * a.o_ld + g.o_off + n];
+          bool ok;
+          const int64_t m = orow(r, ok);
+          if (ok) v[r] += a.residual[m * a.o_ld + g.o_off + ncol];
         }
       }
       if (n_ok && !(a.glu && (n & 1))) {
-        const int nc = a.glu ? n >> 1 : n;
+        const int nc = a.glu ? n >> 1 : ncol;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = rb + (r & 3) + 8 * (r >> 2);
-          if (m < a.M) a.out[(int64_t)m * a.o_ld + g.o_off + nc] = v[r];
+          bool ok;
+          const int64_t m = orow(r, ok);
+          if (ok) a.out[m * a.o_ld + g.o_off + nc] = v[r];
         }
       }
     });
@@ -297,20 +359,28 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
   const int seq = blockIdx.z;
   const int64_t sbase = (int64_t)(seq / a.sdiv) * a.smul_a + (int64_t)(seq % a.sdiv) * a.smul_b;
   auto token = [&](int p) -> int64_t { return sbase + (int64_t)p * a.pstride; };
+  // keys / values: the same sequence of qkv (self) or sequence `seq` of the kv buffer (cross)
+  const float* kvb = a.kv ? a.kv : a.qkv;
+  const int64_t kv_ld = a.kv ? a.kv_ld : a.ld;
+  const int Lk = a.Lk > 0 ? a.Lk : a.L;
+  auto ktoken = [&](int p) -> int64_t { return a.kv ? (int64_t)seq * a.kv_smul + p : token(p); };
+  const int dh = a.dh > 0 ? a.dh : kHD;   // <= 64, % 4 == 0: dims >= dh are zero-padded
+  const float qscale = dh == kHD ? 0.125f : 1.0f / sqrtf((float)dh);
   const int q_pos = blockIdx.x * 128 + wave * 32 + l32;  // this lane's query
   const bool q_ok = q_pos < a.L;
 
-  // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16 ks + 8 hl + j] * 1/8, split
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16 ks + 8 hl + j] / sqrt(dh), split
   bf16x8 qh[4], ql[4];
   {
-    const float* qp = a.qkv + token(q_ok ? q_pos : 0) * a.ld + head * kHD;
+    const float* qp = a.qkv + token(q_ok ? q_pos : 0) * a.ld + head * dh;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const f32x4 v0 = q_ok ? *reinterpret_cast<const f32x4*>(qp + 16 * ks + 8 * hl) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 v1 = q_ok ? *reinterpret_cast<const f32x4*>(qp + 16 * ks + 8 * hl + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int d0 = 16 * ks + 8 * hl;
+      const f32x4 v0 = q_ok && d0 < dh ? *reinterpret_cast<const f32x4*>(qp + d0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 v1 = q_ok && d0 + 4 < dh ? *reinterpret_cast<const f32x4*>(qp + d0 + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float v = (j < 4 ? v0[j] : v1[j - 4]) * 0.125f;  // 1/sqrt(64): exact power of two
+        const float v = (j < 4 ? v0[j] : v1[j - 4]) * qscale;  // 1/sqrt(64) = 0.125 exactly
         __bf16 hi, lo;
         split_bf16(v, hi, lo);
         qh[ks][j] = hi;
@@ -334,8 +404,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
       const int e = tid + i * kThreads;  // (key, 4-d quad): 64 keys x 16 quads
       const int key = e >> 4, dq = (e & 15) * 4;
       const int p = kb * kKB + key;
-      const bool ok = p < a.L;
-      const float* row = a.qkv + token(ok ? p : 0) * a.ld + head * kHD + dq;
+      const bool ok = p < Lk && dq < dh;
+      const float* row = kvb + ktoken(ok ? p : 0) * kv_ld + head * dh + (ok ? dq : 0);
       kreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.k_off) : f32x4{0.f, 0.f, 0.f, 0.f};
       vreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.v_off) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -366,7 +436,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
     }
   };
 
-  const int n_blocks = (a.L + kKB - 1) / kKB;
+  const int n_blocks = (Lk + kKB - 1) / kKB;
   load_block(0);
   for (int kb = 0; kb < n_blocks; ++kb) {
     __syncthreads();
@@ -400,7 +470,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kb * kKB + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        if (key >= a.L) s[rb][r] = -INFINITY;
+        if (key >= Lk) s[rb][r] = -INFINITY;
         bmax = fmaxf(bmax, s[rb][r]);
       }
     bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
@@ -451,14 +521,15 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
 
   if (!q_ok) return;
   const int64_t tq = token(q_pos);
-  const float gate = sigmoidf_(a.qkv[tq * a.ld + a.g_off + head]);
+  const float gate = a.g_off >= 0 ? sigmoidf_(a.qkv[tq * a.ld + a.g_off + head]) : 1.f;
   const float scale = gate / l_run;
-  float* op = a.out + tq * a.o_ld + head * kHD;
+  float* op = a.out + tq * a.o_ld + head * dh;
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const int d = db * 32 + 8 * g4 + 4 * hl;
+      if (d >= dh) continue;
       f32x4 v;
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = o[db][4 * g4 + q] * scale;
@@ -477,21 +548,31 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
   // variant 0 (default): 256 threads, 128 x 128 tile (4 waves of 64 x 64), single stage, 2 WG / CU
   // variant 1: 512 threads, 256 x 128 tile (8 waves of 64 x 64), double-buffered, 1 WG / CU
   static const int variant = getenv("SESA_TOKGEMM_VARIANT") ? atoi(getenv("SESA_TOKGEMM_VARIANT")) : 0;
-  if (variant == 1) {
+  if (a.conv) {
+    const ConvGeo& c = a.geo;
+    SESA_REQUIRE(a.n_groups == 1 && c.Cin > 0 && c.Cin % 4 == 0 && c.n_taps >= 1 && c.n_taps <= kMaxTaps &&
+                     a.x_ld % 4 == 0 && c.P1 > 0 && c.P2 > 0 && c.Q1 > 0 && c.Q2 > 0 && c.phases >= 1 && !a.rope &&
+                     !a.rownorm && (int64_t)c.P1 * c.P2 > 0 && (c.phases == 1 || !a.glu),
+                 SESA_ERR_INVALID, "tok_gemm conv: bad geometry");
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true>), grid, dim3(256), 0, st, a);
+  } else if (variant == 1) {
     const int64_t mt = (a.M + 255) / 256;
     dim3 g1((unsigned)(mt * a.n_tiles_n), (unsigned)a.n_groups);
-    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 512, 256, 2, 2, 2, true>), g1, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 2, true>), g1, dim3(512), 0, st, a);
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 512, 256, 2, 2, 2, true, false>), g1, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 2, true, false>), g1, dim3(512), 0, st, a);
   } else {
-    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false>), grid, dim3(256), 0, st, a);
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, false>), grid, dim3(256), 0, st, a);
   }
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }
 
 int launch_attention(const AttnArgs& a, int x3, hipStream_t st) {
-  SESA_REQUIRE(a.L >= 1 && a.n_seq >= 1 && a.heads >= 1 && a.sdiv >= 1, SESA_ERR_INVALID, "attention: bad shape");
+  SESA_REQUIRE(a.L >= 1 && a.n_seq >= 1 && a.heads >= 1 && a.sdiv >= 1 && a.Lk >= 0 && a.dh >= 0 && a.dh <= kHD &&
+                   a.dh % 4 == 0 && (!a.kv || a.kv_ld % 4 == 0),
+               SESA_ERR_INVALID, "attention: bad shape");
   SESA_REQUIRE(a.n_seq < 65536 * 4 && a.heads < 65536, SESA_ERR_INVALID, "attention: grid too large");
   dim3 grid((unsigned)((a.L + 127) / 128), (unsigned)a.heads, (unsigned)a.n_seq);
   if (x3) hipLaunchKernelGGL(attn_kernel<true>, grid, dim3(kThreads), 0, st, a);

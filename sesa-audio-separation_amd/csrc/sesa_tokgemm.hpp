@@ -14,7 +14,7 @@ constexpr int kTokBM = 256;  // token rows per workgroup tile
 constexpr int kTokBN = 128;  // output columns per workgroup tile (= packed weight row block)
 constexpr int kTokBK = 32;   // K per staged chunk
 
-enum TokAct : int { TOK_ACT_NONE = 0, TOK_ACT_GELU = 1, TOK_ACT_TANH = 2 };
+enum TokAct : int { TOK_ACT_NONE = 0, TOK_ACT_GELU = 1, TOK_ACT_TANH = 2, TOK_ACT_RELU = 3 };
 
 // One GEMM of a (possibly grouped) launch: out[m, o_off + n] = epi(sum_k x[m, x_off + k] W[n, k]).
 struct TokGroup {
@@ -23,6 +23,21 @@ struct TokGroup {
   int64_t o_off;   // float offset of the group's output block inside an output row
   int64_t w_off;   // uint16 offset of the packed weight [ceil(N/128)][ceil(K/32)][hi,lo][128][32]
   int64_t b_off;   // float offset of the bias (< 0: none)
+};
+
+// Implicit-GEMM convolution addressing for tok_gemm (HTDemucs, sesa_htdemucs.hip).  Channels-last
+// activations on a per-item 2-D grid: input element (b, i1, i2, c) at x[((b Q1 + i1) Q2 + i2) x_ld + c].
+// GEMM row m = (b P1 + i1) P2 + i2 (an output position); K = n_taps * Cin with k = tap * Cin + c;
+// tap t reads input position (i1 s1 + d1[t], i2 s2 + d2[t]) (zero outside the grid: conv padding).
+// phases > 1: transposed-conv epilogue -- column n = r * (N / phases) + co is written to output row
+// (b O1 + i1 phases + r - opad) P2 + i2 when 0 <= i1 phases + r - opad < O1 (1-D along axis 1).
+constexpr int kMaxTaps = 9;
+struct ConvGeo {
+  int P1, P2, Q1, Q2, s1, s2;
+  int Cin, n_taps;
+  int d1[kMaxTaps], d2[kMaxTaps];
+  const float* x2;            // nullable: A = x + x2 (same layout; the decoder's x + skip)
+  int phases, O1, opad;
 };
 
 struct TokGemmArgs {
@@ -44,6 +59,8 @@ struct TokGemmArgs {
   int rope_cols;              // columns [0, rope_cols) are rotated (q and k)
   int dim_head;
   int pos_F, pos_T, pos_time; // rotary position of row m: pos_time ? (m / pos_F) % pos_T : m % pos_F
+  int conv;                   // 1: A rows / output rows addressed through `geo` (implicit-GEMM conv)
+  ConvGeo geo;
 };
 
 // Flash attention over strided sequences of a token-major qkv buffer.
@@ -51,12 +68,19 @@ struct TokGemmArgs {
 struct AttnArgs {
   const float* qkv;
   int64_t ld;                 // qkv row stride (floats)
-  int k_off, v_off, g_off;    // column of k / v / gate logits (q at 0); head h adds h * 64 (gates: + h)
-  float* out;                 // [token][heads * 64]
+  int k_off, v_off, g_off;    // column of k / v / gate logits (q at 0); head h adds h * dh (gates: + h);
+                              // g_off < 0: no gate (plain SDPA)
+  float* out;                 // [token][heads * dh]
   int64_t o_ld;
   int L, n_seq, heads;
   int sdiv;
   int64_t smul_a, smul_b, pstride;
+  // cross attention (HTDemucs CrossTransformerEncoderLayer): keys / values from a second buffer
+  const float* kv;            // nullable: k / v columns read from kv (else from qkv)
+  int64_t kv_ld;
+  int Lk;                     // keys per sequence (0: L)
+  int64_t kv_smul;            // kv token of (seq, p) = seq * kv_smul + p (when kv != nullptr)
+  int dh;                     // head dim, <= 64 and % 4 == 0 (0: 64); scale 1 / sqrt(dh)
 };
 
 

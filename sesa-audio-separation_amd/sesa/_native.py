@@ -38,6 +38,16 @@ class SesaScnetConfig(ctypes.Structure):
         ("num_dplayer", c_int), ("expand", c_int), ("precision", c_int)]
 
 
+class SesaHtdemucsConfig(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "chunk_size", "audio_channels", "n_sources", "channels", "channels_time", "growth", "nfft", "depth",
+        "kernel_size", "stride", "context", "context_enc", "norm_starts", "rewrite", "cac", "num_subbands",
+        "dconv_mode", "dconv_depth", "dconv_comp", "bottom_channels", "t_layers", "t_heads", "t_norm_in",
+        "t_norm_first", "t_norm_out", "t_layer_scale", "t_gelu", "t_cross_first")] + [
+        (n, ctypes.c_double) for n in ("t_hidden_scale", "freq_emb", "emb_scale", "t_max_period",
+                                       "t_weight_pos_embed")] + [("precision", c_int)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/sesa.h
 SIGNATURES = {
     "sesa_version": (c_int, []),
@@ -74,6 +84,15 @@ SIGNATURES = {
     "sesa_scnet_workspace_size": (c_size_t, [c_void_p, c_int]),
     "sesa_scnet_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
     "sesa_scnet_destroy": (c_int, [c_void_p]),
+    "sesa_htdemucs_create": (c_int, [ctypes.POINTER(SesaHtdemucsConfig), ctypes.POINTER(c_void_p)]),
+    "sesa_htdemucs_num_params": (c_int, [c_void_p]),
+    "sesa_htdemucs_param_info": (c_int, [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64)]),
+    "sesa_htdemucs_param_shape": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int64), ctypes.POINTER(c_int)]),
+    "sesa_htdemucs_set_param": (c_int, [c_void_p, c_char_p, P_f32, c_int64]),
+    "sesa_htdemucs_finalize": (c_int, [c_void_p, c_void_p]),
+    "sesa_htdemucs_workspace_size": (c_size_t, [c_void_p, c_int]),
+    "sesa_htdemucs_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
+    "sesa_htdemucs_destroy": (c_int, [c_void_p]),
     "sesa_blend_workspace_size": (c_size_t, [c_int, c_int64]),
     "sesa_blend_f32": (c_int, [P_f32, c_int, c_int, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                c_void_p]),
@@ -83,7 +102,7 @@ SIGNATURES = {
 }
 
 KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6, "act": 7, "tokgemm": 8,
-          "attn": 9, "lstm": 10, "simt": 11, "ola": 12}
+          "attn": 9, "lstm": 10, "simt": 11, "ola": 12, "hconv": 13}
 
 
 def profile_enable(on):

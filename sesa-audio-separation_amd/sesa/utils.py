@@ -20,7 +20,7 @@ REFERENCE_MODEL_TYPES = (
     "bandit_v2", "scnet_unofficial", "scnet", "apollo", "bs_mamba2", "experimental_mdx23c_stht",
     "mel_band_roformer_experimental", "bs_roformer_experimental", "bs_roformer_custom", "scnet_tran", "scnet_masked",
     "conformer", "mel_band_conformer")
-NATIVE_MODEL_TYPES = ("mdx23c", "bs_roformer", "mel_band_roformer", "scnet")
+NATIVE_MODEL_TYPES = ("mdx23c", "htdemucs", "bs_roformer", "mel_band_roformer", "scnet")
 
 
 def get_model_from_config(model_type: str, config_path: str):
@@ -38,6 +38,9 @@ def get_model_from_config(model_type: str, config_path: str):
     elif model_type == "scnet":
         from .models.scnet import SCNet
         model = SCNet(**dict(config.model))  # utils.py:119-121
+    elif model_type == "htdemucs":
+        from .models.htdemucs import get_model
+        model = get_model(config)  # utils.py:92-94 -> models/demucs4ht.py:696-711
     elif model_type in REFERENCE_MODEL_TYPES:
         raise NotImplementedError(f"model_type '{model_type}' has no MI355X-native implementation yet "
                                   f"(native: {', '.join(NATIVE_MODEL_TYPES)})")
@@ -57,23 +60,21 @@ def denormalize_audio(audio: np.ndarray, norm_params):
 
 
 def _as_backend(model, device):
-    if hasattr(model, "compiled_model"):
-        return model
-    from .backend import create_inference_session
-    return create_inference_session(model, device=str(device))
+    """The reference passes either a backend or the raw model to demix / apply_tta
+    (inference_pytorch.py:229, :238).  A native model is already a device callable: it is used as
+    is, so its precision (set by the session that owns it) is never changed here."""
+    return model
 
 
 def demix(config, model, mix, device, model_type: str = "generic", pbar: bool = False):
     """utils.demix (utils.py:330-477).  Generic mode: the device chunker with fades and border pad.
     model_type 'htdemucs' selects the reference's demucs mode (C = samplerate * segment, no fades,
     no border pad, zero-padded tails, counter += 1) and returns a bare array when the config has
-    a single instrument, a dict otherwise (:471-477).  The demucs-mode chunker is model-agnostic;
-    the HTDemucs network itself has no native engine yet."""
+    a single instrument, a dict otherwise (:471-477); the native HTDemucs runs under it."""
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     if model_type == "htdemucs":
         from .demix import demix_device_demucs
-        m = _as_backend(model, dev) if isinstance(model, torch.nn.Module) else model
-        est = demix_device_demucs(config, m, mix, dev).cpu().numpy()
+        est = demix_device_demucs(config, _as_backend(model, dev), mix, dev).cpu().numpy()
         instruments = list(config.training.instruments)
         if len(instruments) <= 1:
             return est
