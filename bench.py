@@ -1,26 +1,31 @@
 #!/usr/bin/env python3
-"""Benchmark: separated-audio seconds per wall second (x real-time) for MDX23C-TFC-TDF-v3 on
-MI355X (BASELINE.json metric; workload = configs[1]: 4-min 44.1 kHz stereo track, chunked).
+"""Benchmark: separated-audio seconds per wall second (x real-time) on MI355X (BASELINE.json metric;
+default workload = configs[1]: MDX23C-TFC-TDF-v3 vocals, 4-min 44.1 kHz stereo track, chunked).
 
-One "step" = one full pass of the hot path over the track: chunk gather -> native MDX23C forward
-(exec_batch chunks per launch) -> device windowed overlap-add -> finalize, with the mix already
-resident in HBM.  With --gpus N (launched by torch.distributed.run) the track's chunks are sharded
-contiguously over the N ranks and the span partial sums are joined by one RCCL all_gather
-(sesa/parallel.py); value = track seconds processed / max-over-ranks wall time ("strong" scaling:
-one track, fixed total work).
+One "step" = one full pass of the hot path over the track as SURVEY §8(d) defines the wall time:
+mix on host (pinned) -> H2D -> chunk gather -> native forward (exec_batch chunks per launch) ->
+device windowed overlap-add -> finalize -> stems D2H to host.  With --gpus N (launched by
+torch.distributed.run) the track's chunks are sharded contiguously over the N ranks and the span
+partial sums are joined by one RCCL all_gather (sesa/parallel.py); value = track seconds processed /
+max-over-ranks wall time ("strong" scaling: one track, fixed total work).
+
+Workloads (--model): mdx23c (configs[1], headline), bs_roformer (configs[2]), htdemucs (configs[3]:
+30-min mix, utils.demix demucs-mode chunker, chunk-sharded), ensemble (configs[4]: mdx23c +
+bs_roformer + scnet vocals blended on the device), scnet.
 
 Also reported (rank 0):
-* roofline -- the dominant kernel class (3x3 tap-GEMM convolutions, ~83 % of the FLOPs), timed
-  live in the timed region with hipEvents on the launch stream (libsesa sesa_profile_*):
-  achieved = algorithmic FLOPs / kernel time; peak = dense bf16 MFMA 2.5 PF/s divided by the MFMA
-  passes per algorithmic FLOP (3 in bf16x3 parity precision); traffic = HBM bytes per launch from
-  the committed rocprofv3 PMC summary (profiles/pmc_conv3x3.json) when present.
-* cpu_baseline -- the CPU oracle (PyTorch-CPU fp32 restatement of the reference path, pinned to
-  the reference's golden vectors) on a bounded sample of the same workload (N=1 only).
+* roofline -- the dominant kernel class, timed live in the timed region with hipEvents on the launch
+  stream (libsesa sesa_profile_*): achieved = algorithmic FLOPs / kernel time; peak = dense bf16
+  MFMA 2.5 PF/s divided by the MFMA passes per algorithmic FLOP (3 in bf16x3 parity precision);
+  traffic = HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_<class>.json).
+* cpu_baseline -- the CPU oracle (PyTorch-CPU fp32 restatement of the reference path, pinned to the
+  reference's golden vectors) on a bounded sample of >= 8 chunks of the same workload, on every
+  host core this process may use (N=1 only).
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -34,43 +39,75 @@ import torch.distributed as dist  # noqa: E402
 
 SR = 44100
 CFG_DIR = os.path.join(REPO, "sesa-audio-separation_amd", "sesa", "configs")
-# model -> (config, algorithmic FLOP per chunk (FlopCounterMode on the reference),
-#           dominant kernel class, its description)
+# model -> (config, algorithmic FLOP per chunk, dominant kernel class or None (= most kernel time))
+#   mdx23c / bs_roformer: FlopCounterMode on the reference.
+#   scnet: FlopCounterMode on oracle/scnet.py (LSTM matmuls written out): conv 118.3 + LSTM input proj
+#          128.4 + recurrence 128.4 + Linear 32.1 GFLOP per 485100-sample chunk.
+#   htdemucs: FlopCounterMode on oracle/htdemucs.py (pinned to the reference class): conv 173.5 +
+#          Linear 143.1 GFLOP, plus attention 4 Lq Lk d analytic (FlopCounterMode does not see the
+#          CPU MHA fast path): 3 self layers (3792^2 + 1895^2) + 2 cross layers (2 x 3792 x 1895),
+#          x 4 x 512 = 169.1 GFLOP -> 485.7 GFLOP per 485100-sample segment.
 MODELS = {
-    "mdx23c": ("config_vocals_mdx23c.yaml", 2.4341e12, "conv3x3",
-               "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)"),
-    "bs_roformer": ("config_bs_roformer_vocals.yaml", 7.6429e12, "tokgemm",
-                    "tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)"),
-    # SCNet: FlopCounterMode on oracle/scnet.py (pinned to the reference, LSTM matmuls written out):
-    # conv 118.3 + LSTM input proj 128.4 + recurrence 128.4 + Linear 32.1 GFLOP per 485100-sample chunk
-    "scnet": ("config_musdb18_scnet.yaml", 4.072e11, "lstm",
-              "scn_lstm_kernel (bi-LSTM recurrence, fp32 FMA, W_hh^T streamed from L2)"),
+    "mdx23c": ("config_vocals_mdx23c.yaml", 2.4341e12, "conv3x3"),
+    "bs_roformer": ("config_bs_roformer_vocals.yaml", 7.6429e12, "tokgemm"),
+    "scnet": ("config_musdb18_scnet.yaml", 4.072e11, "lstm"),
+    "htdemucs": ("config_musdb18_htdemucs.yaml", 4.857e11, None),
 }
-# ensemble (BASELINE configs[4]): the three members' vocals stems, blended on the device
 ENSEMBLE = ("mdx23c", "bs_roformer", "scnet")
-MODELS["ensemble"] = (None, sum(MODELS[m][1] for m in ENSEMBLE), None, None)
+MODELS["ensemble"] = (None, sum(MODELS[m][1] for m in ENSEMBLE), None)
 METRIC = {"ensemble": "separated-audio sec/sec (RTF), ensemble mdx23c + bs_roformer + scnet (vocals, avg_wave), MI355X",
           "mdx23c": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X",
           "bs_roformer": "separated-audio sec/sec (RTF), BS-Roformer 44.1kHz stereo, MI355X",
-          "scnet": "separated-audio sec/sec (RTF), SCNet 44.1kHz stereo, MI355X"}
+          "scnet": "separated-audio sec/sec (RTF), SCNet 44.1kHz stereo, MI355X",
+          "htdemucs": "separated-audio sec/sec (RTF), HTDemucs 44.1kHz stereo, 30-min mix chunk-sharded, MI355X"}
 WORKLOAD = {"ensemble": "ensemble.py flow: mdx23c vocals + bs_roformer vocals + scnet musdb18, vocals stems "
                         "blended (sesa_blend_f32)",
             "mdx23c": "mdx23c_tfc_tdf_v3 vocals config",
             "bs_roformer": "bs_roformer (viperx 1297: dim 512, depth 12, 8x64 heads, 62 bands) vocals config",
-            "scnet": "scnet musdb18 config (dims 4/32/64/128, 6 dual-path bi-LSTM layers, 4 sources)"}
+            "scnet": "scnet musdb18 config (dims 4/32/64/128, 6 dual-path bi-LSTM layers, 4 sources)",
+            "htdemucs": "demucs4ht htdemucs musdb18 config (channels 48, depth 4, bottom 512, 5 cross-transformer "
+                        "layers, 4 sources), utils.demix demucs mode (segment 11 s, overlap 4)"}
+TRACK_SECONDS = {"htdemucs": 1800.0}
 # chunks per forward: at most this many, balanced so a rank's last forward is not a small remainder
 # (169 chunks at N=1 -> 3 forwards of 57; 22 per rank at N=8 -> one forward of 22)
-EXEC_BATCH = {"ensemble": 0, "mdx23c": 64, "bs_roformer": 4, "scnet": 48}
+EXEC_BATCH = {"ensemble": 0, "mdx23c": 64, "bs_roformer": 4, "scnet": 48, "htdemucs": 32}
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
+KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)",
+         "tokgemm": "tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)",
+         "lstm": "scn_lstm_mfma_kernel (bi-LSTM recurrence, bf16x3 v_mfma_f32_32x32x16_bf16)",
+         "hconv": "tok_gemm_kernel<conv> (HTDemucs implicit-GEMM convolutions, v_mfma_f32_32x32x16_bf16)",
+         "attn": "attn_kernel (flash attention, S^T = K Q^T, bf16x3 v_mfma_f32_32x32x16_bf16)"}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_cpu():
+    """(threads this process may use, machine CPU count, CPU model string)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(avail, int(omp)) if omp and omp.isdigit() else avail
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return threads, os.cpu_count(), model
+
+
 def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chunks):
-    """Oracle (PyTorch-CPU fp32) forward on `sample_chunks` chunks; extrapolated to the track."""
-    threads = torch.get_num_threads()
+    """Oracle (PyTorch-CPU fp32) forward on `sample_chunks` chunks of the workload; extrapolated to
+    the track (OLA < 1 % of CPU time)."""
+    threads, ncpu, cpu_model = host_cpu()
+    torch.set_num_threads(threads)   # pytorch_backend.py:67-73 uses every core it has
     if model_name == "mdx23c":
         import yaml
         from oracle import mdx23c as om
@@ -79,64 +116,76 @@ def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chu
             cfg = yaml.safe_load(f)
         params = om.to_torch_params(synth_state_dict(om.param_shapes(cfg)))
         fwd = om.forward
+        chunk = int(cfg["audio"]["chunk_size"])
     elif model_name == "scnet":
         from oracle import scnet as osc
         cfg = osc.load_cfg(cfg_path)
         params = osc.to_torch(osc.synth_params(cfg))
         fwd = osc.forward
+        chunk = int(cfg["audio"]["chunk_size"])
+    elif model_name == "htdemucs":
+        import importlib.util
+        from oracle import htdemucs as oh
+        spec = importlib.util.spec_from_file_location("mgh", os.path.join(REPO, "tests", "golden",
+                                                                          "make_golden_htdemucs.py"))
+        mgh = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mgh)
+        cfg = oh.load_cfg(cfg_path)
+        params = oh.load(cfg, mgh.synth_params(dict(oh.param_names(cfg)), "random"))
+        fwd = oh.forward
+        chunk = int(cfg["training"]["samplerate"] * cfg["training"]["segment"])
     else:
         from oracle import bs_roformer as ob
         cfg = ob.load_cfg(cfg_path)
         params = ob.to_torch(ob.synth_params(cfg))
         fwd = ob.forward
+        chunk = int(cfg["audio"]["chunk_size"])
     rng = np.random.default_rng(0)
-    x = torch.from_numpy((0.1 * rng.standard_normal((1, 2, int(cfg["audio"]["chunk_size"])))).astype(np.float32))
-    t0 = time.time()
+    x = torch.from_numpy((0.1 * rng.standard_normal((1, 2, chunk))).astype(np.float32))
     with torch.inference_mode():
+        fwd(params, cfg, x)                       # warm-up (allocator, oneDNN primitives)
+        t0 = time.time()
         for _ in range(sample_chunks):
             fwd(params, cfg, x)
     per_chunk = (time.time() - t0) / sample_chunks
     return {"value": round(track_seconds / (per_chunk * n_chunks_track), 4), "unit": "separated-audio sec/sec",
             "cores": threads, "kind": "port",
-            "sample": f"{sample_chunks} of {n_chunks_track} chunks of the same 4-min track, full-width {model_name} "
-                      f"config, oracle/{model_name}.py PyTorch-CPU "
-                      f"fp32, {per_chunk:.2f} s/chunk, "
-                      f"extrapolated per chunk (OLA <1% of CPU time, SURVEY §6)"}
+            "host": {"cpu_model": cpu_model, "os_cpu_count": ncpu, "threads_used": threads},
+            "sample": f"{sample_chunks} of {n_chunks_track} chunks of the same {track_seconds:.0f} s track "
+                      f"(after 1 warm-up chunk), full-width {model_name} config, oracle/{model_name}.py "
+                      f"PyTorch-CPU fp32 on {threads} threads, {per_chunk:.2f} s/chunk, extrapolated per chunk "
+                      f"(OLA <1% of CPU time, SURVEY §6)"}
+
+
+def synth_weights(model):
+    """Name-keyed random-init weights with PyTorch's default-init bounds (no checkpoint offline)."""
+    import zlib
+    sd = {}
+    shapes = dict(model.param_shapes())
+    defaults = model.state_dict()
+    for pname, shape in shapes.items():
+        wname = pname[:-5] + ".weight" if pname.endswith(".bias") else pname.replace("bias_", "weight_")
+        if len(shape) >= 2:
+            fan_in = int(np.prod(shape[1:]))
+        elif "bias" in pname and wname in shapes and len(shapes[wname]) >= 2:
+            fan_in = int(np.prod(shapes[wname][1:]))
+        else:                                                     # rotary freqs, norm gammas / betas, scales
+            sd[pname] = defaults[pname]
+            continue
+        rng = np.random.Generator(np.random.PCG64(zlib.crc32(pname.encode()) ^ 0x5E5A))
+        b = 1.0 / np.sqrt(fan_in)
+        sd[pname] = torch.from_numpy(rng.uniform(-b, b, size=shape).astype(np.float32))
+    return sd
 
 
 def build_model(name, precision):
-    """Native model of the named workload with name-keyed random-init weights (no checkpoint offline)."""
     from sesa.utils import get_model_from_config
     from sesa.weights import synth_state_dict
     cfg_path = os.path.join(CFG_DIR, MODELS[name][0])
     model, cfg = get_model_from_config(name, cfg_path)
-    if name == "mdx23c":
-        model.load_state_dict(synth_state_dict(model), strict=True)
-    else:
-        import zlib
-        sd = {}
-        shapes = dict(model.param_shapes())
-        defaults = model.state_dict()
-        for pname, shape in shapes.items():                           # PyTorch default-init bounds
-            wname = pname[:-5] + ".weight" if pname.endswith(".bias") else pname.replace("bias_", "weight_")
-            if len(shape) >= 2:
-                fan_in = int(np.prod(shape[1:]))
-            elif "bias" in pname and wname in shapes and len(shapes[wname]) >= 2:
-                fan_in = int(np.prod(shapes[wname][1:]))
-            else:                                                     # rotary freqs, norm gammas / betas
-                sd[pname] = defaults[pname]
-                continue
-            rng = np.random.Generator(np.random.PCG64(zlib.crc32(pname.encode()) ^ 0x5E5A))
-            b = 1.0 / np.sqrt(fan_in)
-            sd[pname] = torch.from_numpy(rng.uniform(-b, b, size=shape).astype(np.float32))
-        model.load_state_dict(sd, strict=True)
+    model.load_state_dict(synth_state_dict(model) if name == "mdx23c" else synth_weights(model), strict=True)
     model.set_precision(precision)
     return model, cfg, cfg_path
-
-
-KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)",
-         "tokgemm": "tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)",
-         "lstm": "scn_lstm_mfma_kernel (bi-LSTM recurrence, bf16x3 v_mfma_f32_32x32x16_bf16)"}
 
 
 def main():
@@ -147,11 +196,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"])
     ap.add_argument("--exec-batch", type=int, default=0, help="chunks per forward (0: per-model default)")
-    ap.add_argument("--track-seconds", type=float, default=240.0)
-    ap.add_argument("--cpu-sample-chunks", type=int, default=0, help="0: 2 (1 for bs_roformer)")
+    ap.add_argument("--track-seconds", type=float, default=0.0, help="0: 240 (1800 for htdemucs)")
+    ap.add_argument("--cpu-sample-chunks", type=int, default=8)
     ap.add_argument("--blend", default="avg_wave", help="ensemble blend method (ensemble.py --type)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    track_seconds = args.track_seconds or TRACK_SECONDS.get(args.model, 240.0)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -162,18 +212,25 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     from sesa import _native
-    from sesa.demix import chunk_plan
+    from sesa.demix import chunk_plan, demucs_chunk_plan
     from sesa.ensemble import ensemble_separate
     from sesa.parallel import demix_sharded
 
     names = list(ENSEMBLE) if args.model == "ensemble" else [args.model]
     members = [build_model(nm, args.precision) for nm in names]
-    n = int(round(args.track_seconds * SR))
+    n = int(round(track_seconds * SR))
     rng = np.random.default_rng(0)
-    mix = (0.1 * rng.standard_normal((2, n))).astype(np.float32)
-    mix_d = torch.from_numpy(mix).to(dev)
-    chunks = [sum(len(b[0]) for b in chunk_plan(n, cfg.audio.chunk_size, cfg.inference.num_overlap,
-                                                 cfg.inference.batch_size)[3]) for _, cfg, _ in members]
+    mix_host = torch.from_numpy((0.1 * rng.standard_normal((2, n))).astype(np.float32)).pin_memory()
+    modes = ["demucs" if nm == "htdemucs" else "generic" for nm in names]
+
+    def n_chunks_of(cfg, mode):
+        if mode == "demucs":
+            return len(demucs_chunk_plan(n, int(cfg.training.samplerate * cfg.training.segment),
+                                         int(cfg.inference.num_overlap)))
+        return sum(len(b[0]) for b in chunk_plan(n, cfg.audio.chunk_size, cfg.inference.num_overlap,
+                                                 cfg.inference.batch_size)[3])
+
+    chunks = [n_chunks_of(cfg, md) for (_, cfg, _), md in zip(members, modes)]
     n_chunks = sum(chunks)
 
     def balanced(cap, total):
@@ -182,13 +239,22 @@ def main():
 
     batches = [args.exec_batch or balanced(EXEC_BATCH[nm], c) for nm, c in zip(names, chunks)]
     path_flop = sum(c * MODELS[nm][1] for c, nm in zip(chunks, names))
+    stems_host = None
 
     def step():
+        nonlocal stems_host
+        mix_d = mix_host.to(dev, non_blocking=True)                          # H2D inside the timed region
         if args.model == "ensemble":
-            return ensemble_separate([(cfg, m) for m, cfg, _ in members], mix_d, "vocals", args.blend, rank=rank,
-                                     world=world, exec_batch=batches)[0]
-        m, cfg, _ = members[0]
-        return demix_sharded(cfg, m, mix_d, dev, rank=rank, world=world, exec_batch=batches[0])
+            est = ensemble_separate([(cfg, m) for m, cfg, _ in members], mix_d, "vocals", args.blend, rank=rank,
+                                    world=world, exec_batch=batches)[0]
+        else:
+            m, cfg, _ = members[0]
+            est = demix_sharded(cfg, m, mix_d, dev, rank=rank, world=world, exec_batch=batches[0], mode=modes[0])
+        if rank == 0:                                                         # stems D2H (one copy of the result)
+            if stems_host is None or stems_host.shape != est.shape or stems_host.dtype != est.dtype:
+                stems_host = torch.empty(est.shape, dtype=est.dtype, pin_memory=True)
+            stems_host.copy_(est, non_blocking=True)
+        return est
 
     for _ in range(args.warmup):
         step()
@@ -211,12 +277,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert torch.isfinite(est).all().item()
+    if rank == 0:
+        assert torch.isfinite(stems_host).all().item() and stems_host.shape == est.shape
 
-    # dominant kernel class: the model's own, or (ensemble) the class with the most kernel time
-    if args.model == "ensemble":
-        kclass = max(("conv3x3", "tokgemm", "lstm"), key=lambda k: _native.profile_read(k)[0])
-    else:
-        kclass = MODELS[args.model][2]
+    # dominant kernel class: the model's own, or the class with the most kernel time
+    kclass = MODELS[args.model][2]
+    if kclass is None:
+        kclass = max(("conv3x3", "tokgemm", "lstm", "hconv", "attn"), key=lambda k: _native.profile_read(k)[0])
     ms, launches, work = _native.profile_read(kclass)
     passes = 3 if args.precision == "bf16x3" else 1
     achieved = work / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
@@ -235,12 +302,13 @@ def main():
             "flop_per_launch": round(work / max(launches, 1)), "peak_note": note}
     path_tflops = path_flop * args.steps / elapsed / 1e12
 
-    value = args.track_seconds * args.steps / elapsed
+    value = track_seconds * args.steps / elapsed
     if rank == 0:
         desc = []
-        for nm, (_, cfg, _), c, eb in zip(names, members, chunks, batches):
-            desc.append(f"{WORKLOAD[nm]} (C={int(cfg.audio.chunk_size)}, overlap {int(cfg.inference.num_overlap)}, "
-                        f"{c} chunks, exec batch {eb})")
+        for nm, (_, cfg, _), c, eb, md in zip(names, members, chunks, batches, modes):
+            C = int(cfg.training.samplerate * cfg.training.segment) if md == "demucs" else int(cfg.audio.chunk_size)
+            desc.append(f"{WORKLOAD[nm]} (C={C}, overlap {int(cfg.inference.num_overlap)}, {c} chunks, "
+                        f"exec batch {eb})")
         if args.model == "ensemble":
             desc = [WORKLOAD["ensemble"] + f" [{args.blend}]: " + "; ".join(desc)]
         line = {
@@ -249,8 +317,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic: 0.1*N(0,1) stereo mix (seed 0), name-keyed random-init weights",
-            "config": {"workload": f"{desc[0]}, {args.track_seconds:.0f} s 44.1 kHz stereo track chunked, "
-                                   f"mix resident in HBM",
+            "config": {"workload": f"{desc[0]}, {track_seconds:.0f} s 44.1 kHz stereo track chunked; timed: pinned "
+                                   f"host mix -> H2D -> separation -> stems D2H",
                        "model": args.model, "chunks": n_chunks,
                        "exec_batch": batches[0] if len(batches) == 1 else batches,
                        "parallelism": f"chunk-shard x{world} + RCCL all_gather" if world > 1 else "1 GPU",
@@ -262,26 +330,33 @@ def main():
         hbm = {}
         for kc in ("stft", "istft", "ola", "act"):  # act: act_split (norm + GELU + bf16 hi/lo), 8 B/element
             kms, kn, kbytes = _native.profile_read(kc)
-            if kn:
+            if kn and kbytes > 0:
                 gbs = kbytes / (kms * 1e-3) / 1e9
                 hbm[kc] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / 8000.0, 4), "launches": kn,
                            "avg_launch_ms": round(kms / kn, 4), "bytes_per_launch": round(kbytes / kn)}
         line["hbm_kernels"] = {"peak_gbs": 8000.0, **hbm}
-        if "bs_roformer" in names:
+        classes = {}
+        for kc in ("conv3x3", "conv1x1", "down", "up", "tdf", "act", "tokgemm", "attn", "lstm", "simt", "hconv",
+                   "stft", "istft", "ola"):
+            kms, kn, kw = _native.profile_read(kc)
+            if kn:
+                classes[kc] = {"ms_per_step": round(kms / args.steps, 2), "launches": kn}
+        line["kernel_classes"] = classes
+        if "bs_roformer" in names or "htdemucs" in names:
             ams, alaunch, awork = _native.profile_read("attn")
-            line["attention"] = {"kernel": "attn_kernel (flash, S^T = K Q^T, bf16x3 MFMA)",
+            line["attention"] = {"kernel": KDESC["attn"],
                                  "achieved_tflops": round(awork / (ams * 1e-3) / 1e12, 2) if ams > 0 else 0.0,
                                  "launches": alaunch, "avg_launch_ms": round(ams / max(alaunch, 1), 4)}
         if world == 1 and not args.no_cpu_baseline:
-            parts = [cpu_baseline(nm, cp, c, args.track_seconds,
-                                  args.cpu_sample_chunks or (1 if nm in ("bs_roformer",) or len(names) > 1 else 2))
+            parts = [cpu_baseline(nm, cp, c, track_seconds, args.cpu_sample_chunks if len(names) == 1 else 2)
                      for nm, (_, _, cp), c in zip(names, members, chunks)]
             if len(parts) == 1:
                 line["cpu_baseline"] = parts[0]
             else:  # the members run one after another: wall times add
                 line["cpu_baseline"] = {
-                    "value": round(args.track_seconds / sum(args.track_seconds / p["value"] for p in parts), 4),
+                    "value": round(track_seconds / sum(track_seconds / p["value"] for p in parts), 4),
                     "unit": "separated-audio sec/sec", "cores": parts[0]["cores"], "kind": "port",
+                    "host": parts[0]["host"],
                     "sample": " + ".join(p["sample"] for p in parts) + "; member wall times summed"}
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -85,6 +85,7 @@ int sesa_chunk_gather_constant_f32(const float* mix, int n_ch, int64_t L, const 
  *   y [n_chunks, n_out_ch, C] (n_out_ch = n_instr * 2), window [C] (device, the batch's window
  *   after the first/last fade fix-ups), result [n_out_ch, L_pad], counter [L_pad].
  *   starts / seg_lens are host arrays (the chunk plan is host-side control).
+ *   n_out_ch == 0 (y and result may be NULL) accumulates the counter only.
  */
 int sesa_ola_accumulate_f32(const float* y, int n_chunks, int n_out_ch, int chunk,
                             const int64_t* starts, const int64_t* seg_lens, const float* window,

@@ -164,7 +164,10 @@ extern "C" int sesa_ola_accumulate_f32(const float* y, int n_chunks, int n_out_c
                                        const int64_t* seg_lens, const float* window, float* result, float* counter,
                                        int64_t L_pad, void* stream) {
   clear_error();
-  SESA_REQUIRE(y && starts && seg_lens && window && result && counter && n_out_ch > 0 && chunk > 0,
+  // n_out_ch == 0 (y / result may be NULL): counter only -- the multi-GPU path recomputes the
+  // deterministic counter locally instead of exchanging it
+  SESA_REQUIRE(starts && seg_lens && window && counter && n_out_ch >= 0 && chunk > 0 &&
+                   (n_out_ch == 0 || (y && result)),
                SESA_ERR_INVALID, "sesa_ola_accumulate_f32: bad arguments");
   // Launch in groups of kMaxChunks; groups are issued in order on one stream, so the per-sample
   // summation order stays the reference's chunk order.
@@ -186,7 +189,7 @@ extern "C" int sesa_ola_accumulate_f32(const float* y, int n_chunks, int n_out_c
     for (int j = 0; j < n; ++j) seg_sum += (double)tab.seg[j];
     void* tok = profile_begin(as_stream(stream));
     hipLaunchKernelGGL(ola_accumulate_kernel, dim3(grid_for(hi - lo, 256)), dim3(256), 0, as_stream(stream),
-                       y + (int64_t)base * n_out_ch * chunk, n, n_out_ch, chunk, tab, lo, hi - lo, window, result,
+                       y ? y + (int64_t)base * n_out_ch * chunk : nullptr, n, n_out_ch, chunk, tab, lo, hi - lo, window, result,
                        counter, L_pad);
     SESA_CHECK_LAUNCH();
     // algorithmic bytes: y read once + result / counter span read and written once

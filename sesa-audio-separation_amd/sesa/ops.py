@@ -113,6 +113,15 @@ def ola_accumulate(y, starts, seg_lens, window, result, counter):
                 "sesa_ola_accumulate_f32")
 
 
+def ola_counter(chunk, starts, seg_lens, window, counter):
+    """The counter half of inference_pytorch.py:158 only (n_out_ch = 0), in place."""
+    counter = _dev_f32(counter, "sesa ola_counter")
+    with _on(counter):
+        N.check(N.lib().sesa_ola_accumulate_f32(None, len(starts), 0, chunk, N.i64_array(starts),
+                                                N.i64_array(seg_lens), window.data_ptr(), None, counter.data_ptr(),
+                                                counter.shape[-1], _stream(counter)), "sesa_ola_accumulate_f32")
+
+
 def ola_finalize(result, counter, border):
     """inference_pytorch.py:174-180 -> [n_out_ch, L_pad - 2*border]."""
     n_out_ch, L_pad = result.shape

@@ -1,14 +1,18 @@
 """Chunk-sharded multi-GPU separation of one track (one process per GPU, RCCL over xGMI).
 
 The reference has no distributed path (only a dead nn.DataParallel, inference.py:209-210).
-Chunks of the chunker/OLA (inference_pytorch.py:123-159) are independent given the mix, so:
+Chunks of the chunker/OLA are independent given the mix, so:
 
-* rank r takes the contiguous global chunk range [lo_r, hi_r) of the reference chunk plan and
-  runs gather -> forward -> windowed OLA into a LOCAL span buffer covering only the samples its
-  chunks touch ([start(lo_r), end(hi_r - 1)) of the padded track): result rows + a counter row;
+* rank r takes the contiguous global chunk range [lo_r, hi_r) of the reference chunk plan -- the
+  generic mode of inference_pytorch.py:85-163 (fades, border reflect pad) or the demucs mode of
+  utils.py:371-445 (C = samplerate * segment, no fades / pad, ``counter += 1``) -- and runs
+  gather -> forward -> windowed OLA into a LOCAL span buffer of result rows covering only the
+  samples its chunks touch ([start(lo_r), end(hi_r - 1)) of the padded track);
 * one ``all_gather_into_tensor`` of the fixed-size span buffers (RCCL, backend "nccl") -- the only
-  exchange; the seams (C - step samples between neighbours) are summed in rank order and
-  ``result / counter`` is finalised.
+  exchange; the seams (C - step samples between neighbours) are summed in rank order;
+* the counter is deterministic: every rank recomputes it for the whole plan with the same kernel
+  and chunk order as the single-GPU path (``sesa_ola_accumulate_f32`` with no result rows), so it
+  is bit-identical to it and is not exchanged; then ``result / counter`` is finalised.
 
 Summation order at the seams differs from the reference's sequential chunk order only by the
 grouping of fp32 additions (rank partial sums), ~1e-7 relative.
@@ -17,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from .config import prefer_target_instrument
-from .demix import chunk_plan
+from .demix import chunk_plan, demucs_chunk_plan
 
 
 def shard_ranges(n_chunks, world):
@@ -25,64 +29,105 @@ def shard_ranges(n_chunks, world):
     return [(min(r * per, n_chunks), min((r + 1) * per, n_chunks)) for r in range(world)]
 
 
-def shard_plan(config, L, world):
-    """Host-side plan: flat chunk list [(start, seg, no_fade_in, no_fade_out)], per-rank chunk ranges
-    and sample spans (padded coordinates)."""
-    C = int(config.audio.chunk_size)
-    padded, border, L_pad, batches, _ = chunk_plan(L, C, int(config.inference.num_overlap),
-                                                   int(config.inference.batch_size))
-    flat = [(s, n, ni_, no) for chunks, ni_, no in batches for (s, n) in chunks]
+def shard_plan(config, L, world, mode="generic"):
+    """Host-side plan: flat chunk list [(start, seg, no_fade_in, no_fade_out)] (padded coordinates),
+    per-rank chunk ranges and sample spans, chunk size C, padded length and border."""
+    if mode == "demucs":
+        C = int(config.training.samplerate * config.training.segment)
+        flat = [(s, n, False, False) for s, n in demucs_chunk_plan(L, C, int(config.inference.num_overlap))]
+        padded, border, L_pad = False, 0, L
+    else:
+        C = int(config.audio.chunk_size)
+        padded, border, L_pad, batches, _ = chunk_plan(L, C, int(config.inference.num_overlap),
+                                                       int(config.inference.batch_size))
+        flat = [(s, n, ni_, no) for chunks, ni_, no in batches for (s, n) in chunks]
     ranges = shard_ranges(len(flat), world)
     spans = []
     for lo, hi in ranges:
         spans.append((0, 0) if lo >= hi else (flat[lo][0], max(s + n for s, n, _, _ in flat[lo:hi])))
     span_max = max(1, max(e - s for s, e in spans))
-    return dict(padded=padded, border=border if padded else 0, L_pad=L_pad, flat=flat, ranges=ranges,
-                spans=spans, span_max=span_max)
+    return dict(mode=mode, chunk=C, padded=padded, border=border if padded else 0, L_pad=L_pad, flat=flat,
+                ranges=ranges, spans=spans, span_max=span_max)
+
+
+class _Windows:
+    """The plan's windows on the device: generic mode -> the batch's faded window
+    (inference_pytorch.py:151-155), demucs mode -> ones (utils.py:443-445)."""
+
+    def __init__(self, plan, device):
+        from .demix import _Windows as W
+        self.ones = torch.ones(plan["chunk"], device=device, dtype=torch.float32) if plan["mode"] == "demucs" else None
+        self.w = None if self.ones is not None else W(plan["chunk"], device)
+
+    def pick(self, no_in, no_out):
+        return self.ones if self.ones is not None else self.w.pick(no_in, no_out)
+
+
+def _runs(group):
+    """Consecutive runs of chunks sharing a window (== the reference's logical batches), in order."""
+    j = 0
+    while j < len(group):
+        k = j
+        while k < len(group) and group[k][2:] == group[j][2:]:
+            k += 1
+        yield j, k
+        j = k
 
 
 def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch):
-    """gather -> forward -> OLA of this rank's chunks into a [rows + 1, span_max] buffer (HIP)."""
+    """gather -> forward -> OLA of this rank's chunks into a [rows, span_max] result buffer (HIP)."""
     from . import ops
-    from .demix import _Windows
-    C = int(config.audio.chunk_size)
+    C = plan["chunk"]
     n_ch = mix_d.shape[0]
     device = mix_d.device
-    local = torch.zeros(rows + 1, plan["span_max"], device=device, dtype=torch.float32)
+    local = torch.zeros(rows, plan["span_max"], device=device, dtype=torch.float32)
+    scratch = torch.zeros(plan["span_max"], device=device, dtype=torch.float32)   # counter: recomputed later
     lo, hi = plan["ranges"][rank]
     s0 = plan["spans"][rank][0]
     flat = plan["flat"]
-    win = _Windows(C, device)
+    win = _Windows(plan, device)
     xbuf = None
     pos = lo
     while pos < hi:
         grp = flat[pos:min(hi, pos + exec_batch)]
         if xbuf is None or xbuf.shape[0] != len(grp):
             xbuf = torch.empty(len(grp), n_ch, C, device=device, dtype=torch.float32)
-        ops.chunk_gather(mix_d, plan["border"], [g[0] for g in grp], C, out=xbuf)
+        starts = [g[0] for g in grp]
+        if plan["mode"] == "demucs":
+            ops.chunk_gather_constant(mix_d, starts, C, out=xbuf)
+        else:
+            ops.chunk_gather(mix_d, plan["border"], starts, C, out=xbuf)
         y = model(xbuf).reshape(len(grp), rows, C)
-        j = 0
-        while j < len(grp):
-            k = j
-            while k < len(grp) and grp[k][2:] == grp[j][2:]:
-                k += 1
+        for j, k in _runs(grp):
             ops.ola_accumulate(y[j:k], [g[0] - s0 for g in grp[j:k]], [g[1] for g in grp[j:k]],
-                               win.pick(*grp[j][2:]), local[:rows], local[rows])
-            j = k
+                               win.pick(*grp[j][2:]), local, scratch)
         pos += len(grp)
     return local
 
 
+def counter_device(plan, device):
+    """The whole plan's counter (inference_pytorch.py:158 / utils.py:442,445), recomputed locally with
+    the single-GPU kernel and chunk order: bit-identical on every rank, never exchanged."""
+    from . import ops
+    counter = torch.zeros(plan["L_pad"], device=device, dtype=torch.float32)
+    win = _Windows(plan, device)
+    flat = plan["flat"]
+    for j, k in _runs(flat):
+        ops.ola_counter(plan["chunk"], [g[0] for g in flat[j:k]], [g[1] for g in flat[j:k]],
+                        win.pick(*flat[j][2:]), counter)
+    return counter
+
+
 def exchange_and_assemble(local, plan, rank, world, group=None):
-    """All-gather the span buffers and sum them into the full [rows + 1, L_pad] (result, counter)."""
-    rows1, span_max = local.shape
+    """All-gather the span buffers and sum them into the full [rows, L_pad] result."""
+    rows, span_max = local.shape
     if world > 1:
-        gathered = torch.empty(world * rows1, span_max, device=local.device, dtype=local.dtype)
+        gathered = torch.empty(world * rows, span_max, device=local.device, dtype=local.dtype)
         dist.all_gather_into_tensor(gathered, local.contiguous(), group=group)
-        gathered = gathered.view(world, rows1, span_max)
+        gathered = gathered.view(world, rows, span_max)
     else:
         gathered = local[None]
-    full = torch.zeros(rows1, plan["L_pad"], device=local.device, dtype=local.dtype)
+    full = torch.zeros(rows, plan["L_pad"], device=local.device, dtype=local.dtype)
     for r, (s, e) in enumerate(plan["spans"]):
         if e > s:
             full[:, s:e] += gathered[r, :, :e - s]
@@ -90,27 +135,30 @@ def exchange_and_assemble(local, plan, rank, world, group=None):
 
 
 def demix_sharded(config, model, mix_d, device=None, rank=None, world=None, exec_batch=8, group=None,
-                  local_fn=None, finalize_fn=None):
+                  local_fn=None, finalize_fn=None, counter_fn=None, mode="generic"):
     """Separate the device-resident mix [2, L] with chunks sharded across the process group.
-    Returns est [n_instr, 2, L] on every rank.  ``local_fn`` / ``finalize_fn`` exist so the CPU
-    test-suite can drive the sharding + collective + assembly with the oracle's OLA (gloo);
-    the product path uses the HIP ops."""
+    ``mode``: "generic" (inference_pytorch.demix_pytorch_optimized / utils.demix generic) or
+    "demucs" (utils.demix for model_type 'htdemucs').  Returns est [n_instr, 2, L] on every rank.
+    ``local_fn`` / ``counter_fn`` / ``finalize_fn`` exist so the CPU test-suite can drive the
+    sharding + collective + assembly with the oracle's OLA (gloo); the product path uses the HIP ops."""
     rank = dist.get_rank(group) if rank is None else rank
     world = dist.get_world_size(group) if world is None else world
-    ni = len(prefer_target_instrument(config))
+    instruments = list(config.training.instruments) if mode == "demucs" else prefer_target_instrument(config)
+    ni = len(instruments)
     n_ch, L = mix_d.shape
     rows = ni * n_ch
     if L == 0:
         return torch.zeros(ni, n_ch, 0, device=mix_d.device, dtype=torch.float32)
-    plan = shard_plan(config, L, world)
+    plan = shard_plan(config, L, world, mode)
     if local_fn is None:
         local = local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch)
     else:
         local = local_fn(config, model, mix_d, plan, rank, rows)
     full = exchange_and_assemble(local, plan, rank, world, group)
+    counter = counter_device(plan, mix_d.device) if counter_fn is None else counter_fn(plan)
     if finalize_fn is None:
         from . import ops
-        est = ops.ola_finalize(full[:rows].contiguous(), full[rows].contiguous(), plan["border"])
+        est = ops.ola_finalize(full.contiguous(), counter, plan["border"])
     else:
-        est = finalize_fn(full[:rows], full[rows], plan["border"])
+        est = finalize_fn(full, counter, plan["border"])
     return est.reshape(ni, n_ch, L)

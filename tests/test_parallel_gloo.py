@@ -32,27 +32,53 @@ def _mix():
     return (0.1 * rng.standard_normal((2, L_TRACK))).astype(np.float32)
 
 
-def cpu_local(config, model, mix, plan, rank, rows):
-    from oracle.demix import extract_chunk, windowing_array
-    C = int(config.audio.chunk_size)
+def _plan_windows(config, plan):
+    from oracle.demix import windowing_array
+    C = plan["chunk"]
     fade = C // 10
-    mixn = mix.numpy()
-    b = plan["border"]
-    mix_pad = np.pad(mixn, ((0, 0), (b, b)), mode="reflect") if b else mixn
-    local = np.zeros((rows + 1, plan["span_max"]), np.float32)
-    lo, hi = plan["ranges"][rank]
-    s0 = plan["spans"][rank][0]
     base = windowing_array(C, fade)
-    for (s, n, no_in, no_out) in plan["flat"][lo:hi]:
-        y = model(torch.from_numpy(extract_chunk(mix_pad, s, C))[None]).numpy().reshape(rows, C)
+
+    def win(no_in, no_out):
+        if plan["mode"] == "demucs":
+            return np.ones(C, np.float32)
         w = base.copy()
         if no_in:
             w[:fade] = 1
         elif no_out:
             w[-fade:] = 1
-        local[:rows, s - s0:s - s0 + n] += y[:, :n] * w[:n]
-        local[rows, s - s0:s - s0 + n] += w[:n]
+        return w
+    return win
+
+
+def cpu_local(config, model, mix, plan, rank, rows):
+    from oracle.demix import extract_chunk
+    C = plan["chunk"]
+    mixn = mix.numpy()
+    b = plan["border"]
+    mix_pad = np.pad(mixn, ((0, 0), (b, b)), mode="reflect") if b else mixn
+    local = np.zeros((rows, plan["span_max"]), np.float32)
+    lo, hi = plan["ranges"][rank]
+    s0 = plan["spans"][rank][0]
+    win = _plan_windows(config, plan)
+    for (s, n, no_in, no_out) in plan["flat"][lo:hi]:
+        if plan["mode"] == "demucs":
+            part = mixn[:, s:s + C]
+            x = np.pad(part, ((0, 0), (0, C - part.shape[1])))
+        else:
+            x = extract_chunk(mix_pad, s, C)
+        y = model(torch.from_numpy(x)[None]).numpy().reshape(rows, C)
+        local[:, s - s0:s - s0 + n] += y[:, :n] * win(no_in, no_out)[:n]
     return torch.from_numpy(local)
+
+
+def make_cpu_counter(config):
+    def counter_fn(plan):
+        win = _plan_windows(config, plan)
+        c = np.zeros(plan["L_pad"], np.float32)
+        for (s, n, no_in, no_out) in plan["flat"]:
+            c[s:s + n] += win(no_in, no_out)[:n]
+        return torch.from_numpy(c)
+    return counter_fn
 
 
 def cpu_finalize(result, counter, border):
@@ -64,14 +90,22 @@ def cpu_finalize(result, counter, border):
     return torch.from_numpy(np.ascontiguousarray(est))
 
 
-def _worker(rank, world, port, bs, q):
+def _demucs_cfg():
+    from sesa.config import wrap
+    return wrap({"training": {"samplerate": 1000, "segment": 40, "instruments": ["vocals", "other"]},
+                 "inference": {"num_overlap": 4, "batch_size": 2}})
+
+
+def _worker(rank, world, port, bs, q, mode="generic"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from sesa.parallel import demix_sharded
-        est = demix_sharded(_cfg(bs), StandIn(), torch.from_numpy(_mix()), rank=rank, world=world,
-                            local_fn=cpu_local, finalize_fn=cpu_finalize)
+        cfg = _demucs_cfg() if mode == "demucs" else _cfg(bs)
+        est = demix_sharded(cfg, StandIn(), torch.from_numpy(_mix()), rank=rank, world=world,
+                            local_fn=cpu_local, finalize_fn=cpu_finalize, counter_fn=make_cpu_counter(cfg),
+                            mode=mode)
         if rank == 0:
             q.put(est.numpy())
     finally:
@@ -101,11 +135,31 @@ def test_chunk_shard_matches_single_process(world, bs):
     assert np.abs(est - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max())
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_demucs_mode_shard_matches_single_process(world):
+    """utils.demix demucs mode (model_type 'htdemucs', utils.py:371-445) sharded over gloo ranks vs the
+    single-process oracle restatement (pinned to the reference by tests/test_demucs_mode.py)."""
+    from oracle.demix import demix_demucs_mode
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    pc = mp.start_processes(_worker, args=(world, port, 1, q, "demucs"), nprocs=world, join=False,
+                            start_method="spawn")
+    est = q.get()
+    while not pc.join(timeout=120):
+        pass
+    cfg = _demucs_cfg()
+    ref = demix_demucs_mode(cfg, StandIn(), _mix())
+    ref = np.stack([ref["vocals"], ref["other"]])
+    assert est.shape == ref.shape
+    assert np.abs(est - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max())
+
+
 def test_shard_plan_covers_every_chunk_once():
     from sesa.parallel import shard_plan
     c = _cfg(1)
     for world in (1, 2, 3, 8):
-        p = shard_plan(c, L_TRACK, world)
+        p = shard_plan(c, L_TRACK, world) if world % 2 else shard_plan(_demucs_cfg(), L_TRACK, world, "demucs")
         covered = [i for lo, hi in p["ranges"] for i in range(lo, hi)]
         assert covered == list(range(len(p["flat"])))
         for (lo, hi), (s, e) in zip(p["ranges"], p["spans"]):
