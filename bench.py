@@ -68,9 +68,9 @@ WORKLOAD = {"ensemble": "ensemble.py flow: mdx23c vocals + bs_roformer vocals + 
             "htdemucs": "demucs4ht htdemucs musdb18 config (channels 48, depth 4, bottom 512, 5 cross-transformer "
                         "layers, 4 sources), utils.demix demucs mode (segment 11 s, overlap 4)"}
 TRACK_SECONDS = {"htdemucs": 1800.0}
-# chunks per forward: at most this many, balanced so a rank's last forward is not a small remainder
-# (169 chunks at N=1 -> 3 forwards of 57; 22 per rank at N=8 -> one forward of 22)
-EXEC_BATCH = {"ensemble": 0, "mdx23c": 64, "bs_roformer": 4, "scnet": 48, "htdemucs": 32}
+# chunks per forward: sesa.demix.plan_exec_batch (the CLI's planner): the model's cap, balanced so a
+# rank's last forward is not a small remainder (169 chunks at N=1 -> 3 forwards of 57; 22 per rank at
+# N=8 -> one forward of 22)
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
 KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)",
          "tokgemm": "tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)",
@@ -233,11 +233,13 @@ def main():
     chunks = [n_chunks_of(cfg, md) for (_, cfg, _), md in zip(members, modes)]
     n_chunks = sum(chunks)
 
-    def balanced(cap, total):
-        local = -(-total // world)
-        return max(1, -(-local // max(1, -(-local // cap))))
+    from sesa.demix import plan_exec_batch
 
-    batches = [args.exec_batch or balanced(EXEC_BATCH[nm], c) for nm, c in zip(names, chunks)]
+    def chunk_len(cfg, mode):
+        return int(cfg.training.samplerate * cfg.training.segment) if mode == "demucs" else int(cfg.audio.chunk_size)
+
+    batches = [args.exec_batch or plan_exec_batch(m, c, chunk_len(cfg, md), dev, world=world)
+               for (m, cfg, _), c, md in zip(members, chunks, modes)]
     path_flop = sum(c * MODELS[nm][1] for c, nm in zip(chunks, names))
     stems_host = None
 

@@ -255,6 +255,19 @@ int sesa_blend_f32(const float* x, int n_files, int n_ch, int64_t L, int64_t buf
                    void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * FLAC codec (HOST memory; the CLI's audio I/O: inference_pytorch.py:213 librosa.load of FLAC
+ * inputs, :262-272 sf.write(<name>_<instr>.flac, subtype=PCM_16 / PCM_24)).  Decoded samples are
+ * scaled like libsndfile's float read (int / 2^(bits-1)); the encoder quantises like libsndfile's
+ * float write (x * (2^(bits-1) - 1), round half to even), clipped to the bit depth.
+ *   out / in: interleaved float [frames][channels]
+ */
+int sesa_flac_info(const uint8_t* data, size_t n, int* channels, int* sample_rate, int* bits, int64_t* frames);
+int sesa_flac_decode(const uint8_t* data, size_t n, float* out, int64_t max_frames, int64_t* frames_out);
+size_t sesa_flac_encode_bound(int64_t frames, int channels, int bits);
+int sesa_flac_encode(const float* in, int64_t frames, int channels, int sample_rate, int bits, uint8_t* out,
+                     size_t cap, size_t* written);
+
+/* ---------------------------------------------------------------------------------------
  * Kernel timing (measurement support for bench.py; not part of the reference surface).
  * While enabled, every launch issued by libsesa is bracketed by a hipEvent pair on its own
  * stream and tagged with its kernel class and ALGORITHMIC work (reference FLOPs for the

@@ -96,6 +96,11 @@ SIGNATURES = {
     "sesa_blend_workspace_size": (c_size_t, [c_int, c_int64]),
     "sesa_blend_f32": (c_int, [P_f32, c_int, c_int, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                c_void_p]),
+    "sesa_flac_info": (c_int, [c_void_p, c_size_t, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                               ctypes.POINTER(c_int64)]),
+    "sesa_flac_decode": (c_int, [c_void_p, c_size_t, c_void_p, c_int64, ctypes.POINTER(c_int64)]),
+    "sesa_flac_encode_bound": (c_size_t, [c_int64, c_int, c_int]),
+    "sesa_flac_encode": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_size_t, ctypes.POINTER(c_size_t)]),
     "sesa_profile_enable": (c_int, [c_int]),
     "sesa_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
                                   ctypes.POINTER(ctypes.c_double)]),

@@ -1,12 +1,18 @@
-"""Self-contained WAV reader/writer (librosa/soundfile are not available offline).
+"""Self-contained audio reader/writer (librosa/soundfile are not available offline).
 
 * ``read_audio(path, sr=44100)`` -- stands in for ``librosa.load(path, sr=44100, mono=False)``
-  (inference_pytorch.py:213): float32 [channels, samples] scaled like soundfile (PCM / 2^(bits-1)),
-  resampled with scipy's polyphase filter when the file rate differs (librosa's default soxr
-  filter differs in the last bits; documented divergence).
-* ``write_audio(path, data[samples, channels], sr, subtype)`` -- ``sf.write`` for WAV with subtype
-  FLOAT / PCM_16 / PCM_24 (inference_pytorch.py:262-272; ensemble.py:311 uses PCM_24).
+  (inference_pytorch.py:213) for WAV (PCM 8/16/24/32, float 32/64) and FLAC (libsesa's FLAC decoder,
+  csrc/sesa_flac.cpp): float32 [channels, samples] scaled like soundfile (int / 2^(bits-1)),
+  resampled with scipy's polyphase filter when the file rate differs (librosa's default soxr filter
+  differs in the last bits; documented divergence).  Other containers (mp3, ogg, m4a, aac) have no
+  offline decoder here and raise.
+* ``write_audio(path, data[samples, channels], sr, subtype)`` -- ``sf.write``: ``.flac`` paths are
+  FLAC (PCM_16 / PCM_24), anything else WAV (FLOAT / PCM_16 / PCM_24) (inference_pytorch.py:262-272;
+  ensemble.py:311 uses PCM_24).  float -> PCM as libsndfile's write path: ``lrintf(x * (2^(bits-1)
+  - 1))`` in float32 without clipping for WAV (out-of-range samples wrap exactly as libsndfile's
+  non-clipping conversion does); FLAC clips (libFLAC cannot store wider values).
 """
+import ctypes
 import struct
 from fractions import Fraction
 
@@ -56,8 +62,38 @@ def read_wav(path):
     return x.reshape(n, ch).T.copy(), sr
 
 
+def _lib():
+    from . import _native as N
+    return N
+
+
+def read_flac(path):
+    N = _lib()
+    with open(path, "rb") as f:
+        data = f.read()
+    buf = ctypes.create_string_buffer(data, len(data))
+    ch, sr, bits, frames = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+    N.check(N.lib().sesa_flac_info(buf, len(data), ctypes.byref(ch), ctypes.byref(sr), ctypes.byref(bits),
+                                   ctypes.byref(frames)), f"FLAC {path}")
+    out = np.zeros((frames.value, ch.value), np.float32)
+    got = ctypes.c_int64()
+    N.check(N.lib().sesa_flac_decode(buf, len(data), out.ctypes.data, frames.value, ctypes.byref(got)),
+            f"FLAC {path}")
+    return out[:got.value].T.copy(), sr.value
+
+
+def read_any(path):
+    with open(path, "rb") as f:
+        magic = f.read(4)
+    if magic == b"fLaC":
+        return read_flac(path)
+    if magic == b"RIFF":
+        return read_wav(path)
+    raise ValueError(f"{path}: unsupported container (WAV and FLAC only offline; no mp3/ogg/m4a decoder)")
+
+
 def read_audio(path, sr=44100):
-    x, file_sr = read_wav(path)
+    x, file_sr = read_any(path)
     if sr is not None and file_sr != sr:
         from scipy.signal import resample_poly
         fr = Fraction(sr, file_sr).limit_denominator(1000)
@@ -66,8 +102,38 @@ def read_audio(path, sr=44100):
     return x, file_sr
 
 
+def quantize_pcm(data, bits, clip=False):
+    """libsndfile float -> PCM (pcm.c f2s / f2let, normalisation on): lrintf(x * (2^(bits-1) - 1)) in
+    float32, round half to even; without clipping the integer wraps like the C cast."""
+    scale = np.float32(2 ** (bits - 1) - 1)
+    v = np.rint(np.asarray(data, np.float32) * scale).astype(np.int64)
+    if clip:
+        return np.clip(v, -(1 << (bits - 1)), (1 << (bits - 1)) - 1)
+    m = 1 << bits
+    return ((v + (m >> 1)) % m) - (m >> 1)
+
+
+def write_flac(path, data, sr, subtype):
+    N = _lib()
+    bits = {"PCM_16": 16, "PCM_24": 24}.get(subtype)
+    if bits is None:
+        raise ValueError(f"FLAC supports PCM_16 / PCM_24, not {subtype}")
+    x = np.ascontiguousarray(np.asarray(data, np.float32))
+    if x.ndim == 1:
+        x = x[:, None]
+    n, ch = x.shape
+    cap = N.lib().sesa_flac_encode_bound(n, ch, bits)
+    out = ctypes.create_string_buffer(cap)
+    w = ctypes.c_size_t()
+    N.check(N.lib().sesa_flac_encode(x.ctypes.data, n, ch, int(sr), bits, out, cap, ctypes.byref(w)), "FLAC encode")
+    with open(path, "wb") as f:
+        f.write(out.raw[:w.value])
+
+
 def write_audio(path, data, sr, subtype="FLOAT"):
-    """data: [samples, channels] (soundfile orientation)."""
+    """data: [samples, channels] (soundfile orientation); ``.flac`` -> FLAC, else WAV."""
+    if str(path).lower().endswith(".flac"):
+        return write_flac(path, data, sr, subtype)
     data = np.asarray(data)
     if data.ndim == 1:
         data = data[:, None]
@@ -75,10 +141,9 @@ def write_audio(path, data, sr, subtype="FLOAT"):
     if subtype == "FLOAT":
         tag, bits, payload = _FLOAT, 32, data.astype("<f4").tobytes()
     elif subtype == "PCM_16":
-        v = np.clip(np.round(data * 32768.0), -32768, 32767).astype("<i2")
-        tag, bits, payload = _PCM, 16, v.tobytes()
+        tag, bits, payload = _PCM, 16, quantize_pcm(data, 16).astype("<i2").tobytes()
     elif subtype == "PCM_24":
-        v = np.clip(np.round(data * 8388608.0), -8388608, 8388607).astype(np.int32).reshape(-1)
+        v = quantize_pcm(data, 24).astype(np.int64).reshape(-1)
         b = np.stack([v & 0xFF, (v >> 8) & 0xFF, (v >> 16) & 0xFF], -1).astype(np.uint8)
         tag, bits, payload = _PCM, 24, b.tobytes()
     else:

@@ -22,7 +22,7 @@ from ._native import SesaError
 class HipBackend:
     """PyTorchBackend-compatible callable: ``backend(x[B,2,C]) -> model(x)``."""
 
-    def __init__(self, device="cuda:0", optimize_mode="channels_last", exec_batch=8):
+    def __init__(self, device="cuda:0", optimize_mode="channels_last", exec_batch=None):
         if isinstance(device, torch.device):
             device = str(device)
         if not str(device).startswith("cuda"):
@@ -57,9 +57,10 @@ PyTorchBackend = HipBackend
 
 
 def create_inference_session(model, device="cuda:0", optimize_mode="default", enable_amp=False, enable_tf32=True,
-                             enable_cudnn_benchmark=True, exec_batch=8):
+                             enable_cudnn_benchmark=True, exec_batch=None):
     """pytorch_backend.create_inference_session (:492-536).  NOTE: the default of ``enable_amp``
-    is False here (parity precision); the reference CLI also passes False unless --enable_amp."""
+    is False here (parity precision); the reference CLI also passes False unless --enable_amp.
+    ``exec_batch`` None: planned per track (sesa.demix.plan_exec_batch)."""
     be = HipBackend(device=device, optimize_mode=optimize_mode, exec_batch=exec_batch)
     be.optimize_model(model, use_amp=enable_amp)
     return be

@@ -28,6 +28,10 @@ def windowing_array(chunk_size, fade_size):
     return w
 
 
+def flat_plan(batches):
+    return [c for chunks, _, _ in batches for c in chunks]
+
+
 def chunk_plan(L, chunk_size, num_overlap, batch_size):
     """Loop control of inference_pytorch.py:115-163.  Returns (padded, border, L_pad, batches,
     progress) with batches = [(chunks[(start, seg_len)], no_fade_in, no_fade_out)] and progress =
@@ -52,6 +56,27 @@ def chunk_plan(L, chunk_size, num_overlap, batch_size):
             progress.append((idx, pct))
         idx += 1
     return padded, border, L_pad, batches, progress
+
+
+# Chunks per native forward, per model class (measured on MI355X, profiles/r01_bench_*): larger
+# batches amortise per-launch tails until the workspace or the gain runs out.
+EXEC_CAP = {"TFC_TDF_net": 64, "BSRoformer": 4, "MelBandRoformer": 4, "SCNet": 48, "HTDemucs": 32}
+
+
+def plan_exec_batch(model, n_chunks, chunk, device=None, world=1, cap=None):
+    """Execution batch for ``n_chunks`` chunks of length ``chunk`` spread over ``world`` ranks: the
+    model's cap (EXEC_CAP), halved while its workspace would exceed half the free HBM, then balanced
+    so a rank's last forward is not a small remainder (169 chunks at cap 64 -> 3 forwards of 57)."""
+    cap = int(cap or EXEC_CAP.get(type(model).__name__, 8))
+    if hasattr(model, "workspace_bytes") and torch.cuda.is_available():
+        try:
+            free, _ = torch.cuda.mem_get_info(device)
+            while cap > 1 and model.workspace_bytes(cap, chunk) > 0.5 * free:
+                cap //= 2
+        except Exception:  # noqa: BLE001 -- planning only; the forward itself reports real errors
+            pass
+    local = -(-max(1, n_chunks) // max(1, world))
+    return max(1, -(-local // max(1, -(-local // cap))))
 
 
 class _Windows:
@@ -95,7 +120,8 @@ def demix_device(config, model, mix, device, exec_batch=None, progress=True, chu
             return (torch.zeros(ni * n_ch, 0, device=device), torch.zeros(0, device=device), (False, 0, 0))
         return torch.zeros(ni, n_ch, 0, device=device, dtype=torch.float32)
     padded, border, L_pad, batches, prog = chunk_plan(L, C, ov, bs)
-    E = exec_batch or getattr(model, "exec_batch", None) or 8
+    E = exec_batch or getattr(model, "exec_batch", None) or plan_exec_batch(model, len(flat_plan(batches)), C,
+                                                                            device)
     win = _Windows(C, device)
     result = torch.zeros(ni * n_ch, L_pad, device=device, dtype=torch.float32)
     counter = torch.zeros(L_pad, device=device, dtype=torch.float32)
@@ -160,7 +186,7 @@ def demix_device_demucs(config, model, mix, device, exec_batch=None):
     if L == 0:
         return torch.zeros(ni, n_ch, 0, device=device, dtype=torch.float32)
     plan = demucs_chunk_plan(L, C, ov)
-    E = exec_batch or getattr(model, "exec_batch", None) or 8
+    E = exec_batch or getattr(model, "exec_batch", None) or plan_exec_batch(model, len(plan), C, device)
     ones = torch.ones(C, device=device, dtype=torch.float32)
     result = torch.zeros(ni * n_ch, L, device=device, dtype=torch.float32)
     counter = torch.zeros(L, device=device, dtype=torch.float32)

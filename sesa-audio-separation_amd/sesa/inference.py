@@ -8,8 +8,8 @@ Same flags (inference.py:159-181, inference_pytorch.py:281-303), same per-file f
 Differences (all deliberate, all loud):
 * the device is a HIP GPU; ``--force_cpu`` is rejected (there is no CPU path);
 * checkpoints load with ``torch.load(weights_only=True)`` only;
-* audio I/O is the self-contained WAV codec in sesa/audio_io.py: FLAC is not available offline, so
-  ``--flac_file`` writes WAV with the requested PCM subtype and says so;
+* audio I/O is sesa/audio_io.py: WAV and FLAC (libsesa's FLAC codec); mp3 / ogg / m4a inputs have
+  no offline decoder and are skipped with the reference's "cannot read track" message;
 * ``--lora_checkpoint`` is accepted and ignored (LoRA is not on the inference path).
 
 Run:  python -m sesa.inference --model_type mdx23c --config_path C.yaml --start_check_point W.ckpt \
@@ -31,6 +31,13 @@ def shorten_filename(filename, max_length=30):
     if len(base) <= max_length:
         return filename
     return base[:15] + "..." + base[-10:] + ext
+
+
+def get_soundfile_subtype(pcm_type, is_float=False):
+    """inference_pytorch.get_soundfile_subtype (:43-52)."""
+    if is_float:
+        return "FLOAT"
+    return {"PCM_16": "PCM_16", "PCM_24": "PCM_24", "FLOAT": "FLOAT"}.get(pcm_type, "FLOAT")
 
 
 def build_parser():
@@ -59,7 +66,8 @@ def build_parser():
     p.add_argument("--lora_checkpoint", type=str, default="")
     p.add_argument("--use_tta", action="store_true")
     p.add_argument("--demud_phaseremix_inst", action="store_true")
-    p.add_argument("--exec_batch", type=int, default=8, help="chunks per native forward (MI355X only)")
+    p.add_argument("--exec_batch", type=int, default=0,
+                   help="chunks per native forward (MI355X only; 0 = planned from the model and free HBM)")
     return p
 
 
@@ -118,13 +126,10 @@ def run_folder(backend, model, args, config, device):
             est = wav[instr]
             if norm is not None:
                 est = denormalize_audio(est, norm)
-            is_float = getattr(args, "export_format", "").startswith("wav FLOAT")
-            if args.flac_file:
-                subtype = "FLOAT" if is_float else args.pcm_type
-                print("FLAC encoder not available offline: writing WAV", subtype)
-            else:
-                subtype = "FLOAT"
-            out = os.path.join(args.store_dir, f"{shorten_filename(os.path.basename(path))}_{instr}.wav")
+            is_float = getattr(args, "export_format", "").startswith("wav FLOAT")   # :262-272
+            codec = "flac" if getattr(args, "flac_file", False) else "wav"
+            subtype = get_soundfile_subtype(args.pcm_type if codec == "flac" else "FLOAT", is_float)
+            out = os.path.join(args.store_dir, f"{shorten_filename(os.path.basename(path))}_{instr}.{codec}")
             write_audio(out, est.T, sr, subtype=subtype)
     print(f"Elapsed time: {time.time() - start:.2f} sec")
 
@@ -155,7 +160,7 @@ def proc_folder(argv=None):
     backend = create_inference_session(model, device=device, optimize_mode=args.optimize_mode,
                                        enable_amp=args.enable_amp, enable_tf32=args.enable_tf32,
                                        enable_cudnn_benchmark=args.enable_cudnn_benchmark,
-                                       exec_batch=args.exec_batch)
+                                       exec_batch=args.exec_batch or None)
     print(f"Model load time: {time.time() - t0:.2f} sec")
     run_folder(backend, model, args, config, device)
     return 0

@@ -9,13 +9,12 @@ frequencies shared by several bands are averaged (:596-606).  Everything else --
 band split, rotary transformers with output RMSNorm, (depth+1)-layer mask MLPs, scatter-average,
 complex mask, iSTFT -- runs in libsesa (sesa_bsroformer.hip).
 """
-import collections
-
 import numpy as np
 import torch
 
 from .. import _native as N
-from .bs_roformer import BSRoformer, _freqs
+from .bs_roformer import BSRoformer
+from .native import NativeModule
 
 
 def _hz_to_mel(f):
@@ -71,38 +70,28 @@ class MelBandRoformer(BSRoformer):
                  multi_stft_resolutions_window_sizes=(4096, 2048, 1024, 512, 256), multi_stft_hop_size=147,
                  multi_stft_normalized=False, multi_stft_window_fn=None, match_input_audio_length=False,
                  mlp_expansion_factor=4, use_torch_checkpoint=False, skip_connection=False, precision="bf16x3"):
+        NativeModule.__init__(self, precision)
         if linear_transformer_depth or skip_connection or stft_normalized or stft_window_fn is not None:
             raise N.SesaError("MelBandRoformer: linear attention, skip connections, normalized or custom STFT "
                               "windows have no native implementation")
         fpb, idx = mel_bands(sample_rate, stft_n_fft, num_bands, stereo)
         self._freq_indices = idx
-        self.freq_indices = torch.tensor(idx)
         self.match_input_audio_length = match_input_audio_length
         self.stereo = bool(stereo)
         self.audio_channels = 2 if stereo else 1
         self.num_stems = int(num_stems)
         self.freqs_per_bands = fpb
         self.chunk_size = None
-        self.precision = precision
         self._kw = dict(audio_channels=self.audio_channels, n_fft=int(stft_n_fft), hop_length=int(stft_hop_length),
                         win_length=int(stft_win_length), dim=int(dim), depth=int(depth), heads=int(heads),
                         dim_head=int(dim_head), time_transformer_depth=int(time_transformer_depth),
                         freq_transformer_depth=int(freq_transformer_depth), num_stems=self.num_stems,
                         mask_estimator_depth=int(mask_estimator_depth),
                         mlp_expansion_factor=int(mlp_expansion_factor))
-        self._params = collections.OrderedDict((n, torch.zeros(s, dtype=torch.float32))
-                                               for n, s in self.param_shapes())
-        for n, t in self._params.items():
-            if n.endswith("rotary_embed.freqs"):
-                t.copy_(torch.from_numpy(_freqs(dim_head)))
-            elif n.endswith("gamma"):
-                t.fill_(1.0)
-        self._handles, self._ws, self._ws_bytes = {}, {}, {}
-        self._hchunk = None
-        self._dirty = True
-        self.training = False
+        self._register_params(self._shapes(), self._init_value)
+        self.register_buffer("freq_indices", torch.tensor(idx), persistent=False)
 
-    def param_shapes(self):
+    def _shapes(self):
         k = self._kw
         dim, heads, dh = k["dim"], k["heads"], k["dim_head"]
         inner, ff, hid = heads * dh, dim * 4, dim * k["mlp_expansion_factor"]

@@ -141,6 +141,9 @@ class NativeModule(torch.nn.Module):
         ws = self.workspace(x.device, h, B)
         N.check(self._fn("forward")(h, x.data_ptr(), B, out.data_ptr(), ws.data_ptr(), ws.numel(),
                                     torch.cuda.current_stream(x.device).cuda_stream), f"sesa_{self._prefix}_forward")
+        return self._post(out)
+
+    def _post(self, out):
         return out
 
     def __del__(self):

@@ -17,6 +17,8 @@ Fixtures:
   demix_small_*.npz       inference_pytorch.demix_pytorch_optimized on the reduced model
   mdx23c_full_chunk.npz   (--full) one 261120-sample chunk through the full vocals config
   ensemble.npz            ensemble.AudioEnsembleEngine.process_waveform/process_spectral
+  demix_full_10s.npz      (--only demix_full) BASELINE configs[0]: demix_pytorch_optimized, full vocals
+                          config, 10 s mix, 13 chunks
 """
 import argparse
 import io
@@ -152,6 +154,27 @@ def gen_demix():
              vocals=res["vocals"], other=res["other"], progress=np.array(prog))
 
 
+@torch.inference_mode()
+def gen_demix_full():
+    """BASELINE configs[0]: the REAL demix_pytorch_optimized on the full MDX23C vocals config, 10 s of
+    44.1 kHz stereo (seed 0, 441000 samples -> 13 chunks at overlap 4), inference.batch_size 1,
+    unit-affine weights (as mdx23c_full_chunk.npz).  ~75 s of CPU."""
+    import inference_pytorch as ip
+    from pytorch_backend import PyTorchBackend
+    cfg = load_cfg("config_vocals_mdx23c.yaml")
+    model, _ = build_ref_model(cfg, "unit")
+    be = PyTorchBackend(device="cpu", optimize_mode="default")
+    be.compiled_model = model
+    be.model = model
+    be.use_amp = False
+    c = to_attr(json.loads(json.dumps(cfg)))
+    mix = mix_signal(0, 441000)
+    with contextlib.redirect_stdout(io.StringIO()) as out:
+        res = ip.demix_pytorch_optimized(c, be, mix, "cpu")
+    prog = [ln for ln in out.getvalue().splitlines() if ln.startswith("[SESA_PROGRESS]")]
+    save("demix_full_10s.npz", mix=mix, vocals=res["vocals"], other=res["other"], progress=np.array(prog))
+
+
 def gen_ensemble():
     import ensemble as ens
     eng = ens.AudioEnsembleEngine()
@@ -196,6 +219,8 @@ def main():
         gen_demix()
     if "ensemble" in todo:
         gen_ensemble()
+    if "demix_full" in todo:
+        gen_demix_full()
     if args.full or "full" in todo:
         gen_forward("config_vocals_mdx23c.yaml", "mdx23c_full_chunk.npz", 1, 0, "unit")
 

@@ -192,3 +192,42 @@ def test_demix_edge_lengths_vs_oracle(dev, L):
     assert est.shape == (2, 2, L)
     np.testing.assert_array_equal(est[0], ref["vocals"])
     np.testing.assert_array_equal(est[1], ref["other"])
+
+
+def test_config0_demix_10s_full_model_matches_reference(dev, golden):
+    """BASELINE configs[0] end to end: the REAL reference demix_pytorch_optimized (full MDX23C vocals
+    config, 10 s seed-0 mix, 13 chunks, batch_size 1; tests/golden/make_golden.py --only demix_full)
+    against sesa.demix.demix_pytorch_optimized on the device: RMS <= 1e-4, identical progress lines."""
+    from sesa.backend import create_inference_session
+    from sesa.demix import demix_pytorch_optimized
+    g = golden("demix_full_10s.npz")
+    m, c = _model("config_vocals_mdx23c.yaml", "unit")
+    be = create_inference_session(m, device="cuda:0")
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        out = demix_pytorch_optimized(c, be, g["mix"], "cuda:0")
+    prog = [ln for ln in buf.getvalue().splitlines() if ln.startswith("[SESA_PROGRESS]")]
+    assert prog == list(g["progress"])
+    for k in ("vocals", "other"):
+        err = rms(out[k], g[k])
+        print(f"configs[0] 10 s {k}: rms {err:.3e} (ref rms {rms(g[k], 0):.3e})")
+        assert out[k].shape == g[k].shape == (2, 441000) and err <= RMS_GATE
+
+
+def test_full_size_4min_properties(dev):
+    """configs[1] at full size (4-min track, full vocals config, 169 chunks): the sharded path at world 1
+    equals demix_device bit-for-bit, the stems are finite and shaped [2, 2, L], and the two stems
+    are not degenerate (size-independent properties; the oracle would need ~17 min of CPU)."""
+    from sesa.demix import demix_device
+    from sesa.parallel import demix_sharded
+    m, c = _model("config_vocals_mdx23c.yaml", "unit")
+    L = 240 * 44100
+    rng = np.random.default_rng(0)
+    mix = torch.from_numpy((0.1 * rng.standard_normal((2, L))).astype(np.float32)).to(dev)
+    with contextlib.redirect_stdout(io.StringIO()):
+        a = demix_device(c, m, mix, dev)
+    b = demix_sharded(c, m, mix, dev, rank=0, world=1, exec_batch=57)
+    assert a.shape == b.shape == (2, 2, L)
+    assert torch.isfinite(a).all().item()
+    assert torch.equal(a, b)
+    assert float(a[0].std()) > 1e-4 and float((a[0] - a[1]).abs().max()) > 1e-4
