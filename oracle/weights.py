@@ -6,7 +6,8 @@ from U(-1/sqrt(fan_in), +1/sqrt(fan_in)) with fan_in = prod(shape[1:]) (torch's
 ``_calculate_fan_in_and_fan_out`` convention, the bound of torch's default
 init).  Norm affine weights are 1 and biases 0 -- or, with
 ``affine="random"``, gamma ~ U(0.5, 1.5) and beta ~ U(-0.2, 0.2) so that tests
-exercise the affine path.
+exercise the affine path; ``affine="stress"``: beta ~ U(2, 4), so every normalised channel has
+|mean| >> std downstream (InstanceNorm statistics precision).
 """
 import zlib
 
@@ -30,8 +31,10 @@ def synth_param(name: str, shape, affine: str = "unit") -> np.ndarray:
     if name.endswith("bias"):
         if affine == "random":
             return rng.uniform(-0.2, 0.2, size=shape).astype(np.float32)
+        if affine == "stress":
+            return rng.uniform(2.0, 4.0, size=shape).astype(np.float32)
         return np.zeros(shape, np.float32)
-    if affine == "random":
+    if affine in ("random", "stress"):
         return rng.uniform(0.5, 1.5, size=shape).astype(np.float32)
     return np.ones(shape, np.float32)
 

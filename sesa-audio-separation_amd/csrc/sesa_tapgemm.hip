@@ -362,9 +362,11 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
   }
 
   // ---- epilogue ----
-  float ssum[NI], ssq[NI];
+  // InstanceNorm statistics in fp64 from the first add on: E[x^2] - E[x]^2 is formed in double at the
+  // consumer, so channels whose |mean| >> std (large norm beta, DC offsets) keep their precision
+  double ssum[NI], ssq[NI];
 #pragma unroll
-  for (int j = 0; j < NI; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
+  for (int j = 0; j < NI; ++j) { ssum[j] = 0.0; ssq[j] = 0.0; }
   const int C_out = a.out.C_out;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -395,15 +397,15 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
         if (a.out.residual) v += a.out.residual[idx];
         if (a.out.gelu) v = gelu_erf(v);
         a.out.ptr[idx] = v;
-        ssum[j] += v;
-        ssq[j] += v * v;
+        ssum[j] += (double)v;
+        ssq[j] = fma((double)v, (double)v, ssq[j]);
       }
     }
   }
   if (a.out.stats) {
     // reduce over the two lane halves, then over the WM waves sharing these columns (LDS)
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+    double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2]
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       ssum[j] += __shfl_xor(ssum[j], 32);
@@ -416,7 +418,7 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
     }
     __syncthreads();
     for (int n = tid; n < BN; n += kThreads) {
-      float s0 = 0.f, s1 = 0.f;
+      double s0 = 0.0, s1 = 0.0;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
         s0 += red[(w * BN + n) * 2 + 0];
@@ -426,8 +428,8 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
       const int co = UPS ? ncol % C_out : ncol;
       if ((UPS ? ncol < a.n_cols : co < C_out)) {
         double* st = a.out.stats + ((int64_t)b * C_out + co) * 2;
-        atomicAdd(st + 0, (double)s0);
-        atomicAdd(st + 1, (double)s1);
+        atomicAdd(st + 0, s0);
+        atomicAdd(st + 1, s1);
       }
     }
   }
@@ -673,9 +675,11 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   }
 
   // ---- epilogue: fp32 store + per-channel sum / sum-of-squares for the next InstanceNorm ----
-  float ssum[NI], ssq[NI];
+  // InstanceNorm statistics in fp64 from the first add on: E[x^2] - E[x]^2 is formed in double at the
+  // consumer, so channels whose |mean| >> std (large norm beta, DC offsets) keep their precision
+  double ssum[NI], ssq[NI];
 #pragma unroll
-  for (int j = 0; j < NI; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
+  for (int j = 0; j < NI; ++j) { ssum[j] = 0.0; ssq[j] = 0.0; }
   const int C_out = a.out.C_out;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -691,13 +695,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
         const int64_t idx = (((int64_t)b * a.T_out + t) * a.F_out + f) * C_out + co;
         const float v = acc[i][j][r];
         a.out.ptr[idx] = v;
-        ssum[j] += v;
-        ssq[j] += v * v;
+        ssum[j] += (double)v;
+        ssq[j] = fma((double)v, (double)v, ssq[j]);
       }
     }
   }
   if (a.out.stats) {
-    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2] (the last barrier retired all LDS reads)
+    double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2] (the last barrier retired all LDS reads)
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       ssum[j] += __shfl_xor(ssum[j], 32);
@@ -710,7 +714,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     }
     __syncthreads();
     for (int n = tid; n < BN; n += NT) {
-      float s0 = 0.f, s1 = 0.f;
+      double s0 = 0.0, s1 = 0.0;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
         s0 += red[(w * BN + n) * 2 + 0];
@@ -719,8 +723,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       const int co = nb * BN + n;
       if (co < C_out) {
         double* st = a.out.stats + ((int64_t)b * C_out + co) * 2;
-        atomicAdd(st + 0, (double)s0);
-        atomicAdd(st + 1, (double)s1);
+        atomicAdd(st + 0, s0);
+        atomicAdd(st + 1, s1);
       }
     }
   }
@@ -754,7 +758,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
   constexpr int EPI_BYTES = EPI_ROWS * BN * 4;
   constexpr int MAIN_BYTES = 2 * AW_BYTES + 2 * B_BYTES;
   constexpr int SM_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[SM_BYTES + 3 * BN * 4 + 2 * NT * 4 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[SM_BYTES + 3 * BN * 4];
   char* Whi = smem;
   char* Wlo = smem + AW_BYTES;
   char* Bhi = smem + 2 * AW_BYTES;
@@ -762,7 +766,6 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
   float* csc = reinterpret_cast<float*>(smem + SM_BYTES);  // per-column affine
   float* csh = csc + BN;
   int* cvalid = reinterpret_cast<int*>(csh + BN);
-  float* red = reinterpret_cast<float*>(cvalid + BN);      // [2][NT][4] column partial sums
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -917,19 +920,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
 
   // ---- epilogue ----
   // Each thread ends up owning column partial sums for 4 consecutive columns (cs4 = tid % 32).
-  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+  double ssum[4] = {0.0, 0.0, 0.0, 0.0}, ssq[4] = {0.0, 0.0, 0.0, 0.0};   // fp64 norm statistics
   const int cs4 = (tid % (BN / 4)) * 4;
   if (U_OUT) {
     // tiled U: for each register, lanes 0-31 / 32-63 store two full 128-B rows (32 consecutive n)
     const int mchunks = (a.M + 31) >> 5;
     float* ublk = a.out.ptr + (((n0 >> 7) * mchunks) << 12);
-    float* red2 = reinterpret_cast<float*>(smem);  // [WM][BN][2] (main-loop LDS is dead)
+    double* red2 = reinterpret_cast<double*>(smem);  // [WM][BN][2] (main-loop LDS is dead)
+    static_assert(WM * BN * 2 * 8 <= SM_BYTES, "fp64 reduction fits the dead main-loop LDS");
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int jl = (wn * NI + j) * 32 + l32;
       const bool nok = n0 + jl < n_total;
-      float s0 = 0.f, s1 = 0.f;
+      double s0 = 0.0, s1 = 0.0;
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -938,8 +942,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
           if (!nok || m >= a.M) continue;
           const float v = acc[i][j][r];
           ublk[((m >> 5) << 12) + (m & 31) * 128 + jl] = v;
-          s0 += v;
-          s1 += v * v;
+          s0 += (double)v;
+          s1 = fma((double)v, (double)v, s1);
         }
       s0 += __shfl_xor(s0, 32);
       s1 += __shfl_xor(s1, 32);
@@ -953,7 +957,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
       for (int jl = tid; jl < BN; jl += NT) {
         const int64_t n = n0 + jl;
         if (n >= n_total) continue;
-        float s0 = 0.f, s1 = 0.f;
+        double s0 = 0.0, s1 = 0.0;
 #pragma unroll
         for (int w = 0; w < WM; ++w) {
           s0 += red2[(w * BN + jl) * 2 + 0];
@@ -962,8 +966,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
         const int c = (int)(n % C);
         const int b = (int)(n / ((int64_t)a.T * C));
         double* st = a.out.stats + ((int64_t)b * C + c) * 2;
-        atomicAdd(st + 0, (double)s0);
-        atomicAdd(st + 1, (double)s1);
+        atomicAdd(st + 0, s0);
+        atomicAdd(st + 1, s1);
       }
     }
     return;
@@ -1016,31 +1020,37 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
       *reinterpret_cast<f32x4*>(a.out.ptr + (bt * a.M + m) * C + c) = v;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        ssum[q] += v[q];
-        ssq[q] += v[q] * v[q];
+        ssum[q] += (double)v[q];
+        ssq[q] = fma((double)v[q], (double)v[q], ssq[q]);
       }
     }
   }
   if (a.out.stats) {
-    // threads tid, tid + 32, ... own the same 4 columns: reduce through LDS
-    f32x4* r4 = reinterpret_cast<f32x4*>(red);
-    r4[tid] = f32x4{ssum[0], ssum[1], ssum[2], ssum[3]};
-    r4[NT + tid] = f32x4{ssq[0], ssq[1], ssq[2], ssq[3]};
+    // threads tid, tid + 32, ... own the same 4 columns: reduce through LDS in fp64 (the stage
+    // region, dead once every thread has passed the barrier below)
+    static_assert(2 * NT * 4 * 8 <= SM_BYTES, "fp64 reduction fits the stage region");
+    double* r8 = reinterpret_cast<double*>(smem);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      r8[q * NT + tid] = ssum[q];
+      r8[(4 + q) * NT + tid] = ssq[q];
+    }
     __syncthreads();
     if (tid < BN / 4 && col_ok) {
-      f32x4 s0 = r4[tid], s1 = r4[NT + tid];
-      for (int t = tid + BN / 4; t < NT; t += BN / 4) {
-        s0 += r4[t];
-        s1 += r4[NT + t];
-      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int t = tid; t < NT; t += BN / 4) {
+          s0 += r8[q * NT + t];
+          s1 += r8[(4 + q) * NT + t];
+        }
         const int64_t n = ncol + q;
         const int cq = (int)(n % C);
         const int b = (int)(n / ((int64_t)a.T * C));
         double* st = a.out.stats + ((int64_t)b * C + cq) * 2;
-        atomicAdd(st + 0, (double)s0[q]);
-        atomicAdd(st + 1, (double)s1[q]);
+        atomicAdd(st + 0, s0);
+        atomicAdd(st + 1, s1);
       }
     }
   }

@@ -155,6 +155,18 @@ def gen_demix():
 
 
 @torch.inference_mode()
+def gen_stress():
+    """InstanceNorm precision stress: reduced MDX23C, norm beta ~ U(2, 4) (every
+    normalised channel far from zero mean downstream) and a mix with a DC offset of 0.4."""
+    cfg = load_cfg("config_mdx23c_small.yaml")
+    model, _ = build_ref_model(cfg, "stress")
+    C = cfg["audio"]["chunk_size"]
+    x = np.stack([mix_signal(51 + b, C) + np.float32(0.4) for b in range(2)]).astype(np.float32)
+    y = model(torch.from_numpy(x)).numpy()
+    save("mdx23c_small_stress.npz", x=x, y=y, affine=np.array("stress"))
+
+
+@torch.inference_mode()
 def gen_demix_full():
     """BASELINE configs[0]: the REAL demix_pytorch_optimized on the full MDX23C vocals config, 10 s of
     44.1 kHz stereo (seed 0, 441000 samples -> 13 chunks at overlap 4), inference.batch_size 1,
@@ -219,6 +231,8 @@ def main():
         gen_demix()
     if "ensemble" in todo:
         gen_ensemble()
+    if "stress" in todo:
+        gen_stress()
     if "demix_full" in todo:
         gen_demix_full()
     if args.full or "full" in todo:

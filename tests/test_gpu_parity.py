@@ -231,3 +231,15 @@ def test_full_size_4min_properties(dev):
     assert torch.isfinite(a).all().item()
     assert torch.equal(a, b)
     assert float(a[0].std()) > 1e-4 and float((a[0] - a[1]).abs().max()) > 1e-4
+
+
+def test_instancenorm_stress_large_offsets(dev, golden):
+    """InstanceNorm with |mean| >> std (norm beta ~ U(2, 4), DC-offset input; reference golden
+    tests/golden/mdx23c_small_stress.npz): the conv / TDF epilogues accumulate the statistics in
+    fp64, so E[x^2] - E[x]^2 keeps its precision (mdx23c_tfc_tdf_v3.py:47-59)."""
+    g = golden("mdx23c_small_stress.npz")
+    m, _ = _model("config_mdx23c_small.yaml", "stress")
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"IN stress: rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    assert err <= RMS_GATE

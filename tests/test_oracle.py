@@ -40,7 +40,8 @@ def test_stft_istft(golden):
 
 
 @pytest.mark.parametrize("fixture,cfg_name", [("mdx23c_small.npz", "config_mdx23c_small.yaml"),
-                                              ("mdx23c_small_vocals.npz", "config_mdx23c_small_vocals.yaml")])
+                                              ("mdx23c_small_vocals.npz", "config_mdx23c_small_vocals.yaml"),
+                                              ("mdx23c_small_stress.npz", "config_mdx23c_small.yaml")])
 def test_forward_small(golden, fixture, cfg_name):
     g = golden(fixture)
     c = cfg(cfg_name)
