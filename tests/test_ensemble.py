@@ -74,7 +74,7 @@ def test_device_buffer_loop_matches_oracle(L, method):
 
 @pytest.mark.gpu
 def test_run_ensemble_writes_pcm24(tmp_path, capsys):
-    from sesa.audio_io import read_wav, write_audio
+    from sesa.audio_io import quantize_pcm, read_wav, write_audio
     from sesa.ensemble import main
     rng = np.random.default_rng(5)
     files = []
@@ -90,5 +90,7 @@ def test_run_ensemble_writes_pcm24(tmp_path, capsys):
     ins = np.stack([read_wav(f)[0][:, :50000] for f in files]).astype(np.float64)
     exp = oe.blend(ins, "max_fft")
     assert sr == 44100 and y.shape == (2, 50000)
-    assert np.abs(y - exp).max() <= 1.0 / 8388608 + 1e-9     # one PCM_24 step
+    # soundfile's PCM_24 write (libsndfile: lrintf(x * 0x7FFFFF)) read back as int / 2^23
+    exp_q = quantize_pcm(exp.astype(np.float32), 24) / 8388608.0
+    assert np.abs(y - exp_q).max() <= 1.0 / 8388608 + 1e-9     # at most one PCM_24 step (rounding ties)
     assert main(["--files", files[0], "--type", "avg_wave", "--output", str(out)]) == 1   # < 2 files
