@@ -8,7 +8,17 @@ from collections import defaultdict
 
 def main(*dirs):
     acc = defaultdict(lambda: defaultdict(list))
+    import sqlite3
     for d in dirs:
+        for db in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):   # rocpd SQLite output
+            per, names = defaultdict(dict), {}
+            for did, name, cn, v in sqlite3.connect(db).execute(
+                    "select dispatch_id, kernel_name, counter_name, value from counters_collection"):
+                per[did][cn] = per[did].get(cn, 0.0) + float(v)
+                names[did] = name[:90]
+            for did, cs in per.items():
+                for c, v in cs.items():
+                    acc[names[did]][c].append(v)
         for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             per = defaultdict(dict)
             names = {}

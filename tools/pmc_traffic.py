@@ -16,10 +16,24 @@ import sys
 from collections import defaultdict
 
 
+def read_counter_db(path, counter):
+    import sqlite3
+    con = sqlite3.connect(path)
+    per, names = defaultdict(float), {}
+    for did, name, val in con.execute("select dispatch_id, kernel_name, value from counters_collection "
+                                      "where counter_name = ?", (counter,)):
+        per[did] += float(val)
+        names[did] = name
+    return per, names
+
+
 def read_counter(d, counter):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
-        raise SystemExit(f"no counter_collection.csv under {d}")
+        dbs = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)
+        if dbs:   # rocprofv3 >= 7: rocpd SQLite output
+            return read_counter_db(dbs[0], counter)
+        raise SystemExit(f"no counter_collection.csv / .db under {d}")
     per = defaultdict(float)   # dispatch id -> value
     names = {}
     for fn in files:
