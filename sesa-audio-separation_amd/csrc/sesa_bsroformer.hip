@@ -604,7 +604,7 @@ extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
 namespace {
 
 struct Plan {
-  size_t spec, xg, x, qkv, ao, h, h2, mask, maskg, frames, total;
+  size_t spec, xg, x, xp, rsc, qkv, ao, h, h2, mask, maskg, frames, total;
 };
 
 Plan plan(const sesa_bsr* m, int B) {
@@ -615,6 +615,8 @@ Plan plan(const sesa_bsr* m, int B) {
   p.spec = off; off += al((size_t)B * m->T * m->feat);
   p.xg = off; off += m->cfg.mel ? al((size_t)B * m->T * m->gfeat) : 0;
   p.x = off; off += al((size_t)tok * m->cfg.dim);
+  p.xp = off; off += al((size_t)tok * m->cfg.dim);  // X as bf16 hi / lo planes (2 x 2 B per element)
+  p.rsc = off; off += al((size_t)tok);               // RMSNorm row scales of X
   p.qkv = off; off += al((size_t)tok * m->qkv_ld);
   p.ao = off; off += al((size_t)tok * m->inner);
   p.h = off; off += al((size_t)tok * std::max(m->ff, m->hidden));
@@ -638,6 +640,7 @@ TokGemmArgs gemm_args(const sesa_bsr* m, const Gemm& gm, const float* x, int64_t
   a.groups = gm.d_groups;
   a.n_groups = (int)gm.groups.size();
   a.n_tiles_n = gm.n_tiles_n;
+  a.k8 = gm.k8;
   a.M = M;
   a.act = TOK_ACT_NONE;
   a.dim_head = m->cfg.dim_head;
@@ -714,11 +717,35 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
     a.rownorm = 1;
     gemm(a, m->band, B * T);
   }
+  // Transformer GEMM operands as bf16 planes, split once per producer (not once per N tile):
+  // X -> XP (tok_split, + RMSNorm row scales), attention -> AO planes, FF1 epilogue -> H planes.
+  uint16_t* XPhi = reinterpret_cast<uint16_t*>(ws + pl.xp);
+  uint16_t* XPlo = x3 ? XPhi + Mtok * dim : nullptr;
+  float* RSC = reinterpret_cast<float*>(ws + pl.rsc);
+  uint16_t* AOhi = reinterpret_cast<uint16_t*>(AO);
+  uint16_t* AOlo = x3 ? AOhi + Mtok * m->inner : nullptr;
+  uint16_t* Hhi = reinterpret_cast<uint16_t*>(H);
+  uint16_t* Hlo = x3 ? Hhi + Mtok * m->ff : nullptr;
+  auto split_x = [&]() {
+    if (rc) return;
+    void* t0 = profile_begin(st);
+    rc = launch_tok_split(X, dim, Mtok, dim, XPhi, XPlo, dim, RSC, st);
+    profile_end(t0, st, SESA_KCLASS_ACT, (double)Mtok * dim * (x3 ? 8.0 : 6.0) + 4.0 * Mtok);
+  };
+  auto pre = [&](TokGemmArgs& a, const uint16_t* hi, const uint16_t* lo, int64_t ld) {
+    a.x = nullptr;
+    a.a_hi = hi;
+    a.a_lo = lo;
+    a.a_ld = ld;
+    a.row_scale = RSC;
+  };
   for (size_t li = 0; li < m->layers.size(); ++li) {
     const Layer& L = m->layers[li];
     // attention: QKV + gates (RMSNorm, rotary on q/k)
+    split_x();
     {
       TokGemmArgs a = gemm_args(m, L.qkv, X, dim, QKV, m->qkv_ld, M);
+      pre(a, XPhi, XPlo, dim);
       a.rownorm = 1;
       a.rope = m->d_rope + L.rope_off;
       a.rope_cols = 2 * m->inner;
@@ -736,6 +763,8 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
       a.v_off = 2 * m->inner;
       a.g_off = 3 * m->inner;
       a.out = AO;
+      a.out_hi = AOhi;
+      a.out_lo = AOlo;
       a.o_ld = m->inner;
       a.heads = c.heads;
       if (L.time) {  // sequences (b, band) over t
@@ -759,17 +788,23 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
     }
     {
       TokGemmArgs a = gemm_args(m, L.out, AO, m->inner, X, dim, M);
+      pre(a, AOhi, AOlo, m->inner);
       a.residual = X;
       gemm(a, L.out, M);
     }
+    split_x();
     {
       TokGemmArgs a = gemm_args(m, L.ff1, X, dim, H, m->ff, M);
+      pre(a, XPhi, XPlo, dim);
       a.rownorm = 1;
       a.act = TOK_ACT_GELU;
+      a.out_hi = Hhi;
+      a.out_lo = Hlo;
       gemm(a, L.ff1, M);
     }
     {
       TokGemmArgs a = gemm_args(m, L.ff2, H, m->ff, X, dim, M);
+      pre(a, Hhi, Hlo, m->ff);
       a.residual = X;
       gemm(a, L.ff2, M);
     }

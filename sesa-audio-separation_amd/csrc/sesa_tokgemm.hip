@@ -5,9 +5,12 @@
 //   (:97-99, one GEMM, rotary applied to q/k in the epilogue, :111-113), to_out (:101-104, +
 //   residual :214), FeedForward (:55-74, GELU / + residual :215), MaskEstimator MLPs (:277-310,
 //   grouped, Tanh and GLU in the epilogues).  RMSNorm (:43-50) is fused: gamma is folded into W at
-//   pack time and the row scale sqrt(K)/max(||x||, 1e-12) is computed from the staged A values.
-//   Workgroup tile 256 tokens x 256 columns, 8 waves of 64x128 (2x4 blocks of 32x32), K chunks of
-//   32 staged fp32 -> bf16 hi/lo in double-buffered LDS; weights arrive pre-split and pre-swizzled.
+//   pack time and the row scale sqrt(K)/max(||x||, 1e-12) is applied in the epilogue.
+//   Two staging paths: (a) fp32 A rows split to bf16 hi/lo per K chunk in registers and stored to
+//   LDS (band split, mask MLPs, implicit-GEMM conv of HTDemucs, SCNet); (b) A pre-split once into
+//   bf16 planes by its producer (tok_split / split epilogues) and copied to LDS by LDS-DMA
+//   (tok_gemm_glds_kernel: the transformer Linear layers).  Weights arrive pre-split and
+//   pre-swizzled; tiles are ordered XCD-major so the N tiles of an M tile share one L2.
 //   Precision bf16x3 (hi*hi + hi*lo + lo*hi, fp32 accumulate) or bf16 (one pass).
 // attn_kernel -- softmax(Q K^T / sqrt(64)) V per (sequence, head) (attend.py:76-95, SDPA), the
 //   flash formulation with S^T = K Q^T so every query owns one lane column: row max / sum are
@@ -52,15 +55,26 @@ __device__ __forceinline__ uint32_t pack2(__bf16 a, __bf16 b) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
+// XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (each with its own
+// L2), so block b runs on XCD b % 8.  Tile t = (XCD, b / 8) packed XCD-major keeps consecutive tiles
+// -- the N tiles of one M tile, which share the A rows -- on one XCD's L2 instead of fetching the A
+// rows once per XCD.
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
+  return x * q + min(x, r) + i;
+}
+
 // ---------------------------------------------------------------------------------------------
-// 512 threads (8 waves: 4 along M x 2 along N, 64x128 each), tile 256 tokens x 256 columns, LDS
-// double-buffered (2 x 64 KB) with ONE barrier per 32-wide K chunk (48 MFMAs per wave per barrier): iteration k runs the MFMAs of
-// stage k&1, writes chunk k+1 (already in registers) to the other stage and issues the global loads
-// of chunk k+2.  The body is straight-line (clamped addresses, validity applied at store time).
-template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB, bool CONV>
+// Register-staged kernel.  NT threads, tile BM tokens x 128 columns, waves of (32 MI) x (32 NI).
+// DB = false (default, 256 threads, 2 WG / CU): single LDS stage, two barriers per 32-wide K chunk,
+// the next chunk's global loads in flight under the MFMAs.  DB = true (512 threads, 1 WG / CU):
+// two stages, one barrier per chunk.  The body is straight-line (clamped addresses, validity
+// applied at store time).
+template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB, bool CONV, bool PRE>
 __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a) {
   constexpr int BN = kTokBN, BK = kTokBK;
   static_assert((NT / 64) == (BM / (32 * MI)) * WN && BN == WN * NI * 32, "tile");
+  static_assert(!(PRE && CONV), "pre-split A is for token rows");
   constexpr int ROWB = BK * 2;                 // 64 B per image row (32 bf16)
   constexpr int A_BYTES = BM * ROWB;
   constexpr int W_BYTES = BN * ROWB;
@@ -70,8 +84,9 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
   __shared__ int orow_base[CONV ? BM : 1], orow_i1[CONV ? BM : 1];  // transposed-conv output rows
 
   const TokGroup g = a.groups[blockIdx.y];
-  const int n_tile = blockIdx.x % a.n_tiles_n;
-  const int m_tile = blockIdx.x / a.n_tiles_n;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int n_tile = tile % a.n_tiles_n;
+  const int m_tile = tile / a.n_tiles_n;
   const int n0 = n_tile * BN;
   if (n0 >= g.N) return;                       // this group has fewer column tiles
   const int m0 = m_tile * BM;
@@ -96,8 +111,10 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
   const int arow0 = tid >> 3, akq = (tid & 7) * 4;
   f32x4 areg[AI];
   f32x4 a2reg[CONV ? AI : 1];
+  uint2 ahreg[PRE ? AI : 1], alreg[PRE && X3 ? AI : 1];  // pre-split quads (4 bf16 each)
   float ss[AI];
   const float* xrow[AI];
+  int64_t prow[PRE ? AI : 1];                             // plane element offset of the row
   bool rok[AI];
   // CONV: per-row input grid origin (b Q1, i1 s1, i2 s2) and per-chunk validity
   int rb1[CONV ? AI : 1], ri1[CONV ? AI : 1], ri2[CONV ? AI : 1];
@@ -107,7 +124,8 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
     ss[i] = 0.f;
     const int m = m0 + arow0 + RS * i;
     rok[i] = m < a.M;
-    xrow[i] = a.x + (int64_t)(rok[i] ? m : a.M - 1) * a.x_ld + g.x_off;
+    if constexpr (PRE) prow[i] = (int64_t)(rok[i] ? m : a.M - 1) * a.a_ld + g.x_off;
+    else xrow[i] = a.x + (int64_t)(rok[i] ? m : a.M - 1) * a.x_ld + g.x_off;
     if constexpr (CONV) {
       const int mm = rok[i] ? m : 0;
       const int i2 = mm % a.geo.P2, t = mm / a.geo.P2;
@@ -145,6 +163,12 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
         areg[i] = *reinterpret_cast<const f32x4*>(a.x + off);
         if (a.geo.x2) a2reg[i] = *reinterpret_cast<const f32x4*>(a.geo.x2 + off);
       }
+    } else if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        ahreg[i] = *reinterpret_cast<const uint2*>(a.a_hi + prow[i] + kc_);
+        if constexpr (X3) alreg[i] = *reinterpret_cast<const uint2*>(a.a_lo + prow[i] + kc_);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < AI; ++i) areg[i] = *reinterpret_cast<const f32x4*>(xrow[i] + kc_);
@@ -159,6 +183,17 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
       const int e = min(tid + I * NT, W16 - 1);  // duplicates write identical values
       d4[e] = wreg[I];
     });
+    if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int row = arow0 + RS * i;
+        const bool ok = rok[i] && kok;
+        const int off = row * ROWB + ((((akq >> 3) ^ ((row >> 2) & 3))) << 4) + ((akq & 4) << 1);
+        *reinterpret_cast<uint2*>(Ahi + off) = ok ? ahreg[i] : make_uint2(0u, 0u);
+        if (X3) *reinterpret_cast<uint2*>(Alo + off) = ok ? alreg[i] : make_uint2(0u, 0u);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int row = arow0 + RS * i;
@@ -240,7 +275,10 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
   }
 
   // ---- RMSNorm row scales: 8 threads share a row ----
-  if (a.rownorm) {
+  if (PRE && a.rownorm) {
+    for (int r = tid; r < BM; r += NT) rs[r] = a.row_scale[min(m0 + r, a.M - 1)];
+    __syncthreads();
+  } else if (a.rownorm) {
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       float v = ss[i];
@@ -322,15 +360,309 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
       }
       if (n_ok && !(a.glu && (n & 1))) {
         const int nc = a.glu ? n >> 1 : ncol;
+        if (a.out_hi) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          bool ok;
-          const int64_t m = orow(r, ok);
-          if (ok) a.out[m * a.o_ld + g.o_off + nc] = v[r];
+          for (int r = 0; r < 16; ++r) {
+            bool ok;
+            const int64_t m = orow(r, ok);
+            __bf16 hi, lo;
+            split_bf16(v[r], hi, lo);
+            if (ok) {
+              a.out_hi[m * a.o_ld + g.o_off + nc] = __builtin_bit_cast(uint16_t, hi);
+              if (a.out_lo) a.out_lo[m * a.o_ld + g.o_off + nc] = __builtin_bit_cast(uint16_t, lo);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            bool ok;
+            const int64_t m = orow(r, ok);
+            if (ok) a.out[m * a.o_ld + g.o_off + nc] = v[r];
+          }
         }
       }
     });
   });
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pre-split A, LDS-DMA staging, big tile (bf16x3).  512 threads (8 waves: 2 along M x 4 along N,
+// 128 x 64 each = 4 x 2 blocks of 32x32), tile 256 tokens x 256 columns (two packed 128-column
+// weight tiles), K chunks of 32 in two 64 KiB LDS stages filled by global_load_lds_dwordx4 (1 KiB per
+// wave-instruction, lane-linear destination; the A image's 16-B XOR swizzle goes on the per-lane
+// SOURCE address, so fragment reads match tok_gemm_kernel's).  Per chunk and wave: 48 MFMAs on 12
+// fragment reads per k-step (0.5 ds_read_b128 per MFMA vs 0.67 for 64x64 wave tiles); chunk kc + 1's
+// DMA is issued at the top of iteration kc and retired by one counted wait + raw barrier at its end.
+// All LDS in one array (a second __shared__ object can make hipcc wait vmcnt(0) before the fragment
+// reads).
+// The epilogue is specialised at compile time (EP flags) and has a guard-free body for full tiles:
+// with runtime mode flags and per-element row / column guards it compiled to ~1.4k branches and
+// cost more than the main loop.  Operands a 32x32 block would gather with a load -> wait round trip
+// each are staged once into the freed LDS by LDS-DMA: the rotary (cos, sin) rows of the tile's tokens
+// (64 KiB), the residual in two 128-row halves (128 KiB each).
+enum : int { EP_RS = 1, EP_ROPE = 2, EP_GELU = 4, EP_RES = 8, EP_SPLIT = 16, EP_RAW = 32, EP_NONE = 64 };
+
+__device__ __forceinline__ float dpp_xor1(float x) {  // lane ^ 1 (quad_perm [1, 0, 3, 2])
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t dpp_xor1u(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
+}
+
+// EP: EP_RS (row scale) | EP_ROPE (rotary, dim_head 64) | EP_GELU | EP_RES (residual) | EP_SPLIT
+// (bf16 planes out); bias always (per group).  EP_RAW / EP_NONE: ablations for tools/tokgemm_bench.hip.
+template <int EP>
+__global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
+  constexpr int NT = 512, BM = 256, BK = kTokBK, MI = 4, NI = 2, WN = 4;
+  constexpr int ROWB = BK * 2;
+  constexpr int A_BYTES = BM * ROWB;                       // 16 KiB per plane
+  constexpr int A_REG = 2 * A_BYTES;
+  constexpr int W_PLANE = kTokBN * ROWB;                   // 8 KiB: one packed 128-column image plane
+  constexpr int W_IMG = 2 * W_PLANE;
+  constexpr int STAGE = A_REG + 2 * W_IMG;                 // 64 KiB
+  constexpr int A_PIECES = A_REG / 1024, W_PIECES = 2 * W_IMG / 1024, W_HALF = W_IMG / 1024;
+  constexpr int PPW = (A_PIECES + W_PIECES) / (NT / 64);   // glds per wave per chunk (8)
+  constexpr int APW = A_PIECES / (NT / 64);                 // of which A pieces (4)
+  static_assert((A_PIECES + W_PIECES) % (NT / 64) == 0 && A_PIECES % (NT / 64) == 0, "piece split");
+  static_assert(2 * STAGE >= 128 * 1024, "epilogue staging reuses the two stages");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * BM * 4];
+  float* rs = reinterpret_cast<float*>(smem + 2 * STAGE);
+  int* rpos = reinterpret_cast<int*>(rs + BM);
+
+  const TokGroup g = a.groups[blockIdx.y];
+  const int n_tiles2 = (a.n_tiles_n + 1) >> 1;             // 256-column tiles
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int n_tile2 = tile % n_tiles2;
+  const int m_tile = tile / n_tiles2;
+  const int n0 = n_tile2 * 256;
+  if (n0 >= g.N) return;
+  const int m0 = m_tile * BM;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int n_chunks = (g.K + BK - 1) / BK;
+
+  for (int r = tid; r < BM; r += NT) {                      // ordinary loads, before any DMA is in flight
+    const int m = min(m0 + r, a.M - 1);
+    if (EP & EP_RS) rs[r] = a.row_scale[m];
+    if (EP & EP_ROPE) rpos[r] = a.pos_time ? (m / a.pos_F) % a.pos_T : m % a.pos_F;
+  }
+
+  // this lane's A pieces: piece p (per plane) covers tile rows 16 p .. 16 p + 15, 4 lanes a row
+  constexpr int AP1 = A_BYTES / 1024 / (NT / 64);           // pieces per plane per wave (2)
+  int64_t asrc[AP1];
+  int aslot8[AP1];
+#pragma unroll
+  for (int i = 0; i < AP1; ++i) {
+    const int row = 16 * (wave + 8 * i) + (lane >> 2);
+    asrc[i] = (int64_t)min(m0 + row, a.M - 1) * a.a_ld + g.x_off;
+    aslot8[i] = 8 * ((lane & 3) ^ ((row >> 2) & 3));
+  }
+  const int64_t wimg = W_IMG / 2;                           // uint16 per packed chunk image (hi + lo)
+  const uint16_t* wblk0 = a.w + g.w_off + (int64_t)(2 * n_tile2) * n_chunks * wimg;
+  // the second 128-column tile; past the group's last tile a harmless repeat (its columns are >= N)
+  const uint16_t* wblk1 = n0 + kTokBN < g.N ? wblk0 + (int64_t)n_chunks * wimg : wblk0;
+
+  auto issue = [&](int kc, char* stg) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      if (i < APW) {                                        // A: plane i / AP1, piece wave + 8 (i % AP1)
+        const int ii = i % AP1, plane = i / AP1;
+        const int k = kc * BK + aslot8[ii];
+        const int64_t off = asrc[ii] + (k < g.K ? k : 0);  // K % 8 == 0 (host check); W is zero past K
+        const uint16_t* src = (plane ? a.a_lo : a.a_hi) + off;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stg + plane * A_BYTES +
+                                                                                       (wave + 8 * ii) * 1024),
+                                         16, 0, 0);
+      } else {                                              // W piece q: image half q / W_HALF
+        const int q = wave + 8 * (i - APW);
+        const int half = q / W_HALF, qq = q - half * W_HALF;
+        const uint16_t* src = (half ? wblk1 : wblk0) + (int64_t)kc * wimg + qq * 512 + lane * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stg + A_REG + q * 1024), 16,
+                                         0, 0);
+      }
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  struct Frags {
+    bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
+  };
+  auto read_frags = [&](Frags& f, const char* stg, int ks) {
+    const int q = ks * 2 + h;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = (wm * MI + i) * 32 + l32;
+      const int off = row * ROWB + ((q ^ ((row >> 2) & 3)) << 4);
+      f.ah[i] = *reinterpret_cast<const bf16x8*>(stg + off);
+      f.al[i] = *reinterpret_cast<const bf16x8*>(stg + A_BYTES + off);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int c = (wn * NI + j) * 32 + l32;               // 0..255
+      const int r = c & (kTokBN - 1);
+      const int off = A_REG + (c >> 7) * W_IMG + r * ROWB + ((q ^ ((r >> 2) & 3)) << 4);
+      f.bh[j] = *reinterpret_cast<const bf16x8*>(stg + off);
+      f.bl[j] = *reinterpret_cast<const bf16x8*>(stg + off + W_PLANE);
+    }
+  };
+  auto mfmas = [&](const Frags& f) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        acc[i][j] = mfma32(f.al[i], f.bh[j], acc[i][j]);
+        acc[i][j] = mfma32(f.ah[i], f.bl[j], acc[i][j]);
+        acc[i][j] = mfma32(f.ah[i], f.bh[j], acc[i][j]);
+      }
+  };
+
+  __syncthreads();                                         // rs / rpos visible; no DMA in flight yet
+  issue(0, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int kc = 0; kc < n_chunks; ++kc) {
+    char* cur = smem + (kc & 1) * STAGE;
+    // chunk kc + 1 into the other stage: its last fragment reads (iteration kc - 1) were retired
+    // by the lgkmcnt(0) before that iteration's barrier
+    if (kc + 1 < n_chunks) issue(kc + 1, smem + ((kc + 1) & 1) * STAGE);
+    Frags f0, f1;
+    read_frags(f0, cur, 0);
+    read_frags(f1, cur, 1);
+    mfmas(f0);
+    mfmas(f1);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  if constexpr ((EP & EP_NONE) != 0) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+
+  // ---- epilogue ----
+  const float* lres = reinterpret_cast<const float*>(smem);
+  const float2* lrope = reinterpret_cast<const float2*>(smem);
+  if constexpr ((EP & EP_ROPE) != 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {                          // piece q: tile rows 4 q .. 4 q + 3 (256 B each)
+      const int q = wave + 8 * i;
+      const int row = 4 * q + (lane >> 4);
+      const float2* src = a.rope + (int64_t)rpos[row] * 32 + (lane & 15) * 2;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + q * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  const bool full = m0 + BM <= a.M && n0 + 256 <= g.N;
+  float bias[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = n0 + (wn * NI + j) * 32 + l32;
+    bias[j] = (g.b_off >= 0 && n < g.N) ? a.bias[g.b_off + n] : 0.f;
+  }
+  // one 32x32 block: FULL = no row / column guards
+  auto block = [&](auto I, auto J, auto P, auto FULLT) {
+    constexpr int i = decltype(I)::value, j = decltype(J)::value, p = decltype(P)::value;
+    constexpr bool FULL = decltype(FULLT)::value;
+    const int nl = (wn * NI + j) * 32 + l32;
+    const int n = n0 + nl;
+    f32x16 v = acc[i][j];
+    if constexpr ((EP & EP_RAW) == 0) {
+      const int d = n & 63;
+      const bool rot = n < a.rope_cols;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float x = v[r];
+        if constexpr ((EP & EP_RS) != 0) x *= rs[ml];
+        x += bias[j];
+        if constexpr ((EP & EP_GELU) != 0) x = gelu_erf(x);
+        if constexpr ((EP & EP_ROPE) != 0) {
+          const float partner = dpp_xor1(x);
+          const float2 cs = lrope[ml * 32 + (d >> 1)];
+          const float y = (d & 1) ? fmaf(x, cs.x, partner * cs.y) : fmaf(x, cs.x, -partner * cs.y);
+          x = rot ? y : x;
+        }
+        if constexpr ((EP & EP_RES) != 0) x += lres[(ml - p * 64 - wm * 64) * 256 + nl];
+        v[r] = x;
+      }
+    }
+    const int rb = m0 + (wm * MI + i) * 32 + 4 * h;
+    if constexpr ((EP & EP_SPLIT) != 0) {
+      // bf16 planes, two columns per 4-byte store: even lanes write the hi pair (n, n + 1), odd
+      // lanes the lo pair (n - 1, n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = rb + (r & 3) + 8 * (r >> 2);
+        __bf16 hi, lo;
+        split_bf16(v[r], hi, lo);
+        const uint32_t hb = __builtin_bit_cast(uint16_t, hi), lb = __builtin_bit_cast(uint16_t, lo);
+        const int64_t o = (int64_t)m * a.o_ld + g.o_off + n;
+        // both exchanges in uniform control flow (a DPP read of a lane masked off by a branch yields 0)
+        const uint32_t hn = dpp_xor1u(hb), ln = dpp_xor1u(lb);
+        if (FULL) {
+          const uint32_t pv = (l32 & 1) ? ln | (lb << 16) : hb | (hn << 16);
+          uint16_t* dst = (l32 & 1) ? a.out_lo + o - 1 : a.out_hi + o;
+          *reinterpret_cast<uint32_t*>(dst) = pv;
+        } else if (m < a.M && n < g.N) {
+          a.out_hi[o] = (uint16_t)hb;
+          a.out_lo[o] = (uint16_t)lb;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = rb + (r & 3) + 8 * (r >> 2);
+        if (FULL || (m < a.M && n < g.N)) a.out[(int64_t)m * a.o_ld + g.o_off + n] = v[r];
+      }
+    }
+  };
+  auto run = [&](auto FULLT) {
+    Unroll<0, 2>::run([&](auto P) {                        // row half p: blocks i = 2p, 2p + 1
+      constexpr int p = decltype(P)::value;
+      if constexpr ((EP & EP_RES) != 0) {
+        if (p == 1) {                                      // every wave is done with half 0
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {                     // local row rl <-> tile row (half p of each wm)
+          const int rl = wave + 8 * i;
+          const int row = rl < 64 ? p * 64 + rl : 128 + p * 64 + (rl - 64);
+          const int m = min(m0 + row, a.M - 1);
+          int col = n0 + lane * 4;
+          if (col + 4 > g.N) col = n0;                     // columns >= N are never used
+          const float* src = a.residual + (int64_t)m * a.o_ld + g.o_off + col;
+          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + rl * 1024), 16, 0,
+                                           0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      Unroll<2 * p, 2 * p + 2>::run([&](auto I) {
+        Unroll<0, NI>::run([&](auto J) { block(I, J, P, FULLT); });
+      });
+    });
+  };
+  if (full) run(std::true_type{});
+  else run(std::false_type{});
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -523,7 +855,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
   const int64_t tq = token(q_pos);
   const float gate = a.g_off >= 0 ? sigmoidf_(a.qkv[tq * a.ld + a.g_off + head]) : 1.f;
   const float scale = gate / l_run;
-  float* op = a.out + tq * a.o_ld + head * dh;
+  const int64_t obase = tq * a.o_ld + head * dh;
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -533,14 +865,53 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
       f32x4 v;
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = o[db][4 * g4 + q] * scale;
-      *reinterpret_cast<f32x4*>(op + d) = v;
+      if (a.out_hi) {
+        __bf16 hi[4], lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) split_bf16(v[q], hi[q], lo[q]);
+        *reinterpret_cast<uint2*>(a.out_hi + obase + d) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
+        if (a.out_lo)
+          *reinterpret_cast<uint2*>(a.out_lo + obase + d) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
+      } else {
+        *reinterpret_cast<f32x4*>(a.out + obase + d) = v;
+      }
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp32 rows -> bf16 hi / lo planes (+ RMSNorm row scale): one wave per row, f32x4 per lane-step.
+__global__ void __launch_bounds__(256) tok_split_kernel(const float* __restrict__ x, int64_t x_ld, int64_t M, int K,
+                                                        uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
+                                                        int64_t p_ld, float* __restrict__ row_scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const float* xr = x + m * x_ld;
+  float ss = 0.f;
+  for (int k = lane * 4; k < K; k += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + k);
+    __bf16 h[4], l[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ss = fmaf(v[q], v[q], ss);
+      split_bf16(v[q], h[q], l[q]);
+    }
+    *reinterpret_cast<uint2*>(hi + m * p_ld + k) = make_uint2(pack2(h[0], h[1]), pack2(h[2], h[3]));
+    if (lo) *reinterpret_cast<uint2*>(lo + m * p_ld + k) = make_uint2(pack2(l[0], l[1]), pack2(l[2], l[3]));
+  }
+  if (row_scale) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) ss += __shfl_xor(ss, s);
+    if (lane == 0) row_scale[m] = sqrtf((float)K) / fmaxf(sqrtf(ss), 1e-12f);
+  }
 }
 
 }  // namespace
 
 int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
   SESA_REQUIRE(a.n_groups >= 1 && a.n_tiles_n >= 1 && a.M >= 0, SESA_ERR_INVALID, "tok_gemm: bad grid");
+  SESA_REQUIRE(!(a.out_hi && a.residual) && (a.out_hi || a.out), SESA_ERR_INVALID,
+               "tok_gemm: split epilogue takes no residual; an output is required");
   if (a.M == 0) return SESA_OK;
   const int64_t m_tiles = (a.M + 127) / 128;
   SESA_REQUIRE(m_tiles * a.n_tiles_n < (1ll << 31) && a.n_groups < 65536, SESA_ERR_INVALID, "tok_gemm: grid too large");
@@ -554,24 +925,69 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
                      a.x_ld % 4 == 0 && c.P1 > 0 && c.P2 > 0 && c.Q1 > 0 && c.Q2 > 0 && c.phases >= 1 && !a.rope &&
                      !a.rownorm && (int64_t)c.P1 * c.P2 > 0 && (c.phases == 1 || !a.glu),
                  SESA_ERR_INVALID, "tok_gemm conv: bad geometry");
-    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true>), grid, dim3(256), 0, st, a);
+    SESA_REQUIRE(!a.a_hi, SESA_ERR_INVALID, "tok_gemm conv: pre-split A is for token rows");
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, true, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true, false>), grid, dim3(256), 0, st, a);
+  } else if (a.a_hi) {
+    SESA_REQUIRE(a.a_ld % 4 == 0 && (!x3 || a.a_lo) && (!a.rownorm || a.row_scale), SESA_ERR_INVALID,
+                 "tok_gemm: pre-split A needs a_ld %% 4 == 0, the lo plane for bf16x3, row_scale for rownorm");
+    // LDS-DMA kernel for the bf16x3 transformer Linears (every group's K % 8 == 0, epilogue one of
+    // the specialised forms); SESA_TOKGEMM_GLDS=0 selects the register-staged kernel for A/B runs
+    static const int glds = getenv("SESA_TOKGEMM_GLDS") ? atoi(getenv("SESA_TOKGEMM_GLDS")) : 1;
+    int ep = -1;
+    if (glds && x3 && a.k8 && a.a_ld % 8 == 0 && !a.glu && !a.conv && a.o_ld % 4 == 0 &&
+        (a.act == TOK_ACT_NONE || a.act == TOK_ACT_GELU) && (!a.rope || (a.dim_head == 64 && !a.residual)) &&
+        (!a.out_hi || a.out_lo)) {
+      ep = (a.rownorm ? EP_RS : 0) | (a.rope ? EP_ROPE : 0) | (a.act == TOK_ACT_GELU ? EP_GELU : 0) |
+           (a.residual ? EP_RES : 0) | (a.out_hi ? EP_SPLIT : 0);
+    }
+    const dim3 gbig((unsigned)(((a.M + 255) / 256) * ((a.n_tiles_n + 1) / 2)), (unsigned)a.n_groups);
+    switch (ep) {
+      case 0: hipLaunchKernelGGL(tok_gemm_glds_kernel<0>, gbig, dim3(512), 0, st, a); break;
+      case EP_RS | EP_ROPE: hipLaunchKernelGGL(tok_gemm_glds_kernel<EP_RS | EP_ROPE>, gbig, dim3(512), 0, st, a); break;
+      case EP_RES: hipLaunchKernelGGL(tok_gemm_glds_kernel<EP_RES>, gbig, dim3(512), 0, st, a); break;
+      case EP_RS | EP_GELU | EP_SPLIT:
+        hipLaunchKernelGGL(tok_gemm_glds_kernel<EP_RS | EP_GELU | EP_SPLIT>, gbig, dim3(512), 0, st, a);
+        break;
+      case EP_GELU | EP_SPLIT:
+        hipLaunchKernelGGL(tok_gemm_glds_kernel<EP_GELU | EP_SPLIT>, gbig, dim3(512), 0, st, a);
+        break;
+      default: ep = -1;
+    }
+    if (ep >= 0) {
+      SESA_CHECK_LAUNCH();
+      return SESA_OK;
+    }
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, false, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, false, true>), grid, dim3(256), 0, st, a);
   } else if (variant == 1) {
     const int64_t mt = (a.M + 255) / 256;
     dim3 g1((unsigned)(mt * a.n_tiles_n), (unsigned)a.n_groups);
-    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 512, 256, 2, 2, 2, true, false>), g1, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 2, true, false>), g1, dim3(512), 0, st, a);
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 512, 256, 2, 2, 2, true, false, false>), g1, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 2, true, false, false>), g1, dim3(512), 0, st, a);
   } else {
-    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, false>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, false>), grid, dim3(256), 0, st, a);
+    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, false, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, false, false>), grid, dim3(256), 0, st, a);
   }
+  SESA_CHECK_LAUNCH();
+  return SESA_OK;
+}
+
+int launch_tok_split(const float* x, int64_t x_ld, int64_t M, int K, uint16_t* hi, uint16_t* lo, int64_t p_ld,
+                     float* row_scale, hipStream_t st) {
+  SESA_REQUIRE(x && hi && M >= 0 && K > 0 && K % 4 == 0 && x_ld % 4 == 0 && p_ld % 4 == 0 && p_ld >= K &&
+                   (M + 3) / 4 < (1ll << 31),
+               SESA_ERR_INVALID, "tok_split: bad shape");
+  if (M == 0) return SESA_OK;
+  hipLaunchKernelGGL(tok_split_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, x, x_ld, M, K, hi, lo, p_ld,
+                     row_scale);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }
 
 int launch_attention(const AttnArgs& a, int x3, hipStream_t st) {
   SESA_REQUIRE(a.L >= 1 && a.n_seq >= 1 && a.heads >= 1 && a.sdiv >= 1 && a.Lk >= 0 && a.dh >= 0 && a.dh <= kHD &&
-                   a.dh % 4 == 0 && (!a.kv || a.kv_ld % 4 == 0),
+                   a.dh % 4 == 0 && (!a.kv || a.kv_ld % 4 == 0) && (!a.out_hi || a.o_ld % 4 == 0),
                SESA_ERR_INVALID, "attention: bad shape");
   SESA_REQUIRE(a.n_seq < 65536 * 4 && a.heads < 65536, SESA_ERR_INVALID, "attention: grid too large");
   dim3 grid((unsigned)((a.L + 127) / 128), (unsigned)a.heads, (unsigned)a.n_seq);

@@ -61,7 +61,26 @@ struct TokGemmArgs {
   int pos_F, pos_T, pos_time; // rotary position of row m: pos_time ? (m / pos_F) % pos_T : m % pos_F
   int conv;                   // 1: A rows / output rows addressed through `geo` (implicit-GEMM conv)
   ConvGeo geo;
+  // Pre-split A (not with conv): A[m, k] = a_hi + a_lo as bf16 planes [M][a_ld] (tok_split or a split
+  // epilogue wrote them once), so the kernel stages them without per-N-tile fp32 -> hi/lo work.
+  // a_lo may be null for one-pass bf16.  With rownorm the row scales come from row_scale[M].  On this
+  // path every group's o_off % 4 == 0 (the residual is staged in 16-B pieces).
+  const uint16_t* a_hi;
+  const uint16_t* a_lo;
+  int64_t a_ld;
+  const float* row_scale;
+  int k8;                     // every group's K % 8 == 0 (Gemm::k8): pre-split A may take the LDS-DMA kernel
+  // Split epilogue: write bf16 planes out_hi / out_lo [.][o_ld] instead of fp32 `out` (the result
+  // only feeds another tok_gemm; no residual).  out_lo may be null (bf16).
+  uint16_t* out_hi;
+  uint16_t* out_lo;
 };
+
+// Split fp32 rows into bf16 planes for tok_gemm's pre-split A: hi = bf16(x), lo = bf16(x - hi),
+// row m of x (x_ld floats) -> row m of the planes (p_ld elements); K % 4 == 0.  row_scale (nullable)
+// gets sqrt(K) / max(||x_m||_2, 1e-12) (the RMSNorm scale of rownorm).  lo null: hi only.
+int launch_tok_split(const float* x, int64_t x_ld, int64_t M, int K, uint16_t* hi, uint16_t* lo, int64_t p_ld,
+                     float* row_scale, hipStream_t st);
 
 // Flash attention over strided sequences of a token-major qkv buffer.
 // token(seq, p) = (seq / sdiv) * smul_a + (seq % sdiv) * smul_b + p * pstride
@@ -81,6 +100,8 @@ struct AttnArgs {
   int Lk;                     // keys per sequence (0: L)
   int64_t kv_smul;            // kv token of (seq, p) = seq * kv_smul + p (when kv != nullptr)
   int dh;                     // head dim, <= 64 and % 4 == 0 (0: 64); scale 1 / sqrt(dh)
+  uint16_t* out_hi;           // nullable: write bf16 planes (o_ld) instead of fp32 `out` (pre-split A of
+  uint16_t* out_lo;           //   the following to_out tok_gemm); out_lo may be null (bf16)
 };
 
 
@@ -103,6 +124,7 @@ struct Gemm {          // one packed (possibly grouped) GEMM
   std::vector<TokGroup> groups;
   TokGroup* d_groups = nullptr;
   int n_tiles_n = 0;
+  int k8 = 0;          // every group's K % 8 == 0
 };
 
 // Pack W[n][k] (row accessor) of an N x K GEMM for one group; returns the TokGroup with w_off/b_off set.
@@ -147,7 +169,11 @@ inline int upload_groups(Gemm& gm) {
   SESA_CHECK_HIP(hipMalloc(&gm.d_groups, gm.groups.size() * sizeof(TokGroup)));
   SESA_CHECK_HIP(hipMemcpy(gm.d_groups, gm.groups.data(), gm.groups.size() * sizeof(TokGroup), hipMemcpyHostToDevice));
   gm.n_tiles_n = 0;
-  for (auto& g : gm.groups) gm.n_tiles_n = std::max(gm.n_tiles_n, (g.N + kTokBN - 1) / kTokBN);
+  gm.k8 = 1;
+  for (auto& g : gm.groups) {
+    gm.n_tiles_n = std::max(gm.n_tiles_n, (g.N + kTokBN - 1) / kTokBN);
+    if (g.K % 8) gm.k8 = 0;
+  }
   return SESA_OK;
 }
 
