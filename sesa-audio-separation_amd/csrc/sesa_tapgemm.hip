@@ -448,7 +448,9 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 // XTRA: the raw block input rides along as extra K over the centre tap (the 1x1 shortcut, :126,
 // :137): its chunks load only the 16x32 inner positions (fp32, split in registers).
 // Weight image and A-image layouts are exactly tap_gemm_kernel's (same host packing).
-template <bool X3, bool XTRA>
+// EPI (ablation knob for tools/conv_bench.hip; the product uses 0): 1 = store without statistics,
+// 2 = no epilogue.
+template <bool X3, bool XTRA, int EPI = 0>
 __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   constexpr int NT = 512;
   constexpr int TM = 16, WM = 8, MI = 2, NI = 2, BN = 64;
@@ -674,6 +676,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     }
   }
 
+  if constexpr (EPI == 2) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   // ---- epilogue: fp32 store + per-channel sum / sum-of-squares for the next InstanceNorm ----
   // InstanceNorm statistics in fp64 from the first add on: E[x^2] - E[x]^2 is formed in double at the
   // consumer, so channels whose |mean| >> std (large norm beta, DC offsets) keep their precision
@@ -695,12 +704,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
         const int64_t idx = (((int64_t)b * a.T_out + t) * a.F_out + f) * C_out + co;
         const float v = acc[i][j][r];
         a.out.ptr[idx] = v;
+        if constexpr (EPI == 1) continue;
         ssum[j] += (double)v;
         ssq[j] = fma((double)v, (double)v, ssq[j]);
       }
     }
   }
-  if (a.out.stats) {
+  if (EPI == 0 && a.out.stats) {
     double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2] (the last barrier retired all LDS reads)
 #pragma unroll
     for (int j = 0; j < NI; ++j) {

@@ -3,9 +3,9 @@
 # SQ_WAIT_ANY (parked on s_waitcnt / barrier) + SQ_WAIT_INST_ANY (issue stall) + SQ_ACTIVE_INST_ANY
 # ~= SQ_WAVE_CYCLES (MI355X_MICROARCH.md, rocprofv3 PMC slots).
 set -e
-M=$1; TAG=$2; S=${3:-24}
+M=$1; TAG=$2; S=${3:-24}; EXTRA=${4:-}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-B="python3 bench.py --model $M --steps 1 --warmup 0 --track-seconds $S --no-cpu-baseline"
+B="python3 bench.py --model $M --steps 1 --warmup 0 --track-seconds $S --no-cpu-baseline $EXTRA"
 O=gpurun_out
 timeout -s KILL 60 rocprofv3 -L > $O/rocprof_counters.txt 2>&1 || true
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM -d $O/pmc_${TAG}_st -o run -- $B > /dev/null 2>&1
