@@ -240,7 +240,9 @@ int sesa_htdemucs_destroy(sesa_htdemucs* m);
  *   weights: host float[n_files] or NULL (normalised in float32 exactly as :288-293)
  * Spectral methods process independent `buffer`-sample pieces (scipy stft/istft per piece,
  * nperseg = min(1024, piece)); pieces < 256 samples use avg_wave (:355-357).  They need a
- * caller-owned workspace of sesa_blend_workspace_size(n_ch, buffer) bytes.  1 <= n_files <= 8.
+ * caller-owned workspace of sesa_blend_workspace_size_n(n_files, n_ch, buffer) bytes
+ * (sesa_blend_workspace_size(n_ch, buffer) covers n_files <= 8).  1 <= n_files <= 64.  NaN
+ * propagates through max / min / median as in numpy.
  */
 #define SESA_BLEND_AVG_WAVE 0
 #define SESA_BLEND_MEDIAN_WAVE 1
@@ -250,6 +252,7 @@ int sesa_htdemucs_destroy(sesa_htdemucs* m);
 #define SESA_BLEND_MIN_FFT 5
 #define SESA_BLEND_MEDIAN_FFT 6
 size_t sesa_blend_workspace_size(int n_ch, int64_t buffer);
+size_t sesa_blend_workspace_size_n(int n_files, int n_ch, int64_t buffer);
 int sesa_blend_f32(const float* x, int n_files, int n_ch, int64_t L, int64_t buffer, int method,
                    const float* weights, double* out, void* workspace, size_t workspace_bytes,
                    void* stream);

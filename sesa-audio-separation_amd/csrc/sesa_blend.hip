@@ -15,9 +15,13 @@
 //  combined per bin, inverse-transformed and windowed into a frame scratch; a second kernel
 //  overlap-adds.  HBM-bound: reads n_files x 4 B per sample (x2 frame overlap through L2),
 //  writes 8 B per sample.
+//  Up to kMaxFiles (64) files: max / min / mean reduce over the files in a loop; the medians keep one
+//  value per file (waveform: a per-thread array; spectral: magnitudes in LDS for <= kLdsFiles files,
+//  else in a global scratch after the frame images).  NaN propagates like numpy's max / min / median.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <mutex>
 #include <vector>
 
 #include "sesa_common.hpp"
@@ -26,7 +30,8 @@
 namespace sesa {
 namespace {
 
-constexpr int kMaxFiles = 8;
+constexpr int kMaxFiles = 64;
+constexpr int kLdsFiles = 8;   // spectral median: magnitudes of up to 8 files in LDS
 constexpr int kT = 256;
 constexpr int kSeg = 1024;
 
@@ -36,17 +41,24 @@ struct Weights {
   int has;
 };
 
-__device__ double median_of(double* v, int n) {
-  for (int i = 1; i < n; ++i) {  // insertion sort (n <= 8)
-    const double x = v[i];
+// numpy semantics: any NaN makes max / min / median NaN (fmax / fmin would drop it)
+__device__ __forceinline__ double nmax(double a, double b) { return (a != a || b != b) ? a + b : fmax(a, b); }
+__device__ __forceinline__ double nmin(double a, double b) { return (a != a || b != b) ? a + b : fmin(a, b); }
+
+// median of v[0 .. n) with stride `st` (insertion sort in place; n <= kMaxFiles)
+__device__ double median_of(double* v, int n, int st = 1) {
+  for (int i = 0; i < n; ++i)
+    if (v[i * st] != v[i * st]) return v[i * st];
+  for (int i = 1; i < n; ++i) {
+    const double x = v[i * st];
     int j = i - 1;
-    while (j >= 0 && v[j] > x) {
-      v[j + 1] = v[j];
+    while (j >= 0 && v[j * st] > x) {
+      v[(j + 1) * st] = v[j * st];
       --j;
     }
-    v[j + 1] = x;
+    v[(j + 1) * st] = x;
   }
-  return (n & 1) ? v[n / 2] : (v[n / 2 - 1] + v[n / 2]) * 0.5;
+  return (n & 1) ? v[(n / 2) * st] : (v[(n / 2 - 1) * st] + v[(n / 2) * st]) * 0.5;
 }
 
 // out[ch][t] for t in [t0, t1): x [file][n_ch][L] fp32
@@ -57,27 +69,27 @@ __global__ void blend_wave_kernel(const float* __restrict__ x, int n_files, int 
   if (i >= span * n_ch) return;
   const int ch = (int)(i / span);
   const int64_t t = t0 + (i - (int64_t)ch * span);
-  double v[kMaxFiles];
-  for (int f = 0; f < n_files; ++f) v[f] = (double)x[((int64_t)f * n_ch + ch) * L + t];
+  auto val = [&](int f) { return (double)x[((int64_t)f * n_ch + ch) * L + t]; };
   double r;
   if (method == SESA_BLEND_AVG_WAVE) {
+    double s = 0.0;
     if (wt.has) {
-      double s = 0.0;
-      for (int f = 0; f < n_files; ++f) s += v[f] * wt.w[f];
+      for (int f = 0; f < n_files; ++f) s += val(f) * wt.w[f];
       r = s / wt.sum;
     } else {
-      double s = 0.0;
-      for (int f = 0; f < n_files; ++f) s += v[f];
+      for (int f = 0; f < n_files; ++f) s += val(f);
       r = s / (double)n_files;
     }
   } else if (method == SESA_BLEND_MEDIAN_WAVE) {
+    double v[kMaxFiles];
+    for (int f = 0; f < n_files; ++f) v[f] = val(f);
     r = median_of(v, n_files);
   } else if (method == SESA_BLEND_MAX_WAVE) {
-    r = v[0];
-    for (int f = 1; f < n_files; ++f) r = fmax(r, v[f]);
+    r = val(0);
+    for (int f = 1; f < n_files; ++f) r = nmax(r, val(f));
   } else {
-    r = v[0];
-    for (int f = 1; f < n_files; ++f) r = fmin(r, v[f]);
+    r = val(0);
+    for (int f = 1; f < n_files; ++f) r = nmin(r, val(f));
   }
   out[(int64_t)ch * L + t] = r;
 }
@@ -114,16 +126,23 @@ struct Piece {
 };
 
 // One workgroup per (frame, channel): files' frames -> spectra -> combined -> windowed inverse frame.
+// mg_g: global magnitude scratch [n_files][nb] per (frame, channel) workgroup, used by the median
+// when n_files > kLdsFiles.
 __global__ void __launch_bounds__(kT) blend_fft_frames_kernel(const float* __restrict__ x, int n_files, int n_ch,
                                                               int64_t L, Piece pc, int method,
                                                               const double2* __restrict__ tw,
-                                                              double* __restrict__ frames) {
+                                                              double* __restrict__ frames, double* __restrict__ mg_g) {
   __shared__ double2 bufA[kSeg];
   __shared__ double2 bufB[kSeg];
-  __shared__ double2 Z[kMaxFiles][kSeg / 2 + 1];
+  __shared__ double2 Z0[kSeg / 2 + 1];                  // file 0's spectrum (its phase is kept)
+  __shared__ double mg_l[kLdsFiles][kSeg / 2 + 1];      // magnitudes: median over <= kLdsFiles files,
+                                                        // running max / min in row 0 otherwise
   __shared__ double win[kSeg];
   const int fr = blockIdx.x, ch = blockIdx.y;
   const int N = pc.N, half = N / 2, nb = N / 2 + 1;
+  const bool med = method == SESA_BLEND_MEDIAN_FFT;
+  const bool lds_med = med && n_files <= kLdsFiles;
+  double* mgw = mg_g + ((int64_t)ch * pc.nseg + fr) * (int64_t)n_files * nb;
   for (int n = threadIdx.x; n < N; n += kT) win[n] = 0.5 - 0.5 * cospi(2.0 * n / N);
   __syncthreads();
   const int64_t start = (int64_t)fr * pc.nstep - half;  // piece coordinates of frame sample 0
@@ -134,12 +153,12 @@ __global__ void __launch_bounds__(kT) blend_fft_frames_kernel(const float* __res
       const double v = (t >= 0 && t < pc.len) ? (double)xs[t] : 0.0;  // boundary zeros + padding
       bufA[n] = zc(v * win[n], 0.0);
     }
+    const double2* y = nullptr;
     if (N == kSeg) {
-      double2* y = fft1024d(bufA, bufB, tw, false);
-      for (int k = threadIdx.x; k < nb; k += kT) Z[f][k] = zc(y[k].x / pc.wsum, y[k].y / pc.wsum);
+      y = fft1024d(bufA, bufB, tw, false);
     } else {
       __syncthreads();
-      for (int k = threadIdx.x; k < nb; k += kT) {  // direct DFT (short last piece only)
+      for (int k = threadIdx.x; k < nb; k += kT) {  // direct DFT (short last piece only) into bufB
         double re = 0.0, im = 0.0;
         for (int n = 0; n < N; ++n) {
           const int64_t kn = ((int64_t)k * n) % N;
@@ -148,29 +167,31 @@ __global__ void __launch_bounds__(kT) blend_fft_frames_kernel(const float* __res
           re += bufA[n].x * cs;
           im -= bufA[n].x * sn;
         }
-        Z[f][k] = zc(re / pc.wsum, im / pc.wsum);
+        bufB[k] = zc(re, im);
       }
+      y = bufB;
+    }
+    for (int k = threadIdx.x; k < nb; k += kT) {
+      const double2 z = zc(y[k].x / pc.wsum, y[k].y / pc.wsum);
+      const double m = hypot(z.x, z.y);
+      if (f == 0) Z0[k] = z;
+      if (lds_med) mg_l[f][k] = m;
+      else if (med) mgw[(int64_t)f * nb + k] = m;
+      else if (f == 0) mg_l[0][k] = m;
+      else mg_l[0][k] = method == SESA_BLEND_MAX_FFT ? nmax(mg_l[0][k], m) : nmin(mg_l[0][k], m);
     }
     __syncthreads();
   }
   // combine magnitudes, phase of file 0 (np.abs / np.angle / exp(1j * angle))
   for (int k = threadIdx.x; k < nb; k += kT) {
-    double mg[kMaxFiles];
-    for (int f = 0; f < n_files; ++f) mg[f] = hypot(Z[f][k].x, Z[f][k].y);
     double c;
-    if (method == SESA_BLEND_MAX_FFT) {
-      c = mg[0];
-      for (int f = 1; f < n_files; ++f) c = fmax(c, mg[f]);
-    } else if (method == SESA_BLEND_MIN_FFT) {
-      c = mg[0];
-      for (int f = 1; f < n_files; ++f) c = fmin(c, mg[f]);
-    } else {
-      c = median_of(mg, n_files);
-    }
-    const double ang = atan2(Z[0][k].y, Z[0][k].x);
+    if (lds_med) c = median_of(&mg_l[0][k], n_files, kSeg / 2 + 1);
+    else if (med) c = median_of(mgw + k, n_files, nb);
+    else c = mg_l[0][k];
+    const double ang = atan2(Z0[k].y, Z0[k].x);
     double sn, cs;
     sincos(ang, &sn, &cs);
-    Z[0][k] = zc(c * cs, c * sn);  // (only this thread reads bin k of file 0)
+    Z0[k] = zc(c * cs, c * sn);  // (only this thread reads bin k)
   }
   __syncthreads();
   // irfft(n = N): Hermitian extension, imaginary parts of DC (and Nyquist, even N) ignored
@@ -178,25 +199,25 @@ __global__ void __launch_bounds__(kT) blend_fft_frames_kernel(const float* __res
   if (N == kSeg) {
     for (int k = threadIdx.x; k < N; k += kT) {
       double2 v;
-      if (k == 0) v = zc(Z[0][0].x, 0.0);
-      else if (k == half) v = zc(Z[0][half].x, 0.0);
-      else if (k < half) v = Z[0][k];
-      else v = zc(Z[0][N - k].x, -Z[0][N - k].y);
+      if (k == 0) v = zc(Z0[0].x, 0.0);
+      else if (k == half) v = zc(Z0[half].x, 0.0);
+      else if (k < half) v = Z0[k];
+      else v = zc(Z0[N - k].x, -Z0[N - k].y);
       bufA[k] = v;
     }
     double2* y = fft1024d(bufA, bufB, tw, true);
     for (int n = threadIdx.x; n < N; n += kT) out[n] = y[n].x / N * pc.wsum * win[n];
   } else {
     for (int n = threadIdx.x; n < N; n += kT) {
-      double acc = Z[0][0].x;
+      double acc = Z0[0].x;
       const int kmax = (N & 1) ? half : half - 1;
       for (int k = 1; k <= kmax; ++k) {
         const int64_t kn = ((int64_t)k * n) % N;
         double sn, cs;
         sincospi(2.0 * (double)kn / N, &sn, &cs);
-        acc += 2.0 * (Z[0][k].x * cs - Z[0][k].y * sn);
+        acc += 2.0 * (Z0[k].x * cs - Z0[k].y * sn);
       }
-      if (!(N & 1)) acc += Z[0][half].x * ((n & 1) ? -1.0 : 1.0);
+      if (!(N & 1)) acc += Z0[half].x * ((n & 1) ? -1.0 : 1.0);
       out[n] = acc / N * pc.wsum * win[n];
     }
   }
@@ -223,27 +244,28 @@ __global__ void blend_fft_ola_kernel(const double* __restrict__ frames, int n_ch
   out[(int64_t)ch * L + pc.pos + t] = acc / (norm > 1e-10 ? norm : 1.0);
 }
 
-double2* g_tw = nullptr;  // exp(-2 pi i j / 1024), j < 512 (per process; device 0 style cache)
-int g_tw_dev = -1;
+std::mutex g_tw_mu;
+std::vector<double2*> g_tw;  // per device: exp(-2 pi i j / 1024), j < 512
 
-int twiddles(const double2** tw) {
+int twiddles(const double2** tw, hipStream_t st) {
   int dev = 0;
   SESA_CHECK_HIP(hipGetDevice(&dev));
-  if (g_tw && g_tw_dev == dev) {
-    *tw = g_tw;
-    return SESA_OK;
+  std::lock_guard<std::mutex> lk(g_tw_mu);
+  if ((int)g_tw.size() <= dev) g_tw.resize(dev + 1, nullptr);
+  if (!g_tw[dev]) {
+    std::vector<double2> h(kSeg / 2);
+    for (int j = 0; j < kSeg / 2; ++j) {
+      const double a = -2.0 * M_PI * j / kSeg;
+      h[j] = make_double2(cos(a), sin(a));
+    }
+    double2* d = nullptr;
+    SESA_CHECK_HIP(hipMalloc(&d, h.size() * sizeof(double2)));
+    // ordered before the caller's kernels on its stream; the host copy must outlive the transfer
+    SESA_CHECK_HIP(hipMemcpyAsync(d, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice, st));
+    SESA_CHECK_HIP(hipStreamSynchronize(st));
+    g_tw[dev] = d;
   }
-  std::vector<double2> h(kSeg / 2);
-  for (int j = 0; j < kSeg / 2; ++j) {
-    const double a = -2.0 * M_PI * j / kSeg;
-    h[j] = make_double2(cos(a), sin(a));
-  }
-  double2* d = nullptr;
-  SESA_CHECK_HIP(hipMalloc(&d, h.size() * sizeof(double2)));
-  SESA_CHECK_HIP(hipMemcpy(d, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice));
-  g_tw = d;
-  g_tw_dev = dev;
-  *tw = d;
+  *tw = g_tw[dev];
   return SESA_OK;
 }
 
@@ -265,8 +287,20 @@ Piece make_piece(int64_t pos, int64_t len) {
 Weights make_weights(const float* w, int n) {
   Weights wt{};
   if (!w) return wt;
+  // np.float32 array .sum(): numpy's pairwise summation (sequential below 8 items, else 8 partial
+  // sums combined as ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the remainder)
   float sum = 0.f;
-  for (int i = 0; i < n; ++i) sum += w[i];
+  if (n < 8) {
+    for (int i = 0; i < n; ++i) sum += w[i];
+  } else {
+    float r[8];
+    for (int j = 0; j < 8; ++j) r[j] = w[j];
+    int i = 8;
+    for (; i + 8 <= n; i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += w[i + j];
+    sum = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) sum += w[i];
+  }
   double dsum = 0.0;
   for (int i = 0; i < n; ++i) {
     const float wn = w[i] / sum;  // float32 normalisation (ensemble.py:289-290)
@@ -278,14 +312,25 @@ Weights make_weights(const float* w, int n) {
   return wt;
 }
 
+// frame images (+ the spectral-median magnitude scratch when n_files > kLdsFiles)
+size_t blend_workspace(int n_files, int n_ch, int64_t buffer) {
+  const Piece p = make_piece(0, buffer);
+  size_t b = (size_t)n_ch * p.nseg * p.N * sizeof(double) + 1024;
+  if (n_files > kLdsFiles) b += (size_t)n_ch * p.nseg * n_files * (p.N / 2 + 1) * sizeof(double);
+  return b;
+}
+
 }  // namespace
 }  // namespace sesa
 
 using namespace sesa;
 
 extern "C" size_t sesa_blend_workspace_size(int n_ch, int64_t buffer) {
-  const Piece p = make_piece(0, buffer < kSeg ? buffer : buffer);
-  return (size_t)n_ch * p.nseg * p.N * sizeof(double) + 1024;
+  return sesa::blend_workspace(sesa::kLdsFiles, n_ch, buffer);
+}
+
+extern "C" size_t sesa_blend_workspace_size_n(int n_files, int n_ch, int64_t buffer) {
+  return sesa::blend_workspace(n_files, n_ch, buffer);
 }
 
 extern "C" int sesa_blend_f32(const float* x, int n_files, int n_ch, int64_t L, int64_t buffer, int method,
@@ -307,10 +352,11 @@ extern "C" int sesa_blend_f32(const float* x, int n_files, int n_ch, int64_t L, 
     SESA_CHECK_LAUNCH();
     return SESA_OK;
   }
-  SESA_REQUIRE(workspace && workspace_bytes >= sesa_blend_workspace_size(n_ch, buffer), SESA_ERR_INVALID,
-               "sesa_blend_f32: workspace too small");
+  SESA_REQUIRE(workspace && workspace_bytes >= blend_workspace(method == SESA_BLEND_MEDIAN_FFT ? n_files : 1, n_ch,
+                                                               buffer),
+               SESA_ERR_INVALID, "sesa_blend_f32: workspace too small (sesa_blend_workspace_size_n)");
   const double2* tw = nullptr;
-  int rc = twiddles(&tw);
+  int rc = twiddles(&tw, st);
   if (rc) return rc;
   for (int64_t pos = 0; pos < L; pos += buffer) {
     const int64_t len = buffer < L - pos ? buffer : L - pos;
@@ -322,8 +368,9 @@ extern "C" int sesa_blend_f32(const float* x, int n_files, int n_ch, int64_t L, 
     }
     const Piece pc = make_piece(pos, len);
     double* frames = reinterpret_cast<double*>(workspace);
+    double* mg = frames + (size_t)n_ch * pc.nseg * pc.N;
     hipLaunchKernelGGL(blend_fft_frames_kernel, dim3(pc.nseg, n_ch), dim3(kT), 0, st, x, n_files, n_ch, L, pc, method,
-                       tw, frames);
+                       tw, frames, mg);
     SESA_CHECK_LAUNCH();
     hipLaunchKernelGGL(blend_fft_ola_kernel, dim3((unsigned)((len * n_ch + 255) / 256)), dim3(256), 0, st, frames,
                        n_ch, L, pc, out);

@@ -94,6 +94,7 @@ SIGNATURES = {
     "sesa_htdemucs_forward": (c_int, [c_void_p, P_f32, c_int, P_f32, c_void_p, c_size_t, c_void_p]),
     "sesa_htdemucs_destroy": (c_int, [c_void_p]),
     "sesa_blend_workspace_size": (c_size_t, [c_int, c_int64]),
+    "sesa_blend_workspace_size_n": (c_size_t, [c_int, c_int, c_int64]),
     "sesa_blend_f32": (c_int, [P_f32, c_int, c_int, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                c_void_p]),
     "sesa_flac_info": (c_int, [c_void_p, c_size_t, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int),

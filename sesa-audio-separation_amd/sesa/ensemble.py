@@ -37,7 +37,7 @@ def blend_device(waves, method, weights=None, buffer=32768):
     w = None
     if weights is not None and len(weights) == n:
         w = np.ascontiguousarray(np.asarray(weights, np.float32))
-    ws_bytes = N.lib().sesa_blend_workspace_size(ch, int(buffer))
+    ws_bytes = N.lib().sesa_blend_workspace_size_n(n, ch, int(buffer))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if method.endswith("_fft") else None
     N.check(N.lib().sesa_blend_f32(x.data_ptr(), n, ch, L, int(buffer), METHODS.index(method),
                                    w.ctypes.data if w is not None else None, out.data_ptr(),

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from .. import _native as N
+from .. import ops as _ops  # noqa: F401  (registers the sesa::<net>_forward custom ops)
 
 
 class _Node(torch.nn.Module):
@@ -137,10 +138,8 @@ class NativeModule(torch.nn.Module):
         x = x.to(torch.float32).contiguous()
         B, ch, L = x.shape
         h = self._handle(x.device, L)
-        out = torch.empty(self._out_shape(B, ch, L), device=x.device, dtype=torch.float32)
         ws = self.workspace(x.device, h, B)
-        N.check(self._fn("forward")(h, x.data_ptr(), B, out.data_ptr(), ws.data_ptr(), ws.numel(),
-                                    torch.cuda.current_stream(x.device).cuda_stream), f"sesa_{self._prefix}_forward")
+        out = getattr(torch.ops.sesa, f"{self._prefix}_forward")(h.value, x, ws, list(self._out_shape(B, ch, L)))
         return self._post(out)
 
     def _post(self, out):

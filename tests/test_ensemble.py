@@ -73,6 +73,32 @@ def test_device_buffer_loop_matches_oracle(L, method):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_files", [9, 13])
+@pytest.mark.parametrize("method", ["avg_wave", "median_wave", "max_wave", "min_wave", "max_fft", "median_fft",
+                                    "min_fft"])
+def test_device_blend_many_files(n_files, method):
+    """More than 8 inputs (ensemble.py has no file limit): every method against the oracle."""
+    from sesa.ensemble import blend_device
+    rng = np.random.default_rng(n_files)
+    waves = (0.1 * rng.standard_normal((n_files, 2, 40000))).astype(np.float32)
+    weights = list(rng.uniform(0.5, 2.0, n_files))
+    got = blend_device(waves, method, weights, buffer=32768).cpu().numpy()
+    exp = oe.blend(waves.astype(np.float64), method, weights, buffer=32768)
+    assert np.abs(got - exp).max() <= TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["median_wave", "max_wave", "min_wave"])
+def test_device_blend_nan_propagates(method):
+    """np.max / np.min / np.median propagate NaN (fmax / fmin would drop it)."""
+    from sesa.ensemble import blend_device
+    waves = np.full((3, 1, 1000), 0.25, np.float32)
+    waves[1, 0, 17] = np.nan
+    got = blend_device(waves, method).cpu().numpy()
+    assert np.isnan(got[0, 17]) and np.isfinite(np.delete(got[0], 17)).all()
+
+
+@pytest.mark.gpu
 def test_run_ensemble_writes_pcm24(tmp_path, capsys):
     from sesa.audio_io import quantize_pcm, read_wav, write_audio
     from sesa.ensemble import main
