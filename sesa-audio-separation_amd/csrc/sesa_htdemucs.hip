@@ -30,9 +30,14 @@
 //   tok_gemm (conv mode)   encoder convs (+ bias + GELU), rewrite 1x1 (+ GLU), decoder 3x3 / k3 rewrite
 //                          with the skip added on load (+ GLU), transposed convs (phase-scatter
 //                          epilogue, trim, + GELU) -- bf16x3 MFMA (sesa_tokgemm.hip)
-//   htd_dc_conv_kernel     DConv layer head: dilated conv1d k3 over T + GroupNorm(1, h) statistics
-//   htd_dc_stats_kernel    DConv: GroupNorm statistics of the 1x1 conv output (recomputed, not stored)
-//   htd_dc_apply_kernel    DConv: 1x1 conv, GroupNorm(1, 2C), GLU, LayerScale, residual (in place)
+//   DConv (per layer, demucs.demucs.DConv restated):
+//     tok_gemm (conv mode)   dilated conv1d k3 over T as an implicit GEMM (N = h, K = 3 C, bias) -> U
+//     htd_item_stats_kernel  GroupNorm(1, h) sums of U per row
+//     htd_dc_gram_kernel     G = GELU(GN(U)): per-row sum(G) and Gram matrix sum(G G^T) (fp64).  The
+//                            GroupNorm(1, 2C) moments of the 1x1 output V = W2 G + b2 are quadratic
+//                            forms in those (sum V = wbar.sum G + T sum b2, sum V^2 = <W2^T W2, sum G G^T>
+//                            + 2 (W2^T b2).sum G + T |b2|^2), so V is never materialised or recomputed
+//     htd_dc_apply_kernel    1x1 conv, GroupNorm(1, 2C), GLU, LayerScale, residual (in place)
 //   htd_layernorm_kernel   LayerNorm rows (+ the weighted positional embedding for norm_in)
 //   htd_gn_apply_kernel    MyGroupNorm(1, d) (norm_out) over a whole token sequence, in place
 //   tok_gemm / attn_kernel transformer Linears (bias, GELU, LayerScale folded, residual) and SDPA
@@ -185,82 +190,24 @@ __global__ void htd_add_rows_kernel(float* __restrict__ X, int F, int T, int C, 
 // time branch -------------------------------------------------------------------------------
 struct DcArgs {
   float* X;            // [rows][T][C]
-  int rows, T, C, h, dil;
-  const float* W1;     // [C][3][h]
-  const float* b1;     // [h]
+  int rows, T, C, h;
+  const float* b1;     // unused by the kernels (the k3 conv's bias is in its GEMM)
   const float *g1, *be1;
   const float* W2t;    // [h][2C]
   const float* b2;     // [2C]
   const float *g2, *be2;
   const float* scale;  // [C]
-  float* U;            // [rows][T][h]
-  double* st1;         // [rows][2]  GroupNorm(1, h) sums of U
-  double* st2;         // [rows][2]  GroupNorm(1, 2C) sums of V = W2 gelu(gn(U)) + b2
+  const float* U;      // [rows][T][h]  k3 conv output (+ bias)
+  const double* st1;   // [rows][2]     GroupNorm(1, h) sums of U
+  double* gram;        // [rows][nS]    sum G_j (h), then sum G_j G_k for j <= k (row-major triangle)
+  const double* gc;    // layer constants: coef of the triangle (M_jj or 2 M_jk, M = W2^T W2), wbar[h] =
+                       // sum_c W2[c][:], v2[h] = 2 sum_c b2[c] W2[c][:], sum b2, sum b2^2
 };
-constexpr int kDcP = 64;      // positions per workgroup
-constexpr int kDcK = 32;      // channel chunk of the k3 conv
+constexpr int kDcP = 64;      // positions per workgroup (apply)
+constexpr int kDcG = 128;     // positions per workgroup (Gram)
 constexpr int kDcMaxH = 64;
-constexpr int kDcMaxDil = 8;
 
-__global__ void __launch_bounds__(kT) htd_dc_conv_kernel(DcArgs a) {
-  constexpr int XW = kDcP + 2 * kDcMaxDil + 1;
-  __shared__ float xs[kDcK][XW];
-  __shared__ float ws[kDcK][3][kDcMaxH];
-  __shared__ double red[2 * (kT / 64)];
-  const int row = blockIdx.y;
-  const int t0 = blockIdx.x * kDcP;
-  const int lane = threadIdx.x & 63, jg = threadIdx.x >> 6;
-  const int T = a.T, C = a.C, h = a.h, dil = a.dil;
-  const int W = kDcP + 2 * dil;
-  const float* xr = a.X + (int64_t)row * T * C;
-  float acc[16];
-#pragma unroll
-  for (int u = 0; u < 16; ++u) acc[u] = 0.f;
-  const int nu = (h - jg + 3) / 4;   // outputs j = jg + 4 u, u < nu
-  for (int c0 = 0; c0 < C; c0 += kDcK) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < kDcK * W; i += kT) {
-      const int c = i % kDcK, p = i / kDcK;
-      const int t = t0 - dil + p;
-      xs[c][p] = (c0 + c < C && t >= 0 && t < T) ? xr[(int64_t)t * C + c0 + c] : 0.f;
-    }
-    for (int i = threadIdx.x; i < kDcK * 3 * h; i += kT) {
-      const int j = i % h, r = i / h;
-      const int tap = r % 3, c = r / 3;
-      ws[c][tap][j] = c0 + c < C ? a.W1[((int64_t)(c0 + c) * 3 + tap) * h + j] : 0.f;
-    }
-    __syncthreads();
-    const int cn = min(kDcK, C - c0);
-    for (int c = 0; c < cn; ++c) {
-#pragma unroll
-      for (int tap = 0; tap < 3; ++tap) {
-        const float xv = xs[c][lane + tap * dil];
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-          if (u < nu) acc[u] = fmaf(ws[c][tap][jg + 4 * u], xv, acc[u]);
-      }
-    }
-  }
-  const int t = t0 + lane;
-  double s = 0, ss = 0;
-  if (t < T) {
-    float* ur = a.U + ((int64_t)row * T + t) * h;
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (u < nu) {
-        const int j = jg + 4 * u;
-        const float v = acc[u] + a.b1[j];
-        ur[j] = v;
-        s += v;
-        ss += (double)v * v;
-      }
-  }
-  block_sum2(s, ss, red);
-  if (threadIdx.x == 0) {
-    atomicAdd(&a.st1[2 * row], s);
-    atomicAdd(&a.st1[2 * row + 1], ss);
-  }
-}
+__host__ __device__ constexpr int dc_ns(int h) { return h + h * (h + 1) / 2; }
 
 // biased GroupNorm statistics (torch GroupNorm) from fp64 sums
 __device__ __forceinline__ void gn_stats(const double* st, double n, float& mean, float& rstd) {
@@ -270,13 +217,47 @@ __device__ __forceinline__ void gn_stats(const double* st, double n, float& mean
   rstd = (float)(1.0 / sqrt(var + 1e-5));
 }
 
+// Per (t-block, row): G = gelu(gn1(U)) into LDS, then entry e of (sum G | sum G G^T) summed over the
+// block's positions in fp64 and added to the row's totals.
+__global__ void __launch_bounds__(kT) htd_dc_gram_kernel(DcArgs a) {
+  __shared__ float Gs[kDcG][kDcMaxH + 1];
+  const int row = blockIdx.y;
+  const int t0 = blockIdx.x * kDcG;
+  const int T = a.T, h = a.h;
+  const int np = min(kDcG, T - t0);
+  float m1, r1;
+  gn_stats(a.st1 + 2 * row, (double)T * h, m1, r1);
+  for (int i = threadIdx.x; i < np * h; i += kT) {
+    const int p = i / h, j = i - p * h;
+    const float u = a.U[((int64_t)row * T + t0 + p) * h + j];
+    Gs[p][j] = gelu_erf((u - m1) * r1 * a.g1[j] + a.be1[j]);
+  }
+  __syncthreads();
+  const int nS = dc_ns(h);
+  for (int e = threadIdx.x; e < nS; e += kT) {
+    double acc = 0.0;
+    if (e < h) {
+      for (int p = 0; p < np; ++p) acc += (double)Gs[p][e];
+    } else {
+      int j = 0, r = e - h;
+      while (r >= h - j) {
+        r -= h - j;
+        ++j;
+      }
+      const int k = j + r;
+      for (int p = 0; p < np; ++p) acc = fma((double)Gs[p][j], (double)Gs[p][k], acc);
+    }
+    atomicAdd(&a.gram[(int64_t)row * nS + e], acc);
+  }
+}
+
 // G tile [64][h]: gelu(gn1(U)) for the workgroup's positions; then per 64-channel chunk c0 the 1x1 conv
-// columns (a: c, gate: C + c) are recomputed for 16 positions per thread (lane = channel).
-template <bool APPLY>
-__global__ void __launch_bounds__(kT) htd_dc_out_kernel(DcArgs a) {
-  __shared__ float Gs[kDcP][kDcMaxH + 1];
-  __shared__ float Wa[kDcMaxH][64];
-  __shared__ float Wg[kDcMaxH][64];
+// columns (a: c, gate: C + c) for 16 positions per thread (lane = channel, its two W2 columns held in
+// registers: HM >= h, so the only LDS traffic is the broadcast G row), GroupNorm(1, 2C) with the moments
+// from the row's Gram sums, GLU, LayerScale, residual.
+template <int HM>
+__global__ void __launch_bounds__(kT) htd_dc_apply_kernel(DcArgs a) {
+  __shared__ __attribute__((aligned(16))) float Gs[kDcP][HM];
   __shared__ double red[2 * (kT / 64)];
   const int row = blockIdx.y;
   const int t0 = blockIdx.x * kDcP;
@@ -284,57 +265,88 @@ __global__ void __launch_bounds__(kT) htd_dc_out_kernel(DcArgs a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float m1, r1;
   gn_stats(a.st1 + 2 * row, (double)T * h, m1, r1);
-  for (int i = threadIdx.x; i < kDcP * h; i += kT) {
-    const int p = i / h, j = i - p * h;
+  // GroupNorm(1, 2C) moments of V from the Gram sums (fp64)
+  float m2, r2;
+  {
+    const int nS = dc_ns(h);
+    const double* gr = a.gram + (int64_t)row * nS;
+    const double* coefS = a.gc;                  // [nS - h]
+    const double* wbar = a.gc + (nS - h);        // [h]
+    const double* v2 = wbar + h;                 // [h]
+    double s1 = 0.0, s2 = 0.0;
+    for (int e = threadIdx.x; e < nS; e += kT) {
+      if (e < h) {
+        s1 += wbar[e] * gr[e];
+        s2 += v2[e] * gr[e];
+      } else {
+        s2 += coefS[e - h] * gr[e];
+      }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+      s1 += __shfl_xor(s1, o);
+      s2 += __shfl_xor(s2, o);
+    }
+    if (lane == 0) {
+      red[2 * wv] = s1;
+      red[2 * wv + 1] = s2;
+    }
+    __syncthreads();
+    s1 = 0.0;
+    s2 = 0.0;
+    for (int i = 0; i < kT / 64; ++i) {
+      s1 += red[2 * i];
+      s2 += red[2 * i + 1];
+    }
+    const double sb = a.gc[nS + h], sbb = a.gc[nS + h + 1];
+    const double n = (double)T * 2 * C;
+    const double mu = (s1 + (double)T * sb) / n;
+    const double var = fmax((s2 + (double)T * sbb) / n - mu * mu, 0.0);
+    m2 = (float)mu;
+    r2 = (float)(1.0 / sqrt(var + 1e-5));
+  }
+  for (int i = threadIdx.x; i < kDcP * HM; i += kT) {   // pad columns h .. HM are zero
+    const int p = i / HM, j = i - p * HM;
     const int t = t0 + p;
     float g = 0.f;
-    if (t < T) {
+    if (t < T && j < h) {
       const float u = a.U[((int64_t)row * T + t) * h + j];
       g = gelu_erf((u - m1) * r1 * a.g1[j] + a.be1[j]);
     }
     Gs[p][j] = g;
   }
-  float m2 = 0.f, r2 = 0.f;
-  if (APPLY) gn_stats(a.st2 + 2 * row, (double)T * 2 * C, m2, r2);
-  double s = 0, ss = 0;
+  __syncthreads();
   for (int c0 = 0; c0 < C; c0 += 64) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < h * 64; i += kT) {
-      const int j = i >> 6, cc = i & 63;
-      const bool ok = c0 + cc < C;
-      Wa[j][cc] = ok ? a.W2t[(int64_t)j * 2 * C + c0 + cc] : 0.f;
-      Wg[j][cc] = ok ? a.W2t[(int64_t)j * 2 * C + C + c0 + cc] : 0.f;
-    }
-    __syncthreads();
     const int c = c0 + lane;
-    if (c >= C) continue;
+    if (c >= C) break;
+    float wa[HM], wg[HM];
+#pragma unroll
+    for (int j = 0; j < HM; ++j) {
+      wa[j] = j < h ? a.W2t[(int64_t)j * 2 * C + c] : 0.f;
+      wg[j] = j < h ? a.W2t[(int64_t)j * 2 * C + C + c] : 0.f;
+    }
     const float ba = a.b2[c], bg = a.b2[C + c];
+    const float ga = a.g2[c] * r2, gg = a.g2[C + c] * r2;   // (v - mean) * (rstd * gamma) + beta
+    const float oa = a.be2[c], og = a.be2[C + c];
+    const float sc = a.scale[c];
     for (int q = 0; q < kDcP / 4; ++q) {
       const int p = wv + 4 * q;
       const int t = t0 + p;
       if (t >= T) break;
       float va = ba, vg = bg;
-      for (int j = 0; j < h; ++j) {
-        const float g = Gs[p][j];
-        va = fmaf(Wa[j][lane], g, va);
-        vg = fmaf(Wg[j][lane], g, vg);
+#pragma unroll
+      for (int j4 = 0; j4 < HM; j4 += 4) {
+        const float4 g = *reinterpret_cast<const float4*>(&Gs[p][j4]);
+        va = fmaf(wa[j4], g.x, va);
+        vg = fmaf(wg[j4], g.x, vg);
+        va = fmaf(wa[j4 + 1], g.y, va);
+        vg = fmaf(wg[j4 + 1], g.y, vg);
+        va = fmaf(wa[j4 + 2], g.z, va);
+        vg = fmaf(wg[j4 + 2], g.z, vg);
+        va = fmaf(wa[j4 + 3], g.w, va);
+        vg = fmaf(wg[j4 + 3], g.w, vg);
       }
-      if (APPLY) {
-        const float an = (va - m2) * r2 * a.g2[c] + a.be2[c];
-        const float gn = (vg - m2) * r2 * a.g2[C + c] + a.be2[C + c];
-        float* xp = a.X + ((int64_t)row * T + t) * C + c;
-        *xp = *xp + a.scale[c] * (an * sigm(gn));
-      } else {
-        s += (double)va + (double)vg;
-        ss += (double)va * va + (double)vg * vg;
-      }
-    }
-  }
-  if (!APPLY) {
-    block_sum2(s, ss, red);
-    if (threadIdx.x == 0) {
-      atomicAdd(&a.st2[2 * row], s);
-      atomicAdd(&a.st2[2 * row + 1], ss);
+      float* xp = a.X + ((int64_t)row * T + t) * C + c;
+      *xp = *xp + sc * (fmaf(va - m2, ga, oa) * sigm(fmaf(vg - m2, gg, og)));
     }
   }
 }
@@ -456,8 +468,10 @@ struct Param {
 };
 
 struct DcLayer {  // float offsets into the packed fp32 blob
-  int64_t w1, b1, g1, be1, w2t, b2, g2, be2, scale;
+  int64_t b1, g1, be1, w2t, b2, g2, be2, scale;
+  int64_t gc;     // double offset of the Gram constants (htd_dc_apply_kernel)
   int dil;
+  Gemm conv;      // the dilated k3 conv: N = h, K = 3 C (k = tap * C + c), bias b1
 };
 
 struct Branch {   // one encoder / decoder level of one branch
@@ -490,6 +504,7 @@ struct sesa_htdemucs {
   std::vector<sesa::Param> params;
   std::map<std::string, int> by_name;
   float* d_f32 = nullptr;
+  double* d_f64 = nullptr;   // DConv Gram constants
   uint16_t* d_w = nullptr;
   float* d_bias = nullptr;
   bool finalized = false;
@@ -563,7 +578,7 @@ Plan plan(const sesa_htdemucs* m, int B) {
   p.X0 = off; off += al((size_t)B * kF0 * T * 2 * ach);
   p.XT0 = off; off += al((size_t)B * L * 4);
   p.stats = off; off += al((size_t)B * 16 * 2);   // doubles: freq, time, gn (2 per item each), spare
-  size_t e = 0, u = 0, rows = 0, dfa = 0, dfb = 0, dta = 0, dtb = 0;
+  size_t e = 0, u = 0, rows = 0, dfa = 0, dfb = 0, dta = 0, dtb = 0, rst = 0;
   for (int i = 0; i < m->depth; ++i) {
     const Branch& f = m->fq[i];
     const Branch& t = m->tm[i];
@@ -572,6 +587,7 @@ Plan plan(const sesa_htdemucs* m, int B) {
     e = std::max({e, (size_t)B * f.Fout * T * f.Cout, (size_t)B * t.Fout * t.Cout});
     u = std::max({u, (size_t)B * f.Fout * T * f.h, (size_t)B * t.Fout * t.h});
     rows = std::max({rows, (size_t)B * f.Fout, (size_t)B});
+    rst = std::max({rst, (size_t)B * f.Fout * (2 + dc_ns(f.h)), (size_t)B * (2 + dc_ns(t.h))});
     dfa = std::max(dfa, (size_t)B * f.Fin * T * f.Cdec);       // convtr output (next level's input)
     dfb = std::max(dfb, (size_t)B * f.Fout * T * f.Cout);      // rewrite output
     dta = std::max(dta, (size_t)B * t.Fin * t.Cdec);
@@ -579,7 +595,7 @@ Plan plan(const sesa_htdemucs* m, int B) {
   }
   dfa = std::max(dfa, (size_t)B * m->Nx * m->C3);               // downsampler output
   dta = std::max(dta, (size_t)B * m->Nt * m->C3);
-  p.rowst = off; off += al(rows * 4 * 2);                          // doubles: st1, st2
+  p.rowst = off; off += al(rst * 2);                               // doubles: st1 [rows][2], Gram [rows][nS]
   p.E = off; off += al(e);
   p.U = off; off += al(u);
   p.dA = off; off += al(dfa);
@@ -685,7 +701,6 @@ extern "C" int sesa_htdemucs_create(const sesa_htdemucs_config* cfg, sesa_htdemu
     freqs /= c.stride;
     Lt = t.Fout;
   }
-  if ((1 << (c.dconv_depth - 1 > 0 ? c.dconv_depth - 1 : 0)) > kDcMaxDil) return fail("DConv dilation too large", c.dconv_depth);
   m->C3 = m->fq[c.depth - 1].Cout;
   m->F3 = m->fq[c.depth - 1].Fout;
   m->Lt3 = m->tm[c.depth - 1].Fout;
@@ -819,18 +834,24 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
   std::vector<uint16_t> blob;
   std::vector<float> bias;
   auto single = [&](Gemm& gm, const TokGroup& g) { gm.groups = {g}; };
+  std::vector<double> f64;
   auto pack_dconv = [&](std::vector<DcLayer>& out, const std::string& p, int C, int h) {
+    for (auto& L : out)
+      if (L.conv.d_groups) (void)hipFree(L.conv.d_groups);
     out.clear();
     for (int d = 0; d < c.dconv_depth; ++d) {
       const std::string q = p + ".dconv.layers." + S(d);
       DcLayer L{};
       L.dil = 1 << d;
-      const auto& W1 = P(m, q + ".0.weight");   // [h][C][3] -> [C][3][h]
-      std::vector<float> w1((size_t)C * 3 * h);
-      for (int j = 0; j < h; ++j)
-        for (int ci = 0; ci < C; ++ci)
-          for (int k = 0; k < 3; ++k) w1[((size_t)ci * 3 + k) * h + j] = W1[((size_t)j * C + ci) * 3 + k];
-      L.w1 = put(w1);
+      const auto& W1 = P(m, q + ".0.weight");   // [h][C][3]
+      const auto& B1 = P(m, q + ".0.bias");
+      single(L.conv, pack_group(
+                         h, 3 * C,
+                         [&](int n, int k) {
+                           const int tap = k / C, ci = k - tap * C;
+                           return W1[((size_t)n * C + ci) * 3 + tap];
+                         },
+                         true, [&](int n) { return B1[n]; }, blob, bias));
       L.b1 = putp(q + ".0.bias");
       L.g1 = putp(q + ".1.weight");
       L.be1 = putp(q + ".1.bias");
@@ -843,6 +864,32 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
       L.g2 = putp(q + ".4.weight");
       L.be2 = putp(q + ".4.bias");
       L.scale = putp(q + ".6.scale");
+      // Gram constants in fp64: triangle coefficients of M = W2^T W2, wbar, 2 W2^T b2, sum b2, sum b2^2
+      const auto& B2 = P(m, q + ".3.bias");
+      L.gc = (int64_t)f64.size();
+      for (int j = 0; j < h; ++j)
+        for (int k = j; k < h; ++k) {
+          double mjk = 0.0;
+          for (int n = 0; n < 2 * C; ++n) mjk += (double)W2[(size_t)n * h + j] * (double)W2[(size_t)n * h + k];
+          f64.push_back(j == k ? mjk : 2.0 * mjk);
+        }
+      for (int j = 0; j < h; ++j) {
+        double w = 0.0;
+        for (int n = 0; n < 2 * C; ++n) w += (double)W2[(size_t)n * h + j];
+        f64.push_back(w);
+      }
+      for (int j = 0; j < h; ++j) {
+        double v = 0.0;
+        for (int n = 0; n < 2 * C; ++n) v += (double)B2[n] * (double)W2[(size_t)n * h + j];
+        f64.push_back(2.0 * v);
+      }
+      double sb = 0.0, sbb = 0.0;
+      for (int n = 0; n < 2 * C; ++n) {
+        sb += B2[n];
+        sbb += (double)B2[n] * B2[n];
+      }
+      f64.push_back(sb);
+      f64.push_back(sbb);
       out.push_back(L);
     }
   };
@@ -1008,14 +1055,23 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                "htdemucs finalize: hipMalloc gemm weights");
   SESA_REQUIRE(hipMalloc(&m->d_bias, std::max<size_t>(bias.size(), 1) * 4) == hipSuccess, SESA_ERR_NOMEM,
                "htdemucs finalize: hipMalloc bias");
+  if (m->d_f64) (void)hipFree(m->d_f64);
+  m->d_f64 = nullptr;
+  SESA_REQUIRE(hipMalloc(&m->d_f64, std::max<size_t>(f64.size(), 1) * 8) == hipSuccess, SESA_ERR_NOMEM,
+               "htdemucs finalize: hipMalloc Gram constants");
   hipStream_t st = as_stream(stream);
   SESA_CHECK_HIP(hipMemcpyAsync(m->d_f32, f32.data(), f32.size() * 4, hipMemcpyHostToDevice, st));
   if (!blob.empty()) SESA_CHECK_HIP(hipMemcpyAsync(m->d_w, blob.data(), blob.size() * 2, hipMemcpyHostToDevice, st));
   if (!bias.empty()) SESA_CHECK_HIP(hipMemcpyAsync(m->d_bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice, st));
+  if (!f64.empty()) SESA_CHECK_HIP(hipMemcpyAsync(m->d_f64, f64.data(), f64.size() * 8, hipMemcpyHostToDevice, st));
   SESA_CHECK_HIP(hipStreamSynchronize(st));
   std::vector<Gemm*> all;
   for (auto* br : {&m->fq, &m->tm})
-    for (auto& B : *br) all.insert(all.end(), {&B.conv, &B.rewrite, &B.drewrite, &B.convtr});
+    for (auto& B : *br) {
+      all.insert(all.end(), {&B.conv, &B.rewrite, &B.drewrite, &B.convtr});
+      for (auto* dv : {&B.edc, &B.ddc})
+        for (auto& L : *dv) all.push_back(&L.conv);
+    }
   if (c.bottom_channels) all.insert(all.end(), {&m->up, &m->down, &m->up_t, &m->down_t});
   for (auto* tv : {&m->tl, &m->tlt})
     for (auto& L : *tv) {
@@ -1167,17 +1223,21 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   };
   auto dconv = [&](const std::vector<DcLayer>& layers, float* X, int rows, int Tn, int C, int h) {
     if (rc) return;
-    void* tok = profile_begin(st);
     float* U = F32(pl.U);
+    const int nS = dc_ns(h);
+    const int P1 = rows / B;   // frequency rows per item (1 for the time branch)
     for (const DcLayer& Ly : layers) {
+      // dilated k3 conv over T (padding = dilation) -> U [rows][T][h] (+ bias), bf16x3 MFMA
+      conv_gemm(Ly.conv, X, C, nullptr, U, h, P1, Tn, P1, Tn, 1, C, {0, 0, 0}, {-Ly.dil, 0, Ly.dil}, TOK_ACT_NONE, 0,
+                1, 0, 0);
+      if (rc) return;
+      void* tok = profile_begin(st);
       DcArgs a{};
       a.X = X;
       a.rows = rows;
       a.T = Tn;
       a.C = C;
       a.h = h;
-      a.dil = Ly.dil;
-      a.W1 = Wb + Ly.w1;
       a.b1 = Wb + Ly.b1;
       a.g1 = Wb + Ly.g1;
       a.be1 = Wb + Ly.be1;
@@ -1188,25 +1248,33 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       a.scale = Wb + Ly.scale;
       a.U = U;
       a.st1 = rowst;
-      a.st2 = rowst + 2 * (size_t)rows;
-      if (hipMemsetAsync(rowst, 0, (size_t)rows * 4 * sizeof(double), st) != hipSuccess) {
+      a.gram = rowst + 2 * (size_t)rows;
+      a.gc = m->d_f64 + Ly.gc;
+      if (hipMemsetAsync(rowst, 0, (size_t)rows * (2 + nS) * sizeof(double), st) != hipSuccess) {
         rc = SESA_ERR_HIP;
         set_error("htdemucs: memset");
         return;
       }
-      dim3 grid((unsigned)((Tn + kDcP - 1) / kDcP), (unsigned)rows);
-      hipLaunchKernelGGL(htd_dc_conv_kernel, grid, dim3(kT), 0, st, a);
-      hipLaunchKernelGGL(htd_dc_out_kernel<false>, grid, dim3(kT), 0, st, a);
-      hipLaunchKernelGGL(htd_dc_out_kernel<true>, grid, dim3(kT), 0, st, a);
+      const int64_t n_item = (int64_t)Tn * h;
+      hipLaunchKernelGGL(htd_item_stats_kernel, dim3((unsigned)std::min<int64_t>((n_item + kT * 8 - 1) / (kT * 8), 512),
+                                                     (unsigned)rows),
+                         dim3(kT), 0, st, U, n_item, rowst);
+      hipLaunchKernelGGL(htd_dc_gram_kernel, dim3((unsigned)((Tn + kDcG - 1) / kDcG), (unsigned)rows), dim3(kT), 0, st,
+                         a);
+      const dim3 ga((unsigned)((Tn + kDcP - 1) / kDcP), (unsigned)rows);
+      if (h <= 8) hipLaunchKernelGGL(htd_dc_apply_kernel<8>, ga, dim3(kT), 0, st, a);
+      else if (h <= 16) hipLaunchKernelGGL(htd_dc_apply_kernel<16>, ga, dim3(kT), 0, st, a);
+      else if (h <= 32) hipLaunchKernelGGL(htd_dc_apply_kernel<32>, ga, dim3(kT), 0, st, a);
+      else hipLaunchKernelGGL(htd_dc_apply_kernel<64>, ga, dim3(kT), 0, st, a);
       if (hipGetLastError() != hipSuccess) {
         rc = SESA_ERR_HIP;
         set_error("htdemucs: DConv launch failed");
         return;
       }
+      profile_end(tok, st, SESA_KCLASS_SIMT, 2.0 * rows * Tn * (2.0 * h * 2 * C + 0.5 * h * h));
     }
-    profile_end(tok, st, SESA_KCLASS_SIMT,
-                (double)layers.size() * 2.0 * rows * Tn * (3.0 * C * h + 2.0 * 2.0 * h * 2 * C));
   };
+
 
   // ---- 2. encoders (:593-618) ----
   std::vector<int> enc_d1(Kk);
@@ -1429,11 +1497,15 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
 
 extern "C" int sesa_htdemucs_destroy(sesa_htdemucs* m) {
   if (!m) return SESA_OK;
-  for (void* p : {(void*)m->d_f32, (void*)m->d_w, (void*)m->d_bias})
+  for (void* p : {(void*)m->d_f32, (void*)m->d_f64, (void*)m->d_w, (void*)m->d_bias})
     if (p) (void)hipFree(p);
   std::vector<Gemm*> all;
   for (auto* br : {&m->fq, &m->tm})
-    for (auto& B : *br) all.insert(all.end(), {&B.conv, &B.rewrite, &B.drewrite, &B.convtr});
+    for (auto& B : *br) {
+      all.insert(all.end(), {&B.conv, &B.rewrite, &B.drewrite, &B.convtr});
+      for (auto* dv : {&B.edc, &B.ddc})
+        for (auto& L : *dv) all.push_back(&L.conv);
+    }
   all.insert(all.end(), {&m->up, &m->down, &m->up_t, &m->down_t});
   for (auto* tv : {&m->tl, &m->tlt})
     for (auto& L : *tv) all.insert(all.end(), {&L.qkv, &L.q, &L.kv, &L.out, &L.ff1, &L.ff2});
