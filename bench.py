@@ -40,7 +40,11 @@ import torch.distributed as dist  # noqa: E402
 SR = 44100
 CFG_DIR = os.path.join(REPO, "sesa-audio-separation_amd", "sesa", "configs")
 # model -> (config, algorithmic FLOP per chunk, dominant kernel class or None (= most kernel time))
-#   mdx23c / bs_roformer: FlopCounterMode on the reference.
+#   mdx23c: FlopCounterMode on the reference.
+#   bs_roformer: FlopCounterMode on the reference for the Linears (addmm 5039 + mm 2500 GFLOP) plus
+#          attention counted as 4 L^2 d per (sequence, head) -- QK^T + PV, the same definition the
+#          attention class uses (FlopCounterMode saw only 104 GFLOP of it through SDPA): time
+#          62 x 8 x 4 x 801^2 x 64 + freq 801 x 8 x 4 x 62^2 x 64, x 12 layers = 1053.3 GFLOP -> 8592.3 GFLOP.
 #   scnet: FlopCounterMode on oracle/scnet.py (LSTM matmuls written out): conv 118.3 + LSTM input proj
 #          128.4 + recurrence 128.4 + Linear 32.1 GFLOP per 485100-sample chunk.
 #   htdemucs: FlopCounterMode on oracle/htdemucs.py (pinned to the reference class): conv 173.5 +
@@ -49,7 +53,7 @@ CFG_DIR = os.path.join(REPO, "sesa-audio-separation_amd", "sesa", "configs")
 #          x 4 x 512 = 169.1 GFLOP -> 485.7 GFLOP per 485100-sample segment.
 MODELS = {
     "mdx23c": ("config_vocals_mdx23c.yaml", 2.4341e12, "conv3x3"),
-    "bs_roformer": ("config_bs_roformer_vocals.yaml", 7.6429e12, "tokgemm"),
+    "bs_roformer": ("config_bs_roformer_vocals.yaml", 8.5923e12, "tokgemm"),
     "scnet": ("config_musdb18_scnet.yaml", 4.072e11, "lstm"),
     "htdemucs": ("config_musdb18_htdemucs.yaml", 4.857e11, None),
 }
@@ -73,7 +77,7 @@ TRACK_SECONDS = {"htdemucs": 1800.0}
 # N=8 -> one forward of 22)
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
 KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)",
-         "tokgemm": "tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)",
+         "tokgemm": "tok_gemm_glds_kernel + tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)",
          "lstm": "scn_lstm_mfma_kernel (bi-LSTM recurrence, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "hconv": "tok_gemm_kernel<conv> (HTDemucs implicit-GEMM convolutions, v_mfma_f32_32x32x16_bf16)",
          "attn": "attn_kernel (flash attention, S^T = K Q^T, bf16x3 v_mfma_f32_32x32x16_bf16)"}
