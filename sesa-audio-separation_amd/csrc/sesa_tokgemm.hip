@@ -590,8 +590,21 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
         const int ml = (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         float x = v[r];
         if constexpr ((EP & EP_RS) != 0) x *= rs[ml];
-        x += bias[j];
-        if constexpr ((EP & EP_GELU) != 0) x = gelu_erf(x);
+        v[r] = x + bias[j];
+      }
+      if constexpr ((EP & EP_GELU) != 0) {
+        // two values per packed v_pk_fma_f32 sequence: this epilogue is VALU-issue-bound
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const f32x2 y = gelu_erf2(f32x2{v[r], v[r + 1]});
+          v[r] = y[0];
+          v[r + 1] = y[1];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float x = v[r];
         if constexpr ((EP & EP_ROPE) != 0) {
           const float partner = dpp_xor1(x);
           const float2 cs = lrope[ml * 32 + (d >> 1)];
@@ -667,10 +680,12 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // Flash attention, head dim 64, 4 waves x 32 queries per workgroup, 64-key blocks.
-// LDS images per block (bf16 hi / lo): K [64 key][64 d] and V^T [64 d][64 key'], 128-B rows with
-// the 16-B chunk index XOR-swizzled by ((row >> 1) & 7) (conflict-free ds_read_b128 groups).
-// key' permutes each 16-key group so the P^T registers of one lane are 8 consecutive key' slots:
-//   key_local = (j & 3) + 8 (j >> 2) + 4 hl  <->  key' = 8 hl + j.
+// LDS images per block (bf16 hi / lo): K [64 key][64 d] and V [64 key][64 d], 128-B rows with the
+// 16-B chunk index XOR-swizzled by ((row >> 1) & 7) (conflict-free ds_read_b128 groups), both written
+// with 8-byte stores.  The V^T A-fragments of O^T += V^T P^T are read with ds_read_b64_tr_b16 (a
+// transposing read: 16 lanes get 16 d-columns of 4 key rows), and the key each k-slot needs is chosen
+// in the read address, matching the S^T register layout of P^T:
+//   k-slot 8 h + 4 r + q of k-step ks  <->  key 32 (ks >> 1) + 16 (ks & 1) + 8 r + 4 h + q.
 constexpr int kHD = 64;
 constexpr int kKB = 64;
 
@@ -747,25 +762,35 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
     for (int i = 0; i < 4; ++i) {
       const int e = tid + i * kThreads;
       const int key = e >> 4, dq = (e & 15) * 4;
-      __bf16 hi[4], lo[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) split_bf16(kreg[i][q], hi[q], lo[q]);
-      const int off = swz(key, dq >> 3) + ((dq & 4) << 1);
-      *reinterpret_cast<uint2*>(Khi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
-      if (X3) *reinterpret_cast<uint2*>(Klo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
-      // V^T[d][key'] (2-byte scattered stores)
-      const int kl = key & 15;
-      const int kp = (key & ~15) + 8 * ((kl >> 2) & 1) + (kl & 3) + 4 * (kl >> 3);
+      __bf16 hi[4], lo[4], vh[4], vl[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        __bf16 vh, vl;
-        split_bf16(vreg[i][q], vh, vl);
-        const int d = dq + q;
-        const int voff = swz(d, kp >> 3) + ((kp & 7) << 1);
-        *reinterpret_cast<__bf16*>(Vhi + voff) = vh;
-        if (X3) *reinterpret_cast<__bf16*>(Vlo + voff) = vl;
+        split_bf16(kreg[i][q], hi[q], lo[q]);
+        split_bf16(vreg[i][q], vh[q], vl[q]);
+      }
+      const int off = swz(key, dq >> 3) + ((dq & 4) << 1);
+      *reinterpret_cast<uint2*>(Khi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
+      *reinterpret_cast<uint2*>(Vhi + off) = make_uint2(pack2(vh[0], vh[1]), pack2(vh[2], vh[3]));
+      if (X3) {
+        *reinterpret_cast<uint2*>(Klo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
+        *reinterpret_cast<uint2*>(Vlo + off) = make_uint2(pack2(vl[0], vl[1]), pack2(vl[2], vl[3]));
       }
     }
+  };
+  // V^T fragment of k-step ks, d-block db (see the image comment): two transposing reads
+  const int tg = lane >> 4, ti = lane & 15;
+  const int tr_q = ti >> 2, tp = ti & 3, th = tg >> 1;
+  auto vt_frag = [&](const char* V, int ks, int db) -> bf16x8 {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const int d = db * 32 + 16 * (tg & 1) + 4 * tp;
+    const int key0 = 32 * (ks >> 1) + 16 * (ks & 1) + 4 * th + tr_q;
+    // whole-vector assembly: element-wise short -> bf16 inserts miscompiled (every element became
+    // element 0; tools/tr_probe2.hip)
+    const bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) bf16x4*)(V + swz(key0, d >> 3) + ((d & 7) << 1)));
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) bf16x4*)(V + swz(key0 + 8, d >> 3) + ((d & 7) << 1)));
+    return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
   };
 
   const int n_blocks = (Lk + kKB - 1) / kKB;
@@ -838,11 +863,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
       }
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
-        const int d = db * 32 + l32;
-        const int off = swz(d, 2 * ks + hl);
-        const bf16x8 vh = *reinterpret_cast<const bf16x8*>(Vhi + off);
+        const bf16x8 vh = vt_frag(Vhi, ks, db);
         if (X3) {
-          const bf16x8 vl = *reinterpret_cast<const bf16x8*>(Vlo + off);
+          const bf16x8 vl = vt_frag(Vlo, ks, db);
           o[db] = mfma32(vl, ph, o[db]);
           o[db] = mfma32(vh, pl, o[db]);
         }
