@@ -411,9 +411,15 @@ __device__ __forceinline__ uint32_t dpp_xor1u(uint32_t x) {
 
 // EP: EP_RS (row scale) | EP_ROPE (rotary, dim_head 64) | EP_GELU | EP_RES (residual) | EP_SPLIT
 // (bf16 planes out); bias always (per group).  EP_RAW / EP_NONE: ablations for tools/tokgemm_bench.hip.
-template <int EP>
+// M16: v_mfma_f32_16x16x32_bf16 blocks (8 x 4 per wave, one k-step per 32-deep chunk) instead of
+// 32x32x16 (4 x 2, two k-steps); same wave tile, accumulator count and LDS images.
+template <int EP, bool M16 = false>
 __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
-  constexpr int NT = 512, BM = 256, BK = kTokBK, MI = 4, NI = 2, WN = 4;
+  constexpr int NT = 512, BM = 256, BK = kTokBK, WN = 4;
+  constexpr int BLK = M16 ? 16 : 32;                       // MFMA block edge
+  constexpr int MI = 128 / BLK, NI = 64 / BLK;             // blocks per 128 x 64 wave tile
+  constexpr int RPB = BLK * BLK / 64;                      // accumulator registers per block
+  using Acc = std::conditional_t<M16, f32x4, f32x16>;
   constexpr int ROWB = BK * 2;
   constexpr int A_BYTES = BM * ROWB;                       // 16 KiB per plane
   constexpr int A_REG = 2 * A_BYTES;
@@ -485,43 +491,50 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
     }
   };
 
-  f32x16 acc[MI][NI];
+  Acc acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < RPB; ++r) acc[i][j][r] = 0.f;
 
+  // fragment row / 16-B chunk of this lane: 32x32x16 -> row l32, chunk 2 ks + h (two k-steps per
+  // chunk); 16x16x32 -> row lane & 15, chunk lane >> 4 (one k-step)
+  const int frow = M16 ? (lane & 15) : l32;
   struct Frags {
     bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
   };
   auto read_frags = [&](Frags& f, const char* stg, int ks) {
-    const int q = ks * 2 + h;
+    const int q = M16 ? (lane >> 4) : ks * 2 + h;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      const int row = (wm * MI + i) * 32 + l32;
+      const int row = (wm * MI + i) * BLK + frow;
       const int off = row * ROWB + ((q ^ ((row >> 2) & 3)) << 4);
       f.ah[i] = *reinterpret_cast<const bf16x8*>(stg + off);
       f.al[i] = *reinterpret_cast<const bf16x8*>(stg + A_BYTES + off);
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int c = (wn * NI + j) * 32 + l32;               // 0..255
+      const int c = (wn * NI + j) * BLK + frow;             // 0..255
       const int r = c & (kTokBN - 1);
       const int off = A_REG + (c >> 7) * W_IMG + r * ROWB + ((q ^ ((r >> 2) & 3)) << 4);
       f.bh[j] = *reinterpret_cast<const bf16x8*>(stg + off);
       f.bl[j] = *reinterpret_cast<const bf16x8*>(stg + off + W_PLANE);
     }
   };
+  auto mma = [&](const bf16x8& x, const bf16x8& y, Acc& c) {
+    if constexpr (M16) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, c, 0, 0, 0);
+    else c = mfma32(x, y, c);
+  };
   auto mfmas = [&](const Frags& f) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        acc[i][j] = mfma32(f.al[i], f.bh[j], acc[i][j]);
-        acc[i][j] = mfma32(f.ah[i], f.bl[j], acc[i][j]);
-        acc[i][j] = mfma32(f.ah[i], f.bh[j], acc[i][j]);
+        mma(f.al[i], f.bh[j], acc[i][j]);
+        mma(f.ah[i], f.bl[j], acc[i][j]);
+        mma(f.ah[i], f.bh[j], acc[i][j]);
       }
   };
 
@@ -535,11 +548,17 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
     // chunk kc + 1 into the other stage: its last fragment reads (iteration kc - 1) were retired
     // by the lgkmcnt(0) before that iteration's barrier
     if (kc + 1 < n_chunks) issue(kc + 1, smem + ((kc + 1) & 1) * STAGE);
-    Frags f0, f1;
-    read_frags(f0, cur, 0);
-    read_frags(f1, cur, 1);
-    mfmas(f0);
-    mfmas(f1);
+    if constexpr (M16) {
+      Frags f0;
+      read_frags(f0, cur, 0);
+      mfmas(f0);
+    } else {
+      Frags f0, f1;
+      read_frags(f0, cur, 0);
+      read_frags(f1, cur, 1);
+      mfmas(f0);
+      mfmas(f1);
+    }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -572,22 +591,25 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   float bias[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int n = n0 + (wn * NI + j) * 32 + l32;
+    const int n = n0 + (wn * NI + j) * BLK + (M16 ? (lane & 15) : l32);
     bias[j] = (g.b_off >= 0 && n < g.N) ? a.bias[g.b_off + n] : 0.f;
   }
-  // one 32x32 block: FULL = no row / column guards
+  auto row_of = [&](int i, int r) -> int {
+    return M16 ? (wm * MI + i) * 16 + 4 * (lane >> 4) + r : (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+  };
+  // one MFMA block: FULL = no row / column guards; row of accumulator register r of block i
   auto block = [&](auto I, auto J, auto P, auto FULLT) {
     constexpr int i = decltype(I)::value, j = decltype(J)::value, p = decltype(P)::value;
     constexpr bool FULL = decltype(FULLT)::value;
-    const int nl = (wn * NI + j) * 32 + l32;
+    const int nl = (wn * NI + j) * BLK + (M16 ? (lane & 15) : l32);
     const int n = n0 + nl;
-    f32x16 v = acc[i][j];
+    Acc v = acc[i][j];
     if constexpr ((EP & EP_RAW) == 0) {
       const int d = n & 63;
       const bool rot = n < a.rope_cols;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ml = (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      for (int r = 0; r < RPB; ++r) {
+        const int ml = row_of(i, r);
         float x = v[r];
         if constexpr ((EP & EP_RS) != 0) x *= rs[ml];
         v[r] = x + bias[j];
@@ -595,15 +617,15 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
       if constexpr ((EP & EP_GELU) != 0) {
         // two values per packed v_pk_fma_f32 sequence: this epilogue is VALU-issue-bound
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
+        for (int r = 0; r < RPB; r += 2) {
           const f32x2 y = gelu_erf2(f32x2{v[r], v[r + 1]});
           v[r] = y[0];
           v[r + 1] = y[1];
         }
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ml = (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      for (int r = 0; r < RPB; ++r) {
+        const int ml = row_of(i, r);
         float x = v[r];
         if constexpr ((EP & EP_ROPE) != 0) {
           const float partner = dpp_xor1(x);
@@ -615,13 +637,12 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
         v[r] = x;
       }
     }
-    const int rb = m0 + (wm * MI + i) * 32 + 4 * h;
     if constexpr ((EP & EP_SPLIT) != 0) {
       // bf16 planes, two columns per 4-byte store: even lanes write the hi pair (n, n + 1), odd
       // lanes the lo pair (n - 1, n)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = rb + (r & 3) + 8 * (r >> 2);
+      for (int r = 0; r < RPB; ++r) {
+        const int m = m0 + row_of(i, r);
         __bf16 hi, lo;
         split_bf16(v[r], hi, lo);
         const uint32_t hb = __builtin_bit_cast(uint16_t, hi), lb = __builtin_bit_cast(uint16_t, lo);
@@ -639,14 +660,14 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = rb + (r & 3) + 8 * (r >> 2);
+      for (int r = 0; r < RPB; ++r) {
+        const int m = m0 + row_of(i, r);
         if (FULL || (m < a.M && n < g.N)) a.out[(int64_t)m * a.o_ld + g.o_off + n] = v[r];
       }
     }
   };
   auto run = [&](auto FULLT) {
-    Unroll<0, 2>::run([&](auto P) {                        // row half p: blocks i = 2p, 2p + 1
+    Unroll<0, 2>::run([&](auto P) {                        // row half p
       constexpr int p = decltype(P)::value;
       if constexpr ((EP & EP_RES) != 0) {
         if (p == 1) {                                      // every wave is done with half 0
@@ -669,7 +690,7 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
       }
-      Unroll<2 * p, 2 * p + 2>::run([&](auto I) {
+      Unroll<p * (MI / 2), (p + 1) * (MI / 2)>::run([&](auto I) {   // the blocks of rows wm 128 + p 64 ..
         Unroll<0, NI>::run([&](auto J) { block(I, J, P, FULLT); });
       });
     });
@@ -965,18 +986,19 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
            (a.residual ? EP_RES : 0) | (a.out_hi ? EP_SPLIT : 0);
     }
     const dim3 gbig((unsigned)(((a.M + 255) / 256) * ((a.n_tiles_n + 1) / 2)), (unsigned)a.n_groups);
+    static const int m16 = getenv("SESA_TOKGEMM_M16") ? atoi(getenv("SESA_TOKGEMM_M16")) : 1;
+#define SESA_GLDS(EPV)                                                                                 \
+  if (m16) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true>), gbig, dim3(512), 0, st, a);            \
+  else hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, false>), gbig, dim3(512), 0, st, a);
     switch (ep) {
-      case 0: hipLaunchKernelGGL(tok_gemm_glds_kernel<0>, gbig, dim3(512), 0, st, a); break;
-      case EP_RS | EP_ROPE: hipLaunchKernelGGL(tok_gemm_glds_kernel<EP_RS | EP_ROPE>, gbig, dim3(512), 0, st, a); break;
-      case EP_RES: hipLaunchKernelGGL(tok_gemm_glds_kernel<EP_RES>, gbig, dim3(512), 0, st, a); break;
-      case EP_RS | EP_GELU | EP_SPLIT:
-        hipLaunchKernelGGL(tok_gemm_glds_kernel<EP_RS | EP_GELU | EP_SPLIT>, gbig, dim3(512), 0, st, a);
-        break;
-      case EP_GELU | EP_SPLIT:
-        hipLaunchKernelGGL(tok_gemm_glds_kernel<EP_GELU | EP_SPLIT>, gbig, dim3(512), 0, st, a);
-        break;
+      case 0: SESA_GLDS(0) break;
+      case EP_RS | EP_ROPE: SESA_GLDS(EP_RS | EP_ROPE) break;
+      case EP_RES: SESA_GLDS(EP_RES) break;
+      case EP_RS | EP_GELU | EP_SPLIT: SESA_GLDS(EP_RS | EP_GELU | EP_SPLIT) break;
+      case EP_GELU | EP_SPLIT: SESA_GLDS(EP_GELU | EP_SPLIT) break;
       default: ep = -1;
     }
+#undef SESA_GLDS
     if (ep >= 0) {
       SESA_CHECK_LAUNCH();
       return SESA_OK;

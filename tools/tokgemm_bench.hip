@@ -158,8 +158,56 @@ int main(int argc, char** argv) {
     a1.residual = nullptr;
     rep("v0 reg-staged 128x128", time_ms([&] { hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, false, true>), gv0, dim3(256), 0, 0, a); }));
     rep("glds 256x256 (launch_tok_gemm)", time_ms([&] { launch_tok_gemm(a, 1, 0); }));
-    rep("glds 256x256 raw store", time_ms([&] { hipLaunchKernelGGL((tok_gemm_glds_kernel<EP_RAW>), gbig, dim3(512), 0, 0, a1); }));
-    rep("glds 256x256 no epilogue", time_ms([&] { hipLaunchKernelGGL((tok_gemm_glds_kernel<EP_NONE>), gbig, dim3(512), 0, 0, a1); }));
+    {
+      setenv("SESA_TOKGEMM_M16", "1", 1);   // read once per process: time the M16 instantiation directly
+      const int ep = (sh.rownorm ? EP_RS : 0) | (sh.rope ? EP_ROPE : 0) | (sh.act == TOK_ACT_GELU ? EP_GELU : 0) |
+                     (sh.resid ? EP_RES : 0) | (sh.split_out ? EP_SPLIT : 0);
+      auto l16 = [&] {
+        switch (ep) {
+          case EP_RS | EP_ROPE: hipLaunchKernelGGL((tok_gemm_glds_kernel<EP_RS | EP_ROPE, true>), gbig, dim3(512), 0, 0, a); break;
+          case EP_RES: hipLaunchKernelGGL((tok_gemm_glds_kernel<EP_RES, true>), gbig, dim3(512), 0, 0, a); break;
+          default: hipLaunchKernelGGL((tok_gemm_glds_kernel<EP_RS | EP_GELU | EP_SPLIT, true>), gbig, dim3(512), 0, 0, a);
+        }
+      };
+      rep("glds 16x16x32", time_ms(l16));
+      rep("glds 16x16x32 no epilogue", time_ms([&] { hipLaunchKernelGGL((tok_gemm_glds_kernel<EP_NONE, true>), gbig, dim3(512), 0, 0, a1); }));
+      {  // plain epilogue (bias only): main-loop agreement
+        TokGemmArgs p0 = a, p1 = a;
+        p0.rope = p1.rope = nullptr;
+        p0.rownorm = p1.rownorm = 0;
+        p0.residual = p1.residual = nullptr;
+        p0.out_hi = p1.out_hi = nullptr;
+        p0.out_lo = p1.out_lo = nullptr;
+        p0.act = p1.act = TOK_ACT_NONE;
+        p1.out = out2;
+        hipLaunchKernelGGL((tok_gemm_glds_kernel<0, true>), gbig, dim3(512), 0, 0, p0);
+        hipLaunchKernelGGL((tok_gemm_glds_kernel<0, false>), gbig, dim3(512), 0, 0, p1);
+        CK(hipDeviceSynchronize());
+        std::vector<float> h1((size_t)M * sh.N), h2((size_t)M * sh.N);
+        CK(hipMemcpy(h1.data(), out, h1.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h2.data(), out2, h2.size() * 4, hipMemcpyDeviceToHost));
+        double md = 0;
+        size_t wq = 0;
+        for (size_t q = 0; q < h1.size(); ++q)
+          if (fabsf(h1[q] - h2[q]) > md) { md = fabsf(h1[q] - h2[q]); wq = q; }
+        printf("     plain: max |m16 - 32x32| = %.3g at row %zu col %zu (%g vs %g)\n", md, wq / sh.N, wq % sh.N, h1[wq], h2[wq]);
+      }
+      // cross-check M16 vs 32x32 on the fp32 outputs
+      if (!sh.split_out && !sh.resid) {
+        TokGemmArgs a2 = a;
+        a2.out = out2;
+        l16();
+        hipLaunchKernelGGL((tok_gemm_glds_kernel<EP_RS | EP_ROPE, false>), gbig, dim3(512), 0, 0, a2);
+        CK(hipDeviceSynchronize());
+        std::vector<float> h1((size_t)M * sh.N), h2((size_t)M * sh.N);
+        CK(hipMemcpy(h1.data(), out, h1.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h2.data(), out2, h2.size() * 4, hipMemcpyDeviceToHost));
+        double md = 0;
+        for (size_t q = 0; q < h1.size(); ++q) md = std::max(md, (double)fabsf(h1[q] - h2[q]));
+        printf("     max |m16 - 32x32| = %.3g\n", md);
+      }
+    }
+    rep("glds 256x256 raw store", time_ms([&] { hipLaunchKernelGGL((tok_gemm_glds_kernel<EP_RAW, false>), gbig, dim3(512), 0, 0, a1); }));
     rep("v0 bf16 (1 pass)", time_ms([&] { hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, false, true>), gv0, dim3(256), 0, 0, a); }));
     // cross-check v0 vs glds on the full epilogue (fp32 out, or hi + lo planes; residual = 1)
     {
