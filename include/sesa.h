@@ -126,6 +126,12 @@ int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, float* out, v
                         size_t workspace_bytes, void* stream);
 int sesa_mdx23c_destroy(sesa_mdx23c* m);
 
+/* Kernel choice for the TFC 3x3 convolutions at T >= 32 (process-wide; returns the previous value):
+ * 0 = conv3x3_db_kernel (default; v_mfma_f32_32x32x16_bf16, register-staged double buffer),
+ * 1 = conv3x3_m16_kernel (v_mfma_f32_16x16x32_bf16, persistent, LDS-DMA; measured on par).
+ * Initialised from SESA_CONV_VARIANT=m16.  A forward picks it up at its next call. */
+int sesa_mdx23c_set_conv_variant(int variant);
+
 /* ---------------------------------------------------------------------------------------
  * BS-Roformer (models/bs_roformer/bs_roformer.py:327-587, BSRoformer)
  * and Mel-Band-Roformer (same engine, `mel` fields below).

@@ -351,16 +351,28 @@ struct Fwd {
 
   // One act_split pass: GELU(InstanceNorm_affine(a [++ b])) -> bf16 hi/lo planes, returned as the
   // single pre-activated source its convolution consumes.
-  GemmIn act(Tensor a, Tensor b, const Norm* nrm, int T, int F) {
+  // raw (optional): also split the untransformed input into planes, returned as a SRC_PRE source (the
+  // fused 1x1 shortcut operand of conv3x3_m16_kernel).
+  GemmIn act(Tensor a, Tensor b, const Norm* nrm, int T, int F, GemmIn* raw = nullptr) {
     const int C = a.C + (b.C > 0 ? b.C : 0);
     const int64_t n = (int64_t)B * T * F * C;
     uint16_t* hi = reinterpret_cast<uint16_t*>(buf((n + 1) / 2));
     uint16_t* lo = reinterpret_cast<uint16_t*>(buf((n + 1) / 2));
+    uint16_t* rhi = raw ? reinterpret_cast<uint16_t*>(buf((n + 1) / 2)) : nullptr;
+    uint16_t* rlo = raw ? reinterpret_cast<uint16_t*>(buf((n + 1) / 2)) : nullptr;
     const GemmIn src = input(a, b, SRC_NORM_GELU, SRC_NORM_GELU, nrm, T, F);
     if (!dry && !rc) {
       void* tok = profile_begin(st);
-      rc = launch_act_split(src, (int64_t)T * F, B, hi, lo, st);
-      profile_end(tok, st, SESA_KCLASS_ACT, 8.0 * n);
+      rc = launch_act_split(src, (int64_t)T * F, B, hi, lo, st, rhi, rlo);
+      profile_end(tok, st, SESA_KCLASS_ACT, (raw ? 12.0 : 8.0) * n);
+    }
+    if (raw) {
+      *raw = GemmIn{};
+      raw->src[0] = Src{nullptr, nullptr, nullptr, C, SRC_PRE, rhi, rlo};
+      raw->src[1] = raw->src[0];
+      raw->C_split = C;
+      raw->C_in = C;
+      raw->inv_count = src.inv_count;
     }
     GemmIn in{};
     in.src[0] = Src{nullptr, nullptr, nullptr, C, SRC_PRE, hi, lo};
@@ -386,15 +398,18 @@ struct Fwd {
       double* st_u = stats(c);
       double* st_h2 = stats(c);
       double* st_out = stats(c);
-      // x = tfc1(x)
-      conv(bk.conv1, act(x0, x1, &bk.tfc1, L.T, L.F), L.T, L.F, L.T, L.F, H, nullptr, st_h1, 0);
+      // x = tfc1(x); the shortcut's operand is split here too when conv2 runs on conv3x3_m16_kernel
+      const bool pre_sc = conv3x3_m16_selected(L.T, c, c, x0.C + (x1.C > 0 ? x1.C : 0));
+      GemmIn xs{};
+      conv(bk.conv1, act(x0, x1, &bk.tfc1, L.T, L.F, pre_sc ? &xs : nullptr), L.T, L.F, L.T, L.F, H, nullptr, st_h1,
+           0);
       // x = x + tdf(x)
       tdf(bk.lin1, input(Tensor{H, st_h1, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf0, L.T, L.F), L.T, U, nullptr, st_u,
           c, 0);
       tdf(bk.lin2, input(Tensor{U, st_u, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf3, L.T, L.F / bnf), L.T, H, H, st_h2,
           c, 1);
       // x = tfc2(x) + shortcut(block input): the 1x1 shortcut rides along as extra K (raw input)
-      const GemmIn xs = input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F);
+      if (!pre_sc) xs = input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F);
       conv(bk.conv2, act(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F), L.T, L.F, L.T, L.F, S, nullptr, st_out, 0,
            &xs);
       x0 = Tensor{S, st_out, c};
@@ -648,3 +663,5 @@ extern "C" int sesa_mdx23c_destroy(sesa_mdx23c* m) {
   delete m;
   return SESA_OK;
 }
+
+extern "C" int sesa_mdx23c_set_conv_variant(int variant) { return set_conv3x3_variant(variant); }

@@ -83,37 +83,96 @@ __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
 
-// 4096-point radix-4 Stockham FFT over LDS (x -> result in the returned buffer).
-// INV: conjugated twiddles and +i rotation (un-normalised inverse).
+// 4096-point radix-16 Stockham FFT: 3 stages (16^3), one 16-point DFT per thread per stage, held in
+// registers (a radix-4 x radix-4 decomposition), 4 barriers instead of 7.  The first two stages write
+// a padded image (index i stored at i + i / 16: the stride-16 store pattern of a stage is then
+// bank-conflict free); the last stage writes natural order into `out`.
+// `in` holds natural order; `pad` and `out` are distinct buffers of kFFTPad float2.  INV: conjugated
+// twiddles (un-normalised inverse).
+constexpr int kFFTPad = kFFT + kFFT / 16;
+
 template <bool INV>
-__device__ float2* fft4096(float2* x, float2* y, const float2* __restrict__ tw) {
-  int n = kFFT, s = 1;
-#pragma unroll 1
-  for (int stage = 0; stage < 6; ++stage) {
-    const int m = n >> 2;
-    __syncthreads();
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+  const float2 s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = csub(a1, a3);
+  // forward: y1 = d02 - i d13, y3 = d02 + i d13; inverse: the conjugate rotation
+  const float2 jd13 = INV ? make_float2(-d13.y, d13.x) : make_float2(d13.y, -d13.x);
+  a0 = cadd(s02, s13);
+  a2 = csub(s02, s13);
+  a1 = cadd(d02, jd13);
+  a3 = csub(d02, jd13);
+}
+
+// in-register 16-point DFT: v[r] (r = 4 r1 + r2) -> v[k1 + 4 k2] = X[k1 + 4 k2]
+template <bool INV>
+__device__ __forceinline__ void dft16(float2 (&v)[16]) {
+  // omega_16^j, j = 0..9 (forward: exp(-2 pi i j / 16))
+  constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, C2 = 0.70710678118654752f;
+  const float sg = INV ? 1.f : -1.f;
+  const float2 w16[10] = {make_float2(1.f, 0.f),       make_float2(C1, sg * S1),  make_float2(C2, sg * C2),
+                          make_float2(S1, sg * C1),     make_float2(0.f, sg * 1.f), make_float2(-S1, sg * C1),
+                          make_float2(-C2, sg * C2),    make_float2(-C1, sg * S1), make_float2(-1.f, 0.f),
+                          make_float2(-C1, -sg * S1)};
+  float2 b[16];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int bfly = threadIdx.x + r * kThreads;  // 1024 butterflies per stage
-      const int q = bfly & (s - 1);
-      const int p = bfly >> __builtin_ctz(s);
-      float2 a = x[q + s * p], b = x[q + s * (p + m)], c = x[q + s * (p + 2 * m)], d = x[q + s * (p + 3 * m)];
-      float2 w1 = tw[p * s], w2 = tw[2 * p * s], w3 = tw[3 * p * s];
-      if (INV) { w1 = cconj(w1); w2 = cconj(w2); w3 = cconj(w3); }
-      float2 apc = cadd(a, c), amc = csub(a, c), bpd = cadd(b, d), bmd = csub(b, d);
-      // forward: -i*(b-d); inverse: +i*(b-d)
-      float2 jbmd = INV ? make_float2(-bmd.y, bmd.x) : make_float2(bmd.y, -bmd.x);
-      y[q + s * (4 * p + 0)] = cadd(apc, bpd);
-      y[q + s * (4 * p + 1)] = cmul(w1, cadd(amc, jbmd));
-      y[q + s * (4 * p + 2)] = cmul(w2, csub(apc, bpd));
-      y[q + s * (4 * p + 3)] = cmul(w3, csub(amc, jbmd));
-    }
-    float2* t = x; x = y; y = t;
-    n = m;
-    s <<= 2;
+  for (int r2 = 0; r2 < 4; ++r2) {  // 4-point DFTs over r1 -> B[r2][k1]
+    float2 a0 = v[r2], a1 = v[4 + r2], a2 = v[8 + r2], a3 = v[12 + r2];
+    dft4<INV>(a0, a1, a2, a3);
+    b[r2 * 4 + 0] = a0;
+    b[r2 * 4 + 1] = r2 ? cmul(a1, w16[r2]) : a1;
+    b[r2 * 4 + 2] = r2 ? cmul(a2, w16[2 * r2]) : a2;
+    b[r2 * 4 + 3] = r2 ? cmul(a3, w16[3 * r2]) : a3;
   }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {  // 4-point DFTs over r2 -> X[k1 + 4 k2]
+    float2 a0 = b[k1], a1 = b[4 + k1], a2 = b[8 + k1], a3 = b[12 + k1];
+    dft4<INV>(a0, a1, a2, a3);
+    v[k1] = a0;
+    v[k1 + 4] = a1;
+    v[k1 + 8] = a2;
+    v[k1 + 12] = a3;
+  }
+}
+
+__device__ __forceinline__ int padi(int i) { return i + (i >> 4); }
+
+// X: input, natural order (kFFT float2); Y: result, natural order.  Both kFFTPad float2 (X holds
+// the padded stage-2 image in between).
+template <bool INV>
+__device__ void fft4096(float2* X, float2* Y, const float2* __restrict__ tw) {
+  static_assert(kThreads == 256, "one 16-point butterfly per thread per stage");
+  const int b = threadIdx.x;
+  float2 v[16];
+  // stage 1 (s = 1, p = b): X[b + 256 r] -> Y'[16 b + k] * tw[k b]
   __syncthreads();
-  return x;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = X[b + 256 * r];
+  dft16<INV>(v);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    float2 w = tw[k * b];
+    if (INV) w = cconj(w);
+    Y[padi(16 * b + k)] = k ? cmul(v[k], w) : v[k];
+  }
+  // stage 2 (s = 16, q = b & 15, p = b >> 4): Y'[q + 16 (p + 16 r)] -> X'[q + 16 (16 p + k)] * tw[16 k p]
+  __syncthreads();
+  const int q = b & 15, p = b >> 4;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = Y[padi(q + 16 * (p + 16 * r))];
+  dft16<INV>(v);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    float2 w = tw[16 * k * p];
+    if (INV) w = cconj(w);
+    X[padi(q + 16 * (16 * p + k))] = k ? cmul(v[k], w) : v[k];
+  }
+  // stage 3 (s = 256, p = 0): X'[b + 256 r] -> Y[b + 256 k] (natural order, no twiddle)
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = X[padi(b + 256 * r)];
+  dft16<INV>(v);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) Y[b + 256 * k] = v[k];
+  __syncthreads();
 }
 
 // Output layouts of the forward transform.
@@ -124,8 +183,8 @@ __global__ void __launch_bounds__(kThreads)
 stft_kernel(const float* __restrict__ x, int len, int hop, int frames, int dim_f, int layout, int nsub,
             const float2* __restrict__ tw, const float2* __restrict__ twN, const float* __restrict__ win,
             float* __restrict__ out) {
-  __shared__ float2 bufA[kFFT];
-  __shared__ float2 bufB[kFFT];
+  __shared__ float2 bufA[kFFTPad];
+  __shared__ float2 bufB[kFFTPad];
   const int t = blockIdx.x;
   const int sig = blockIdx.y;
   const float* xs = x + (int64_t)sig * len;
@@ -142,26 +201,44 @@ stft_kernel(const float* __restrict__ x, int len, int hop, int frames, int dim_f
     }
     bufA[m] = make_float2(v[0], v[1]);
   }
-  float2* Z = fft4096<false>(bufA, bufB, tw);
-  const int Fs = dim_f / nsub;
-  for (int k = threadIdx.x; k < dim_f; k += kThreads) {
+  fft4096<false>(bufA, bufB, tw);
+  const float2* Z = bufB;
+  auto bin = [&](int k) {  // real-spectrum split X[k] = E[k] + W_N^k O[k]
     const float2 zk = Z[k & (kFFT - 1)];
     const float2 zm = cconj(Z[(kFFT - k) & (kFFT - 1)]);
     const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y + zm.y));
     const float2 D = csub(zk, zm);                         // O = D / (2i) = (D.y, -D.x)/2
     const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
-    const float2 X = cadd(E, cmul(twN[k], O));
-    if (layout == 0) {
-      float* o = out + ((int64_t)sig * 2) * dim_f * frames;
+    return cadd(E, cmul(twN[k], O));
+  };
+  if (layout == 0) {
+    float* o = out + ((int64_t)sig * 2) * dim_f * frames;
+    for (int k = threadIdx.x; k < dim_f; k += kThreads) {
+      const float2 X = bin(k);
       o[(int64_t)k * frames + t] = X.x;
       o[((int64_t)dim_f + k) * frames + t] = X.y;
-    } else {
-      const int b = sig >> 1, s = sig & 1;
-      const int sub = k / Fs, col = k - sub * Fs;
-      const int C = 4 * nsub;
-      float* o = out + (((int64_t)b * frames + t) * Fs + col) * C;
-      o[(s * 2 + 0) * nsub + sub] = X.x;
-      o[(s * 2 + 1) * nsub + sub] = X.y;
+    }
+  } else {
+    // one thread per column: this signal's 2 * nsub channels of the record are contiguous
+    // ((s * 2 + r) * nsub + sub), written as 16-B stores when nsub == 4
+    const int Fs = dim_f / nsub;
+    const int b = sig >> 1, s = sig & 1;
+    const int C = 4 * nsub;
+    for (int col = threadIdx.x; col < Fs; col += kThreads) {
+      float* o = out + (((int64_t)b * frames + t) * Fs + col) * C + s * 2 * nsub;
+      if (nsub == 4) {
+        float2 X[4];
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub) X[sub] = bin(sub * Fs + col);
+        reinterpret_cast<float4*>(o)[0] = make_float4(X[0].x, X[1].x, X[2].x, X[3].x);
+        reinterpret_cast<float4*>(o)[1] = make_float4(X[0].y, X[1].y, X[2].y, X[3].y);
+      } else {
+        for (int sub = 0; sub < nsub; ++sub) {
+          const float2 X = bin(sub * Fs + col);
+          o[sub] = X.x;
+          o[nsub + sub] = X.y;
+        }
+      }
     }
   }
 }
@@ -176,31 +253,39 @@ __global__ void __launch_bounds__(kThreads)
 istft_frames_kernel(const float* __restrict__ spec, int frames, int dim_f, int layout, int nsub, int ni,
                     const float2* __restrict__ tw, const float2* __restrict__ twN, const float* __restrict__ win,
                     float* __restrict__ frame_ws) {
-  __shared__ float2 bufA[kFFT];
-  __shared__ float2 bufB[kFFT];
+  __shared__ float2 bufA[kFFTPad];
+  __shared__ float2 bufB[kFFTPad];
   float2* Xs = bufB;  // bins 0..4095; bin 4096 (Nyquist) is always the zero pad (dim_f <= 4096)
   const int t = blockIdx.x;
   const int sig = blockIdx.y;
-  const int Fs = dim_f / nsub;
-  for (int k = threadIdx.x; k < kFFT; k += kThreads) {
-    float2 X = make_float2(0.f, 0.f);
-    if (k < dim_f) {
-      if (layout == 0) {
-        const float* sp = spec + ((int64_t)sig * 2) * dim_f * frames;
-        X = make_float2(sp[(int64_t)k * frames + t], sp[((int64_t)dim_f + k) * frames + t]);
+  if (layout == 0) {
+    const float* sp = spec + ((int64_t)sig * 2) * dim_f * frames;
+    for (int k = threadIdx.x; k < kFFT; k += kThreads)
+      Xs[k] = k < dim_f ? make_float2(sp[(int64_t)k * frames + t], sp[((int64_t)dim_f + k) * frames + t])
+                        : make_float2(0.f, 0.f);
+  } else {
+    // one thread per column: the signal's 2 * nsub channels ((instr * 2 + s) * 2 + r) * nsub + sub are
+    // contiguous in the record (16-B loads when nsub == 4)
+    const int Fs = dim_f / nsub;
+    const int s = sig & 1, bi = sig >> 1;
+    const int b = bi / ni, instr = bi - b * ni;
+    const int C = ni * 4 * nsub;
+    for (int col = threadIdx.x; col < Fs; col += kThreads) {
+      const float* sp = spec + (((int64_t)b * frames + t) * Fs + col) * C + (instr * 2 + s) * 2 * nsub;
+      if (nsub == 4) {
+        const float4 re = reinterpret_cast<const float4*>(sp)[0], im = reinterpret_cast<const float4*>(sp)[1];
+        Xs[0 * Fs + col] = make_float2(re.x, im.x);
+        Xs[1 * Fs + col] = make_float2(re.y, im.y);
+        Xs[2 * Fs + col] = make_float2(re.z, im.z);
+        Xs[3 * Fs + col] = make_float2(re.w, im.w);
       } else {
-        const int s = sig & 1, bi = sig >> 1;
-        const int b = bi / ni, instr = bi - b * ni;
-        const int C = ni * 4 * nsub;
-        const int sub = k / Fs, col = k - sub * Fs;
-        const float* sp = spec + (((int64_t)b * frames + t) * Fs + col) * C;
-        const int ch = (instr * 2 + s) * 2;
-        X = make_float2(sp[(ch + 0) * nsub + sub], sp[(ch + 1) * nsub + sub]);
+        for (int sub = 0; sub < nsub; ++sub) Xs[sub * Fs + col] = make_float2(sp[sub], sp[nsub + sub]);
       }
     }
-    if (k == 0) X.y = 0.f;  // C2R ignores the imaginary part of DC
-    Xs[k] = X;
+    for (int k = dim_f + threadIdx.x; k < kFFT; k += kThreads) Xs[k] = make_float2(0.f, 0.f);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) Xs[0].y = 0.f;  // C2R ignores the imaginary part of DC
   __syncthreads();
   for (int k = threadIdx.x; k < kFFT; k += kThreads) {
     const float2 xk = Xs[k];
@@ -211,7 +296,8 @@ istft_frames_kernel(const float* __restrict__ spec, int frames, int dim_f, int l
     const float2 O = cmul(make_float2(0.5f * D.x, 0.5f * D.y), w);
     bufA[k] = make_float2(E.x - O.y, E.y + O.x);          // E + i O
   }
-  float2* z = fft4096<true>(bufA, bufB, tw);
+  fft4096<true>(bufA, bufB, tw);
+  const float2* z = bufB;
   float* fw = frame_ws + ((int64_t)sig * frames + t) * kNFFT;
   const float scale = 1.0f / (float)kFFT;
   for (int m = threadIdx.x; m < kFFT; m += kThreads) {

@@ -25,6 +25,9 @@
 // ds_read_b128 lane groups are bank-conflict free.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 #include "sesa_common.hpp"
@@ -740,6 +743,361 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   }
 }
 
+// Sum of a double over the 16 lanes of each DPP row (every lane of the row gets the sum): xor 1 and
+// xor 2 by quad_perm, then row_half_mirror (i <-> 7 - i) and row_mirror (i <-> 15 - i), each applied to
+// both 32-bit halves.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double row16_sum(double x) {
+  x += dpp_f64<0xB1>(x);   // quad_perm [1, 0, 3, 2]
+  x += dpp_f64<0x4E>(x);   // quad_perm [2, 3, 0, 1]
+  x += dpp_f64<0x141>(x);  // row_half_mirror
+  x += dpp_f64<0x140>(x);  // row_mirror
+  return x;
+}
+
+// ---------------------------------------------------------------------------------------------
+// conv3x3_m16_kernel: the TFC 3x3 convolutions (mdx23c_tfc_tdf_v3.py:104-112, 121-129) on
+// v_mfma_f32_16x16x32_bf16 -- the same cycles per FLOP as 32x32x16 but ~1.12x its FLOP/s under the
+// power limit (MI355X_MICROARCH.md, DVFS) -- as a PERSISTENT kernel with LDS-DMA staging.
+//   * Tile 16 rows (t) x 32 columns (f) x 64 output channels, 512 threads; wave w owns rows 2w, 2w+1:
+//     4 position blocks (row, 16-column half) x 4 channel blocks of 16x16.
+//   * K chunk = 16 input channels x 9 taps = 4.5 k-steps of 32: k-step s pairs taps 2s (lanes 0-31)
+//     and 2s+1 (lanes 32-63); tap 8 of an even chunk is read into registers by lanes 0-31 and paired
+//     with tap 8 of the next (odd) chunk, read by lanes 32-63 -- 9 full k-steps per chunk pair.
+//   * Each stage (halo 18x34 hi + lo, 9-tap weight image hi + lo = 76 KiB) is filled by
+//     global_load_lds_dwordx4 (lane-linear LDS destination; the host weight swizzle is undone in the
+//     per-lane source offset; out-of-image halo lanes read zeros past the buffer range), two stages,
+//     one counted wait + barrier per step.  Unswizzled 32-B position rows are conflict-free for the 16x16x32
+//     fragment pattern (lane groups of ds_read_b128 see 8 distinct positions x both halves).
+//   * Persistent: one workgroup per CU walks work items (b, tile, channel block) with stride
+//     gridDim.x; the DMA of the next item's first chunk is issued under the current item's last
+//     step, so no per-tile prologue is exposed, and the epilogue's stores drain under the next tile.
+//   * XTRA: the 1x1 shortcut (:126, :137) as extra K over the centre tap, read from bf16 hi / lo
+//     planes of the raw block input (act_split's second output), 32 channels per step.
+// EPI (ablation knob for tools/conv_bench.hip; the product uses 0): 1 = no statistics, 2 = no epilogue.
+
+template <bool X3, bool XTRA, int EPI = 0>
+__global__ void __launch_bounds__(512, 1) conv3x3_m16_kernel(ConvArgs a, int n_work) {
+  constexpr int TM = 16, BN = 64, HW = kTF + 2, NPOS = (TM + 2) * HW;
+  constexpr int A_IMG = ((NPOS * 32 + 1023) / 1024) * 1024;  // 20 KiB per plane (612 x 32 B, padded)
+  constexpr int W_IMG = 9 * BN * 32;                          // 18 KiB per plane
+  constexpr int STAGE = 2 * A_IMG + 2 * W_IMG;                // 76 KiB
+  constexpr int XA_IMG = TM * kTF * 64;                       // ext: 512 positions x 32 ch (32 KiB)
+  constexpr int XW_IMG = BN * 64;                             // ext: 64 channels x 32 ch (4 KiB)
+  constexpr int RED = 8 * BN * 2 * 8;                         // [wave][channel][sum, sumsq] fp64
+  static_assert(2 * XA_IMG + 2 * XW_IMG <= STAGE && 2 * STAGE + RED <= 163840, "LDS budget");
+  constexpr int NPL = X3 ? 2 : 1;                             // planes staged
+  constexpr int A_PC = A_IMG / 1024, W_PC = W_IMG / 1024, XA_PC = XA_IMG / 1024, XW_PC = XW_IMG / 1024;
+  constexpr int MAIN_PC = NPL * (A_PC + W_PC), EXT_PC = NPL * (XA_PC + XW_PC);
+  constexpr int W_CHUNK = 2 * 9 * BN * 16;                    // uint16 per packed (hi, lo) chunk image
+  constexpr int W1_CHUNK = 2 * BN * 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + RED];
+  double* red = reinterpret_cast<double*>(smem + 2 * STAGE);
+
+  const int tid = threadIdx.x;
+  int lane = tid & 63;  // re-materialised per step (below): keeps lane-derived addresses out of the hoisted set
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: piece loops and descriptors in SGPRs
+  int fr = lane & 15, q = lane >> 4;
+  const int tiles_f = a.F_out / kTF;
+  const int NB = (a.n_cols + BN - 1) / BN;
+  const int n_tiles = ((a.T_out + TM - 1) / TM) * tiles_f;
+  const int per_b = n_tiles * NB;
+  const int n_main = a.n_chunks;
+  const int n_ext = XTRA ? a.x_chunks / 2 : 0;
+  const int S = n_main + n_ext;
+  const Src src = pick_src(a.in, 0);
+  const int C = src.C;
+  const int64_t w_nb = (int64_t)n_main * W_CHUNK + (XTRA ? (int64_t)a.x_chunks * W1_CHUNK : 0);
+
+  struct Item {
+    int b, t0, f0, nb;
+  };
+  // XCD-aware order within a batch item (as tap_gemm_kernel): ids 8g + x .. share XCD x, and the NB
+  // channel blocks of a tile are 8 ids apart (same XCD, same round), so their input is read from L2
+  auto decode = [&](int w) {
+    Item it;
+    it.b = w / per_b;
+    const int id = w - it.b * per_b;
+    const int full = (n_tiles / 8) * 8 * NB;
+    int tile;
+    if (id < full) {
+      const int g = id / (8 * NB), r = id - g * 8 * NB;
+      tile = g * 8 + (r & 7);
+      it.nb = r >> 3;
+    } else {
+      const int r = id - full;
+      tile = (n_tiles / 8) * 8 + r / NB;
+      it.nb = r % NB;
+    }
+    it.t0 = (tile / tiles_f) * TM;
+    it.f0 = (tile % tiles_f) * kTF;
+    return it;
+  };
+
+  // ---- LDS-DMA issue of step s of item `it` into stage `stg` (wave-uniform piece loop) ----
+  // buffer_load ... lds through per-item buffer resources: 32-bit per-lane offsets, and an offset past
+  // num_records (out-of-image halo lanes) returns zeros, so padding costs no extra load or branch
+  constexpr uint32_t kOOB = 0x80000000u;
+  constexpr int kRsrcW3 = 0x00020000;  // raw buffer, gfx9 data format word
+  auto rsrc = [](const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, kRsrcW3);
+  };
+  auto dma = [](__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+  };
+  const uint32_t w_bytes = (uint32_t)(w_nb * 2);
+  auto issue = [&](const Item& it, int s, char* stg) {
+    const __amdgpu_buffer_rsrc_t rw = rsrc(a.w + (int64_t)it.nb * w_nb, w_bytes);
+    if (!XTRA || s < n_main) {
+      const int kc = s;
+      const int64_t item = (int64_t)it.b * a.T_in * a.F_in * C;
+      const uint32_t plane_bytes = (uint32_t)((int64_t)a.T_in * a.F_in * C * 2);
+      const __amdgpu_buffer_rsrc_t rh = rsrc(src.hi + item, plane_bytes);
+      const __amdgpu_buffer_rsrc_t rl = rsrc(src.lo + item, plane_bytes);
+#pragma unroll
+      for (int i = 0; i < (MAIN_PC + 7) / 8; ++i) {
+        const int pc = wave + 8 * i;
+        if (pc >= MAIN_PC) break;
+        if (pc < NPL * A_PC) {
+          const int plane = pc / A_PC, qq = pc - plane * A_PC;
+          const int u = qq * 64 + lane, p = u >> 1, hf = u & 1;
+          const int hr = p / HW, hc = p - hr * HW;
+          const int ti = it.t0 - 1 + hr, fi = it.f0 - 1 + hc;
+          const bool ok = p < NPOS && ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in;
+          const uint32_t voff = ok ? (uint32_t)(((ti * a.F_in + fi) * C + kc * kConvBK + 8 * hf) * 2) : kOOB;
+          dma(plane ? rl : rh, stg + plane * A_IMG + qq * 1024, voff);
+        } else {
+          const int pw = pc - NPL * A_PC;
+          const int plane = pw / W_PC, qq = pw - plane * W_PC;
+          const int u = qq * 64 + lane, e = u >> 1, hf = u & 1;
+          dma(rw, stg + 2 * A_IMG + plane * W_IMG + qq * 1024,
+              (uint32_t)((kc * W_CHUNK + plane * (W_CHUNK / 2) + 8 * (2 * e + (hf ^ ((e >> 3) & 1)))) * 2));
+        }
+      }
+    } else {
+      const int kx = s - n_main;  // 32-channel ext step over the shortcut planes
+      const int Cx = a.xin.C_in;
+      const int64_t item = (int64_t)it.b * a.T_in * a.F_in * Cx;
+      const uint32_t plane_bytes = (uint32_t)((int64_t)a.T_in * a.F_in * Cx * 2);
+      const __amdgpu_buffer_rsrc_t rh = rsrc(a.xin.src[0].hi + item, plane_bytes);
+      const __amdgpu_buffer_rsrc_t rl = rsrc(a.xin.src[0].lo + item, plane_bytes);
+#pragma unroll
+      for (int i = 0; i < (EXT_PC + 7) / 8; ++i) {
+        const int pc = wave + 8 * i;
+        if (pc >= EXT_PC) break;
+        if (pc < NPL * XA_PC) {
+          const int plane = pc / XA_PC, qq = pc - plane * XA_PC;
+          const int u = qq * 64 + lane, p = u >> 2, c16 = u & 3;
+          const int kq = c16 ^ (((p >> 3) & 1) << 1);  // 64-B rows: 16-B unit swizzle for 16x16x32 reads
+          const int ti = it.t0 + (p >> 5), fi = it.f0 + (p & 31);
+          const uint32_t voff = ti < a.T_in ? (uint32_t)(((ti * a.F_in + fi) * Cx + kx * 32 + 8 * kq) * 2) : kOOB;
+          dma(plane ? rl : rh, stg + plane * XA_IMG + qq * 1024, voff);
+        } else {
+          const int pw = pc - NPL * XA_PC;
+          const int plane = pw / XW_PC, qq = pw - plane * XW_PC;
+          const int u = qq * 64 + lane, n = u >> 2, c16 = u & 3;
+          const int kq = c16 ^ (((n >> 3) & 1) << 1);
+          const int hf = kq & 1;
+          dma(rw, stg + 2 * XA_IMG + plane * XW_IMG + qq * 1024,
+              (uint32_t)((n_main * W_CHUNK + (2 * kx + (kq >> 1)) * W1_CHUNK + plane * (W1_CHUNK / 2) +
+                          8 * (2 * n + (hf ^ ((n >> 3) & 1)))) *
+                         2));
+        }
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+  struct Frags {
+    bf16x8 ah[4], al[4], bh[4], bl[4];
+  };
+  // main-chunk fragments of tap `tap` (per lane) from stage stg
+  auto read_main = [&](Frags& f, const char* stg, int tap) {
+    const int dy = tap / 3, dx = tap - 3 * (tap / 3);
+    const int hf = q & 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wave * 2 + (i >> 1), col = (i & 1) * 16 + fr;
+      const int off = ((row + dy) * HW + col + dx) * 32 + hf * 16;
+      f.ah[i] = *reinterpret_cast<const bf16x8*>(stg + off);
+      if (X3) f.al[i] = *reinterpret_cast<const bf16x8*>(stg + A_IMG + off);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int off = 2 * A_IMG + (tap * BN + j * 16 + fr) * 32 + hf * 16;
+      f.bh[j] = *reinterpret_cast<const bf16x8*>(stg + off);
+      if (X3) f.bl[j] = *reinterpret_cast<const bf16x8*>(stg + W_IMG + off);
+    }
+  };
+  auto read_ext = [&](Frags& f, const char* stg) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = (wave * 2 + (i >> 1)) * 32 + (i & 1) * 16 + fr;
+      const int off = p * 64 + ((q ^ (((p >> 3) & 1) << 1)) << 4);
+      f.ah[i] = *reinterpret_cast<const bf16x8*>(stg + off);
+      if (X3) f.al[i] = *reinterpret_cast<const bf16x8*>(stg + XA_IMG + off);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = j * 16 + fr;
+      const int off = 2 * XA_IMG + n * 64 + ((q ^ (((n >> 3) & 1) << 1)) << 4);
+      f.bh[j] = *reinterpret_cast<const bf16x8*>(stg + off);
+      if (X3) f.bl[j] = *reinterpret_cast<const bf16x8*>(stg + XW_IMG + off);
+    }
+  };
+  // D = W x act^T: output channels are the MFMA rows, positions the columns, so lane l's 4 registers
+  // of block (i, j) are 4 consecutive channels (4 (l >> 4) .. + 3 of block j) at position l & 15 of
+  // block i -- one 16-byte store each in the epilogue
+  auto mfmas = [&](const Frags& f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (X3) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.bh[j], f.al[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.bl[j], f.ah[i], acc[i][j], 0, 0, 0);
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.bh[j], f.ah[i], acc[i][j], 0, 0, 0);
+      }
+  };
+
+  int w = blockIdx.x;
+  if (w >= n_work) return;  // (uniform per workgroup)
+  Item cur = decode(w);
+  issue(cur, 0, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  int g = 0;  // global step counter: stage parity
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int w_next = w + (int)gridDim.x;
+    for (int s = 0; s < S; ++s, ++g) {
+      lane = tid & 63;
+      asm volatile("" : "+v"(lane));
+      fr = lane & 15;
+      q = lane >> 4;
+      char* stg = smem + (g & 1) * STAGE;
+      char* oth = smem + ((g + 1) & 1) * STAGE;
+      const bool main_step = !XTRA || s < n_main;
+      if (main_step && (s & 1)) {
+        // the tap-8 k-step of the chunk pair (s - 1, s): lanes 0-31 read the even chunk, still in the
+        // other stage, lanes 32-63 this one; then one barrier before that stage is overwritten
+        Frags f;
+        read_main(f, (q >> 1) ? stg : oth, 8);
+        mfmas(f);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      // next step's DMA into the other stage (its last reads are retired by the barrier above, or for
+      // an even step by the previous step's wait + barrier)
+      {
+        const bool last = s + 1 >= S;  // (one issue site: it inlines to a lot of code)
+        if (!last || w_next < n_work) issue(last ? decode(w_next) : cur, last ? 0 : s + 1, oth);
+      }
+      if (main_step) {
+        Unroll<0, 4>::run([&](auto KS) {
+          constexpr int ks = decltype(KS)::value;
+          Frags f;
+          read_main(f, stg, 2 * ks + (q >> 1));
+          mfmas(f);
+        });
+      } else {
+        Frags f;
+        read_ext(f, stg);
+        mfmas(f);
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else {
+      // ---- epilogue: fp32 store (16 B per lane) + fp64 per-channel sum / sum-of-squares ----
+      const int C_out = a.out.C_out;
+      double ssum[4][4], ssq[4][4];  // [channel block j][channel 4 (l >> 4) + r]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = cur.nb * BN + j * 16 + 4 * q;  // C_out % 16 == 0 (conv3x3_m16_selected)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ssum[j][r] = 0.0;
+          ssq[j][r] = 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = cur.t0 + wave * 2 + (i >> 1);
+          const int f = cur.f0 + (i & 1) * 16 + fr;
+          if (co >= C_out || t >= a.T_out) continue;
+          *reinterpret_cast<f32x4*>(a.out.ptr + (((int64_t)cur.b * a.T_out + t) * a.F_out + f) * C_out + co) =
+              acc[i][j];
+          if constexpr (EPI == 1) continue;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double v = (double)acc[i][j][r];
+            ssum[j][r] += v;
+            ssq[j][r] = fma(v, v, ssq[j][r]);
+          }
+        }
+      }
+      if (EPI == 0 && a.out.stats) {
+        // sum over the 16 positions (lanes l & 15) of each lane group: DPP within rows of 16
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ssum[j][r] = row16_sum(ssum[j][r]);
+            ssq[j][r] = row16_sum(ssq[j][r]);
+          }
+        if (fr == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int n = j * 16 + 4 * q + r;
+              red[(wave * BN + n) * 2 + 0] = ssum[j][r];
+              red[(wave * BN + n) * 2 + 1] = ssq[j][r];
+            }
+        }
+        __syncthreads();
+        if (tid < BN) {
+          double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+          for (int wv = 0; wv < 8; ++wv) {
+            s0 += red[(wv * BN + tid) * 2 + 0];
+            s1 += red[(wv * BN + tid) * 2 + 1];
+          }
+          const int co = cur.nb * BN + tid;
+          if (co < C_out) {
+            double* st = a.out.stats + ((int64_t)cur.b * C_out + co) * 2;
+            atomicAdd(st + 0, s0);
+            atomicAdd(st + 1, s1);
+          }
+        }
+        // red is rewritten only after the next item's step barriers
+      }
+    }
+    w = w_next;
+    if (w >= n_work) break;
+    cur = decode(w);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // TDF linear (mdx23c_tfc_tdf_v3.py:113-120) as one GEMM per launch over all (b, t):
 //   D[m][n] = sum_k W[m][k] * act(X[k][n]),  n = (b, t, c) flattened over the whole batch.
@@ -878,12 +1236,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
         const float scale = csc[j], shift = csh[j];
         const bool okc = cvalid[j];
         __bf16 hi[4], lo[4];
+        float xv[4] = {breg[I][0][cc], breg[I][1][cc], breg[I][2][cc], breg[I][3][cc]};
+        if (src.mode == SRC_NORM_GELU) {
+          // packed pairs (v_pk_fma_f32): this staging is VALU-issue-bound and not overlapped with the
+          // workgroup's own MFMAs
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float x = breg[I][q][cc];
-          if (src.mode == SRC_NORM_GELU) x = (okc && k0 + 4 * g + q < a.K) ? gelu_erf(x * scale + shift) : 0.f;
-          split_bf16(x, hi[q], lo[q]);
+          for (int q = 0; q < 4; q += 2) {
+            const f32x2 y = gelu_erf2(__builtin_elementwise_fma(f32x2{xv[q], xv[q + 1]}, f32x2{scale, scale},
+                                                                f32x2{shift, shift}));
+            xv[q] = (okc && k0 + 4 * g + q < a.K) ? y[0] : 0.f;
+            xv[q + 1] = (okc && k0 + 4 * g + q + 1 < a.K) ? y[1] : 0.f;
+          }
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) split_bf16(xv[q], hi[q], lo[q]);
         const int off = j * ROWB + ((((g >> 1) ^ ((j >> 2) & 3))) << 4) + ((g & 1) << 3);
         *reinterpret_cast<uint2*>(Bhi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
         if (X3) *reinterpret_cast<uint2*>(Blo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
@@ -992,10 +1358,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
   const bool col_ok = ncol < n_total;
   const int64_t bt = ncol / C;
   const int c = (int)(ncol - bt * C);
-  for (int p = 0; p < BM / EPI_ROWS; ++p) {
+  // residual rows of pass p (they alias the output: each pass's rows are loaded before that pass's
+  // stores; pass p + 1's are issued right after pass p's stores, in flight over its LDS staging)
+  auto load_res = [&](f32x4 (&res)[ITEMS], int p) {
     const int row0 = mb * BM + p * EPI_ROWS;
-    // residual loads first (they alias the output, so they are issued before any store of this pass)
-    f32x4 res[ITEMS];
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
       const int rl = (tid + it * NT) / (BN / 4);
@@ -1004,6 +1370,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
                     ? *reinterpret_cast<const f32x4*>(a.out.residual + (bt * a.M + m) * C + c)
                     : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  };
+  f32x4 res[ITEMS];
+  load_res(res, 0);
+  Unroll<0, BM / EPI_ROWS>::run([&](auto P) {
+    constexpr int p = decltype(P)::value;
+    const int row0 = mb * BM + p * EPI_ROWS;
     __syncthreads();  // previous pass's stage reads (and the main loop's LDS reads) are done
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
@@ -1034,7 +1406,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
         ssq[q] = fma((double)v[q], (double)v[q], ssq[q]);
       }
     }
-  }
+    if constexpr (p + 1 < BM / EPI_ROWS) load_res(res, p + 1);  // in flight over the next pass's staging
+  });
   if (a.out.stats) {
     // threads tid, tid + 32, ... own the same 4 columns: reduce through LDS in fp64 (the stage
     // region, dead once every thread has passed the barrier below)
@@ -1076,8 +1449,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
 // 32-B pieces of a row (coalesced), with no per-item index division or LDS affine reads.  Four
 // positions' loads are issued before any is transformed; the GELU runs on packed float2 pairs.
 constexpr int kActUnroll = 4;
+// rhi / rlo (nullable): the raw (untransformed) input split to bf16 planes as well -- the fused 1x1
+// shortcut operand of conv3x3_m16_kernel, written while the input is in registers anyway.
 __global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t n_pos, int pos_per_block,
-                                                             uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+                                                             uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
+                                                             uint16_t* __restrict__ rhi, uint16_t* __restrict__ rlo) {
   __shared__ float sc_s[kMaxCin], sh_s[kMaxCin];
   const int b = blockIdx.y;
   build_affine(in, b, sc_s, sh_s);
@@ -1122,6 +1498,19 @@ __global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t 
       f32x2 v[4] = {f32x2{x[u][0][0], x[u][0][1]}, f32x2{x[u][0][2], x[u][0][3]}, f32x2{x[u][1][0], x[u][1][1]},
                     f32x2{x[u][1][2], x[u][1][3]}};
       uint32_t hw[4], lw[4];
+      const int64_t o = obase + p * C;
+      if (rhi) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          __bf16 h0, l0, h1, l1;
+          split_bf16(v[q][0], h0, l0);
+          split_bf16(v[q][1], h1, l1);
+          hw[q] = pack2(h0, h1);
+          lw[q] = pack2(l0, l1);
+        }
+        *reinterpret_cast<uint4*>(rhi + o) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+        *reinterpret_cast<uint4*>(rlo + o) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const f32x2 y = act ? gelu_erf2(__builtin_elementwise_fma(v[q], sc[q], sh[q])) : v[q];
@@ -1131,7 +1520,6 @@ __global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t 
         hw[q] = pack2(h0, h1);
         lw[q] = pack2(l0, l1);
       }
-      const int64_t o = obase + p * C;
       *reinterpret_cast<uint4*>(hi + o) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
       *reinterpret_cast<uint4*>(lo + o) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
     }
@@ -1157,6 +1545,43 @@ int launch_conv_t(int x3, const ConvArgs& a, int batch, hipStream_t st) {
 
 }  // namespace
 
+namespace {
+int cu_count() {
+  static int n[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+// SESA_CONV_VARIANT=m16 selects conv3x3_m16_kernel (measured on par with conv3x3_db_kernel -- see
+// DESIGN.md 4a -- while its shortcut operand costs act_split an extra plane write); default: db.
+std::atomic<int> g_conv_variant{-1};
+int conv_variant() {
+  int v = g_conv_variant.load(std::memory_order_relaxed);
+  if (v < 0) {
+    v = getenv("SESA_CONV_VARIANT") && std::string(getenv("SESA_CONV_VARIANT")) == "m16" ? 1 : 0;
+    int expect = -1;
+    g_conv_variant.compare_exchange_strong(expect, v);
+    v = g_conv_variant.load(std::memory_order_relaxed);
+  }
+  return v;
+}
+}  // namespace
+
+int set_conv3x3_variant(int v) {
+  const int prev = conv_variant();
+  g_conv_variant.store(v == 1 ? 1 : 0);
+  return prev;
+}
+
+bool conv3x3_m16_selected(int T_out, int C_in, int C_out, int C_shortcut) {
+  return conv_variant() == 1 && T_out >= 32 && C_in % 32 == 0 && C_out % 16 == 0 && C_shortcut % 32 == 0;
+}
+
 // Tile choices per kind (BN = 64 unless the GEMM N is <= 32).
 int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStream_t st) {
   SESA_REQUIRE(a.F_out % kTF == 0, SESA_ERR_INVALID, "conv: F_out %d not a multiple of %d", a.F_out, kTF);
@@ -1165,6 +1590,29 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
                kMaxCin);
   switch (kind) {
     case CONV3X3:
+      if (a.out.residual == nullptr && a.out.gelu == 0 &&
+          conv3x3_m16_selected(a.T_out, a.in.C_in, a.out.C_out, a.x_chunks > 0 ? a.xin.C_in : 0)) {
+        SESA_REQUIRE(a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && a.in.src[0].lo && a.in.C_split == a.in.C_in,
+                     SESA_ERR_INVALID, "conv3x3: needs a single pre-activated (act_split) input");
+        SESA_REQUIRE(a.x_chunks == 0 || (a.xin.src[0].mode == SRC_PRE && a.xin.src[0].hi && a.xin.src[0].lo &&
+                                         a.xin.C_split == a.xin.C_in && a.x_chunks * kConvBK == a.xin.C_in),
+                     SESA_ERR_INVALID, "conv3x3: the fused shortcut must be given as act_split raw planes");
+        SESA_REQUIRE(a.T_in == a.T_out && a.F_in == a.F_out && a.n_chunks * kConvBK == a.in.C_in, SESA_ERR_INVALID,
+                     "conv3x3: same-size convolution expected");
+        const int64_t n_work =
+            (int64_t)batch * ((a.T_out + 15) / 16) * (a.F_out / kTF) * ((a.n_cols + 63) / 64);
+        SESA_REQUIRE(n_work < (1ll << 31), SESA_ERR_INVALID, "conv3x3: too many work items");
+        const dim3 grid((unsigned)std::min<int64_t>(n_work, cu_count()));
+        if (a.x_chunks > 0) {
+          if (x3) hipLaunchKernelGGL((conv3x3_m16_kernel<true, true>), grid, dim3(512), 0, st, a, (int)n_work);
+          else hipLaunchKernelGGL((conv3x3_m16_kernel<false, true>), grid, dim3(512), 0, st, a, (int)n_work);
+        } else {
+          if (x3) hipLaunchKernelGGL((conv3x3_m16_kernel<true, false>), grid, dim3(512), 0, st, a, (int)n_work);
+          else hipLaunchKernelGGL((conv3x3_m16_kernel<false, false>), grid, dim3(512), 0, st, a, (int)n_work);
+        }
+        SESA_CHECK_LAUNCH();
+        return SESA_OK;
+      }
       if (a.T_out >= 32 && a.out.residual == nullptr && a.out.gelu == 0) {
         // double-buffered 16-row tile (levels with T >= 32); tile rows past T_out are masked
         SESA_REQUIRE(a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && a.in.src[0].lo && a.in.C_split == a.in.C_in,
@@ -1229,15 +1677,18 @@ int64_t tdf_u_floats(int64_t n_cols, int M) { return ((n_cols + 127) / 128) * 12
 int tdf_block_rows(int M) { return M > 128 ? 256 : M > 64 ? 128 : M > 32 ? 64 : 32; }
 
 
-int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st) {
+int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st,
+                     uint16_t* raw_hi, uint16_t* raw_lo) {
   SESA_REQUIRE(in.C_in % 16 == 0 && in.C_split % 8 == 0 && in.C_in <= kMaxCin, SESA_ERR_INVALID,
                "act_split: C %d must be a multiple of 16 (<= %d)", in.C_in, kMaxCin);
+  SESA_REQUIRE((raw_hi == nullptr) == (raw_lo == nullptr), SESA_ERR_INVALID, "act_split: raw planes come in pairs");
   // blockDim = groups * lanes_pos (every thread owns one 8-channel group); ~32 positions per thread
   const int groups = in.C_in / 8;
   const int lanes_pos = groups >= kThreads ? 1 : kThreads / groups;
   const int ppb = lanes_pos * 32;
   dim3 grid((unsigned)((n_pos + ppb - 1) / ppb), (unsigned)batch);
-  hipLaunchKernelGGL(act_split_kernel, grid, dim3((unsigned)(groups * lanes_pos)), 0, st, in, n_pos, ppb, hi, lo);
+  hipLaunchKernelGGL(act_split_kernel, grid, dim3((unsigned)(groups * lanes_pos)), 0, st, in, n_pos, ppb, hi, lo,
+                     raw_hi, raw_lo);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }

@@ -67,7 +67,12 @@ enum ConvKind : int { CONV3X3 = 0, CONV1X1 = 1, CONV2X2S2 = 2, DECONV2X2S2 = 3 }
 int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStream_t st);
 // act_split: hi/lo[b][pos][c] = split_bf16(GELU(IN_affine(x))) for the (possibly two-source,
 // channel-concatenated) input `in` of n_pos positions per batch item.
-int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st);
+int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st,
+                     uint16_t* raw_hi = nullptr, uint16_t* raw_lo = nullptr);
+// True when launch_conv runs a 3x3 same-size conv on conv3x3_m16_kernel, whose fused 1x1 shortcut
+// (C_shortcut > 0) must then be given as act_split raw planes (SRC_PRE) instead of a raw fp32 input.
+bool conv3x3_m16_selected(int T_out, int C_in, int C_out, int C_shortcut);
+int set_conv3x3_variant(int v);  // 0 = conv3x3_db_kernel, 1 = conv3x3_m16_kernel; returns the previous
 int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io);
 int tdf_block_rows(int M);
 // floats of the tiled U^T buffer [n/128][ceil(M/32)][128][32] for n_cols = B*T*C columns

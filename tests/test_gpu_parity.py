@@ -243,3 +243,24 @@ def test_instancenorm_stress_large_offsets(dev, golden):
     err = rms(y, g["y"])
     print(f"IN stress: rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
     assert err <= RMS_GATE
+
+
+@pytest.mark.parametrize("fixture,cfg_name,affine", [("mdx23c_small.npz", "config_mdx23c_small.yaml", None),
+                                                     ("mdx23c_small_stress.npz", "config_mdx23c_small.yaml", "stress"),
+                                                     ("mdx23c_full_chunk.npz", "config_vocals_mdx23c.yaml", "unit")])
+def test_conv3x3_m16_variant_matches_reference(golden, dev, fixture, cfg_name, affine):
+    """The opt-in conv3x3_m16_kernel (16x16x32 MFMA, persistent, LDS-DMA, shortcut from act_split raw
+    planes; sesa_mdx23c_set_conv_variant(1)) against the same reference goldens as the default kernel."""
+    from sesa import _native
+    g = golden(fixture)
+    m, _ = _model(cfg_name, affine or str(g["affine"]))
+    prev = _native.lib().sesa_mdx23c_set_conv_variant(1)
+    try:
+        y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    finally:
+        _native.lib().sesa_mdx23c_set_conv_variant(prev)
+    err = rms(y, g["y"])
+    print(f"{fixture} (m16 conv): rms={err:.3e}")
+    assert err <= RMS_GATE
+    y0 = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()           # default kernel, same model
+    assert rms(y0, y) <= 1e-5                                         # fp32 summation order only

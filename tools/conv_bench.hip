@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 namespace sesa {
@@ -40,6 +41,16 @@ __global__ void fill_bf16(uint16_t* p, int64_t n, uint32_t seed, float scale) {
     const float v = scale * ((float)(x & 0xffff) / 32768.f - 1.f);
     p[i] = __builtin_bit_cast(uint16_t, (__bf16)v);
   }
+}
+
+__global__ void max_diff(const float* a, const float* b, int64_t n, unsigned int* out) {
+  float d = 0.f, m = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    d = fmaxf(d, fabsf(a[i] - b[i]));
+    m = fmaxf(m, fabsf(b[i]));
+  }
+  atomicMax(out, __float_as_uint(d));
+  atomicMax(out + 1, __float_as_uint(m));
 }
 
 template <class F>
@@ -101,17 +112,113 @@ int main(int argc, char** argv) {
     const double flop = 2.0 * B * T * F * (double)C * C * 9;
     const dim3 grid((unsigned)(((T + 15) / 16) * (F / kTF) * ((C + 63) / 64)), 1u, (unsigned)B);
     auto rep = [&](const char* v, float ms) { printf("L%-4d %-26s %9.3f %9.1f\n", lvl, v, ms, flop / ms * 1e-9); };
-    rep("conv3x3_db (launch_conv)", time_ms([&] {
+    const int n_work = (int)grid.x * B;
+    int n_cu = 0;
+    CK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0));
+    const dim3 pgrid((unsigned)std::min(n_work, n_cu));
+    rep("conv3x3 (launch_conv)", time_ms([&] {
           CK(hipMemsetAsync(stats, 0, (size_t)B * C * 16, 0));
           launch_conv(CONV3X3, 64, 1, a, B, 0);
         }));
-    rep("no statistics", time_ms([&] { hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 1>), grid, dim3(512), 0, 0, a); }));
-    rep("no epilogue", time_ms([&] { hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 2>), grid, dim3(512), 0, 0, a); }));
+    rep("m16", time_ms([&] {
+          CK(hipMemsetAsync(stats, 0, (size_t)B * C * 16, 0));
+          hipLaunchKernelGGL((conv3x3_m16_kernel<true, false, 0>), pgrid, dim3(512), 0, 0, a, n_work);
+        }));
+    rep("m16 no statistics",
+        time_ms([&] { hipLaunchKernelGGL((conv3x3_m16_kernel<true, false, 1>), pgrid, dim3(512), 0, 0, a, n_work); }));
+    rep("m16 no epilogue",
+        time_ms([&] { hipLaunchKernelGGL((conv3x3_m16_kernel<true, false, 2>), pgrid, dim3(512), 0, 0, a, n_work); }));
+    rep("db (round 1)", time_ms([&] { hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0>), grid, dim3(512), 0, 0, a); }));
+    rep("db no epilogue", time_ms([&] { hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 2>), grid, dim3(512), 0, 0, a); }));
+    {  // agreement: m16 vs db on the same operands (both bf16x3, fp32 accumulate; summation order differs)
+      float* out2;
+      unsigned int* dm;
+      CK(hipMalloc(&out2, n_act * 4));
+      CK(hipMalloc(&dm, 8));
+      CK(hipMemset(dm, 0, 8));
+      hipLaunchKernelGGL((conv3x3_m16_kernel<true, false, 0>), pgrid, dim3(512), 0, 0, a, n_work);
+      ConvArgs a2 = a;
+      a2.out.ptr = out2;
+      hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0>), grid, dim3(512), 0, 0, a2);
+      hipLaunchKernelGGL(max_diff, dim3(2048), dim3(256), 0, 0, out, out2, n_act, dm);
+      unsigned int h[2];
+      CK(hipMemcpy(h, dm, 8, hipMemcpyDeviceToHost));
+      float d, m;
+      memcpy(&d, &h[0], 4);
+      memcpy(&m, &h[1], 4);
+      printf("L%-4d m16 vs db: max|diff| %.3e  max|out| %.3e  %s\n", lvl, d, m, d <= 1e-4f * m ? "OK" : "MISMATCH");
+      CK(hipFree(out2));
+      CK(hipFree(dm));
+    }
     CK(hipFree(hi));
     CK(hipFree(lo));
     CK(hipFree(w));
     CK(hipFree(out));
     CK(hipFree(stats));
+  }
+  // TDF Linears (first: NHWC -> tiled U, second: U -> NHWC + residual) on the level shapes
+  for (int lvl = 0; lvl < 3; ++lvl) {
+    const int C = 128 * (lvl + 1), T = 256 >> lvl, F = 1024 >> lvl, Fb = F / 4;
+    const int64_t n_act = (int64_t)B * T * F * C;
+    const int64_t n_u = tdf_u_floats((int64_t)B * T * C, Fb);
+    float *x, *h, *u;
+    double *st_x, *st_u, *st_o;
+    uint16_t *w1, *w2;
+    const int64_t w1n = (int64_t)((Fb + tdf_block_rows(Fb) - 1) / tdf_block_rows(Fb)) * ((F + 31) / 32) * 2 *
+                        tdf_block_rows(Fb) * 32;
+    const int64_t w2n = (int64_t)((F + tdf_block_rows(F) - 1) / tdf_block_rows(F)) * ((Fb + 31) / 32) * 2 *
+                        tdf_block_rows(F) * 32;
+    CK(hipMalloc(&x, n_act * 4));
+    CK(hipMalloc(&h, n_act * 4));
+    CK(hipMalloc(&u, n_u * 4));
+    CK(hipMalloc(&st_x, (size_t)B * C * 16));
+    CK(hipMalloc(&st_u, (size_t)B * C * 16));
+    CK(hipMalloc(&st_o, (size_t)B * C * 16));
+    CK(hipMalloc(&w1, w1n * 2));
+    CK(hipMalloc(&w2, w2n * 2));
+    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint16_t*>(x), n_act * 2, 4u, 1.f);
+    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint16_t*>(u), n_u * 2, 5u, 1.f);
+    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, w1, w1n, 6u, 0.03f);
+    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, w2, w2n, 7u, 0.05f);
+    std::vector<double> sth((size_t)B * C * 2);
+    for (size_t i = 0; i < sth.size(); i += 2) { sth[i] = 0.0; sth[i + 1] = (double)T * F; }
+    CK(hipMemcpy(st_x, sth.data(), sth.size() * 8, hipMemcpyHostToDevice));
+    for (size_t i = 0; i < sth.size(); i += 2) sth[i + 1] = (double)T * Fb;
+    CK(hipMemcpy(st_u, sth.data(), sth.size() * 8, hipMemcpyHostToDevice));
+    const double flop = 2.0 * B * T * (double)F * Fb * C;
+    auto mk = [&](const float* in, const double* st, int K, int M, float* out, const float* res, const uint16_t* w,
+                  double inv) {
+      TdfArgs t{};
+      t.in.src[0] = Src{in, st, nullptr, C, SRC_NORM_GELU, nullptr, nullptr};
+      t.in.src[1] = t.in.src[0];
+      t.in.C_split = C;
+      t.in.C_in = C;
+      t.in.inv_count = inv;
+      t.out = GemmOut{out, res, st_o, C, 0};
+      t.w = w;
+      t.T = T;
+      t.K = K;
+      t.M = M;
+      t.n_chunks = (K + 31) / 32;
+      return t;
+    };
+    const TdfArgs t1 = mk(x, st_x, F, Fb, u, nullptr, w1, 1.0 / ((double)T * F));
+    const TdfArgs t2 = mk(u, st_u, Fb, F, h, x, w2, 1.0 / ((double)T * Fb));
+    const double b1 = (double)n_act * 4 + (double)B * T * C * Fb * 4, b2 = (double)n_act * 8 + (double)B * T * C * Fb * 4;
+    const float ms1 = time_ms([&] { launch_tdf(1, t1, B, 0, 0); });
+    const float ms2 = time_ms([&] { launch_tdf(1, t2, B, 0, 1); });
+    printf("L%-4d tdf1 (F %d -> %d)          %9.3f %9.1f  HBM-alg %.0f GB/s\n", lvl, F, Fb, ms1, flop / ms1 * 1e-9,
+           b1 / ms1 * 1e-6);
+    printf("L%-4d tdf2 (%d -> %d, +res)     %9.3f %9.1f  HBM-alg %.0f GB/s\n", lvl, Fb, F, ms2, flop / ms2 * 1e-9,
+           b2 / ms2 * 1e-6);
+    CK(hipFree(x));
+    CK(hipFree(h));
+    CK(hipFree(u));
+    CK(hipFree(st_x));
+    CK(hipFree(st_u));
+    CK(hipFree(st_o));
+    CK(hipFree(w1));
+    CK(hipFree(w2));
   }
   return 0;
 }
