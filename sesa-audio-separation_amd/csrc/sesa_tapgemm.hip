@@ -1440,6 +1440,283 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// tdf_dma_kernel: the TDF Linears (mdx23c_tfc_tdf_v3.py:113-120) with every operand staged by LDS-DMA
+// so each chunk's HBM latency is covered by several chunks of MFMAs (tdf_kernel covers it with one).
+//   * 512 threads (8 waves, WM x WN), tile BM rows x 128 columns (one (b, t) x 128 channels; C % 128 == 0),
+//     wave tile 64 rows x (128 / WN) columns of 32x32x16 blocks.
+//   * per 32-deep K chunk: W (BM x 32, hi + lo, the packed image verbatim) into a 2-stage ring, one
+//     chunk ahead, and X as raw fp32 [32 k][128 n] (one contiguous 512-B row per k for NHWC input, one
+//     16 KiB block for tiled U) into a 4-stage ring, three chunks ahead (one counted s_waitcnt per chunk).
+//     Chunk kc + 1 is converted -- each thread one column x 8 k: 8 conflict-free ds_read_b32, InstanceNorm
+//     affine of its column from registers, packed GELU, hi / lo, one ds_write_b128 per plane (a
+//     4-column x 2-k item put every ds_write_b32 of a wave on 4 banks) -- into the second B image while
+//     chunk kc's MFMAs run: one barrier per chunk.
+//   * epilogue without LDS transposes: the 32x32 D layout has consecutive lanes on consecutive columns
+//     (channels), so U rows (U_OUT) and NHWC rows (+ the residual, prefetched into registers under the
+//     last chunk) are written as full 128-B lines; fp64 per-column statistics reduced through LDS.
+template <bool X3, bool U_IN, bool U_OUT, int BM>
+__global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
+  constexpr int BN = 128;
+  constexpr int WM = BM / 64, WN = 8 / WM;
+  constexpr int MI = 2, NI = BN / WN / 32;
+  static_assert(WM * WN == 8 && NI >= 1, "wave grid");
+  constexpr int ROWB = kTdfBK * 2;                 // 64 B per image row (32 bf16)
+  constexpr int W_PLANE = BM * ROWB;
+  constexpr int W_STAGE = (X3 ? 2 : 1) * W_PLANE;
+  constexpr int X_STAGE = kTdfBK * BN * 4;         // 16 KiB fp32
+  constexpr int B_PLANE = BN * ROWB;                // 8 KiB
+  constexpr int NWS = 2, NXS = 4;                   // W ring (one chunk ahead), X ring (three ahead)
+  constexpr int W_OFF = 0, X_OFF = NWS * W_STAGE, B_OFF = X_OFF + NXS * X_STAGE;
+  constexpr int B_IMG = (X3 ? 2 : 1) * B_PLANE;      // two B images: chunk kc's MFMAs / chunk kc+1's conversion
+  constexpr int SMEM = B_OFF + 2 * B_IMG;
+  static_assert(SMEM <= 163840 && WM * BN * 2 * 8 <= SMEM, "LDS budget");
+  constexpr int W_PC = W_STAGE / 1024, X_PC = X_STAGE / 1024;
+  static_assert(W_PC % 8 == 0 && X_PC % 8 == 0, "uniform DMA pieces per wave");
+  // s_waitcnt: all but the X_PC / 8 youngest vector-memory ops (the X DMA issued last), lgkmcnt(0)
+  constexpr int VMN = X_PC / 8;
+  constexpr int WAIT_ONE = (VMN & 15) | ((VMN >> 4) << 14) | (7 << 4);
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int l32 = lane & 31, h = lane >> 5;
+  const Src src = pick_src(a.in, 0);
+  const int C = src.C;
+  const int n_mb = (a.M + BM - 1) / BM;
+  // XCD-aware order: ids 8 apart share an XCD; the n_mb row blocks of a column tile are 8 ids apart
+  int ntile, mb;
+  {
+    const int id = blockIdx.x;
+    const int x = id & 7, rest = id >> 3;
+    mb = rest % n_mb;
+    ntile = (rest / n_mb) * 8 + x;
+  }
+  const int64_t n0 = (int64_t)ntile * BN;
+  const int64_t n_total = (int64_t)a.batch * a.T * C;
+  if (n0 >= n_total) return;  // (uniform; the grid is rounded up to 8 column tiles)
+  const int64_t bt = n0 / C;
+  const int c0 = (int)(n0 - bt * C);
+  const int b = (int)(bt / a.T);
+  const int nk = a.n_chunks;
+
+  // ---- LDS-DMA issue (buffer resources: 32-bit offsets) ----
+  auto rsrc = [](const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  };
+  auto dma = [](__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+  };
+  const uint16_t* wblk = a.w + (int64_t)mb * nk * (2 * W_PLANE / 2);
+  const __amdgpu_buffer_rsrc_t rw = rsrc(wblk, (uint32_t)((int64_t)nk * 2 * W_PLANE));
+  const float* xbase = U_IN ? src.ptr + (n0 >> 7) * (int64_t)nk * (kTdfBK * BN) : src.ptr + bt * (int64_t)a.K * C + c0;
+  const __amdgpu_buffer_rsrc_t rx =
+      rsrc(xbase, U_IN ? (uint32_t)(nk * X_STAGE) : (uint32_t)(((int64_t)(a.K - 1) * C + BN) * 4));
+  auto issue_w = [&](int kc) {
+    char* stg = smem + W_OFF + (kc % NWS) * W_STAGE;
+#pragma unroll
+    for (int i = 0; i < (W_PC + 7) / 8; ++i) {
+      const int pc = wave + 8 * i;
+      if (pc < W_PC) dma(rw, stg + pc * 1024, (uint32_t)(kc * 2 * W_PLANE + pc * 1024 + lane * 16));
+    }
+  };
+  auto issue_x = [&](int kc) {
+    char* stg = smem + X_OFF + (kc % NXS) * X_STAGE;
+#pragma unroll
+    for (int i = 0; i < X_PC / 8; ++i) {
+      const int pc = wave + 8 * i;                 // piece = k rows 2 pc, 2 pc + 1 (512 B each)
+      uint32_t voff;
+      if (U_IN) voff = (uint32_t)(kc * X_STAGE + pc * 1024 + lane * 16);
+      else {
+        const int k = kc * kTdfBK + 2 * pc + (lane >> 5);
+        voff = (uint32_t)(((int64_t)k * C + (lane & 31) * 4) * 4);
+      }
+      dma(rx, stg + pc * 1024, voff);
+    }
+  };
+
+  // ---- this thread's staging item: column ncol of the tile, k = 8 kq .. 8 kq + 7 of the chunk ----
+  // (X reads: consecutive lanes on consecutive columns of a 512-B fp32 row; B writes: one 16-B unit of
+  // hi and of lo per thread, conflict-free under the image swizzle)
+  const int ncol = tid & (BN - 1), kq = tid >> 7;  // kq 0..3
+  const bool act = src.mode == SRC_NORM_GELU;
+  float csc = 1.f, csh = 0.f;
+  if (act) {
+    const int c = c0 + ncol;
+    const double* st = src.stats + ((int64_t)b * C + c) * 2;
+    const double mean = st[0] * a.in.inv_count;
+    double var = st[1] * a.in.inv_count - mean * mean;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + 1e-5));
+    const float gm = a.in.gamma ? a.in.gamma[c] : 1.f;
+    const float be = a.in.beta ? a.in.beta[c] : 0.f;
+    csc = gm * rstd;
+    csh = be - (float)mean * csc;
+  }
+  const int b_off = ncol * ROWB + ((kq ^ ((ncol >> 2) & 3)) << 4);
+  auto convert = [&](int kc) {
+    const float* xs = reinterpret_cast<const float*>(smem + X_OFF + (kc % NXS) * X_STAGE);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = xs[(8 * kq + e) * BN + ncol];
+    if (act) {
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2 y = gelu_erf2(__builtin_elementwise_fma(f32x2{v[e], v[e + 1]}, f32x2{csc, csc}, f32x2{csh, csh}));
+        v[e] = y[0];
+        v[e + 1] = y[1];
+      }
+    }
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      __bf16 h0, l0, h1, l1;
+      split_bf16(v[e], h0, l0);
+      split_bf16(v[e + 1], h1, l1);
+      hw[e / 2] = pack2(h0, h1);
+      lw[e / 2] = pack2(l0, l1);
+    }
+    char* Bhi = smem + B_OFF + (kc & 1) * B_IMG;
+    *reinterpret_cast<uint4*>(Bhi + b_off) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    if (X3) *reinterpret_cast<uint4*>(Bhi + B_PLANE + b_off) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // residual rows (NHWC, may alias the output): prefetched under the last chunk
+  float res[U_OUT ? 1 : MI][U_OUT ? 1 : NI][U_OUT ? 1 : 16];
+  auto load_res = [&]() {
+    if constexpr (!U_OUT) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int jl = (wn * NI + j) * 32 + l32;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mb * BM + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            res[i][j][r] = (a.out.residual && m < a.M) ? a.out.residual[(bt * a.M + m) * C + c0 + jl] : 0.f;
+          }
+        }
+    }
+  };
+
+  // prologue: W(0), X(0..2) landed; chunk 0 converted
+  issue_w(0);
+#pragma unroll
+  for (int d = 0; d < NXS - 1; ++d)
+    if (d < nk) issue_x(d);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  convert(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  // iteration kc: MFMAs of chunk kc (B image kc & 1, W stage kc % 2) with chunk kc + 1 converted into the
+  // other B image in between; W(kc + 1) and X(kc + 3) issued at the top into stages whose last readers
+  // (iteration kc - 1's MFMAs, iteration kc - 2's conversion) are behind a barrier; one barrier per chunk
+  for (int kc = 0; kc < nk; ++kc) {
+    const bool more_w = kc + 1 < nk, more_x = kc + NXS - 1 < nk;
+    if (more_w) issue_w(kc + 1);
+    if (more_x) issue_x(kc + NXS - 1);
+    if (!U_OUT && kc + 1 == nk) load_res();
+    const char* W = smem + W_OFF + (kc % NWS) * W_STAGE;
+    const char* Bh = smem + B_OFF + (kc & 1) * B_IMG;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
+      const int q = ks * 2 + h;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = (wm * MI + i) * 32 + l32;
+        const int off = row * ROWB + ((q ^ ((row >> 2) & 3)) << 4);
+        ah[i] = *reinterpret_cast<const bf16x8*>(W + off);
+        if (X3) al[i] = *reinterpret_cast<const bf16x8*>(W + W_PLANE + off);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int n = (wn * NI + j) * 32 + l32;
+        const int off = n * ROWB + ((q ^ ((n >> 2) & 3)) << 4);
+        bh[j] = *reinterpret_cast<const bf16x8*>(Bh + off);
+        if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(Bh + B_PLANE + off);
+      }
+      if (ks == 0 && more_w) convert(kc + 1);  // VALU / LDS work between this chunk's MFMAs
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          if (X3) {
+            acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
+            acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
+          }
+          acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+        }
+    }
+    // W(kc + 1) and X(kc + 2) landed (only X(kc + 3), issued last, may stay in flight; the residual
+    // prefetch of the last iteration is waited for at its use)
+    if (more_x) __builtin_amdgcn_s_waitcnt(WAIT_ONE);
+    else if (more_w) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // ---- epilogue: output rows (full 128-B lines) + fp64 per-column statistics ----
+  double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2] (every LDS read retired by the last barrier)
+  const int64_t u_base = U_OUT ? (int64_t)ntile * ((a.M + 31) >> 5) * 4096 : 0;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int jl = (wn * NI + j) * 32 + l32;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb * BM + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= a.M) continue;
+        float v = acc[i][j][r];
+        if constexpr (U_OUT) {
+          a.out.ptr[u_base + ((m >> 5) << 12) + (m & 31) * 128 + jl] = v;
+        } else {
+          v += res[i][j][r];
+          a.out.ptr[(bt * a.M + m) * C + c0 + jl] = v;
+        }
+        s0 += (double)v;
+        s1 = fma((double)v, (double)v, s1);
+      }
+    s0 += __shfl_xor(s0, 32);
+    s1 += __shfl_xor(s1, 32);
+    if (h == 0) {
+      red[(wm * BN + jl) * 2 + 0] = s0;
+      red[(wm * BN + jl) * 2 + 1] = s1;
+    }
+  }
+  if (a.out.stats) {
+    __syncthreads();
+    if (tid < BN) {
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s0 += red[(w * BN + tid) * 2 + 0];
+        s1 += red[(w * BN + tid) * 2 + 1];
+      }
+      double* st = a.out.stats + ((int64_t)b * C + c0 + tid) * 2;
+      atomicAdd(st + 0, s0);
+      atomicAdd(st + 1, s1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // act_split: one pass over a normalised tensor, writing the bf16 hi/lo operand planes of its
 // consumer (InstanceNorm affine + exact GELU applied once per element instead of once per
 // consuming tile).  HBM-bound: reads 4 B, writes 2 + 2 B per element.
@@ -1694,10 +1971,44 @@ int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, u
 }
 
 // transposed_io: 0 = first Linear (NHWC in, U^T out), 1 = second Linear (U^T in, NHWC out)
+namespace {
+int tdf_variant() {  // SESA_TDF_VARIANT=old: the round-1 register-staged tdf_kernel everywhere (A/B)
+  static const int v = getenv("SESA_TDF_VARIANT") && std::string(getenv("SESA_TDF_VARIANT")) == "old" ? 1 : 0;
+  return v;
+}
+}  // namespace
+
 int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io) {
   TdfArgs b = a;
   b.batch = batch;
   SESA_REQUIRE(a.in.src[0].C % 4 == 0, SESA_ERR_INVALID, "tdf: C %d must be a multiple of 4", a.in.src[0].C);
+  {
+    const int C = a.in.src[0].C;
+    const int bm = tdf_block_rows(a.M);
+    const int mode = a.in.src[0].mode;
+    if (tdf_variant() == 0 && C % 128 == 0 && a.K % kTdfBK == 0 && (bm == 256 || bm == 128) &&
+        (mode == SRC_NORM_GELU || mode == SRC_RAW) && a.in.C_split == a.in.C_in && a.in.C_in == C) {
+      const int64_t n_tiles = (int64_t)batch * a.T * C / 128;
+      const int64_t grid = (n_tiles + 7) / 8 * 8 * ((a.M + bm - 1) / bm);
+      SESA_REQUIRE(grid < (1ll << 31), SESA_ERR_INVALID, "tdf: grid too large");
+      const dim3 g((unsigned)grid), blk(512);
+#define SESA_TDF_DMA(UI, UO, BMV)                                                              \
+  do {                                                                                         \
+    if (x3) hipLaunchKernelGGL((tdf_dma_kernel<true, UI, UO, BMV>), g, blk, 0, st, b);         \
+    else hipLaunchKernelGGL((tdf_dma_kernel<false, UI, UO, BMV>), g, blk, 0, st, b);           \
+  } while (0)
+      if (transposed_io == 0) {
+        if (bm == 256) SESA_TDF_DMA(false, true, 256);
+        else SESA_TDF_DMA(false, true, 128);
+      } else {
+        if (bm == 256) SESA_TDF_DMA(true, false, 256);
+        else SESA_TDF_DMA(true, false, 128);
+      }
+#undef SESA_TDF_DMA
+      SESA_CHECK_LAUNCH();
+      return SESA_OK;
+    }
+  }
   if (transposed_io == 0) {
     SESA_REQUIRE(a.M % 4 == 0, SESA_ERR_INVALID, "tdf: M %d must be a multiple of 4", a.M);
     return launch_tdf_bm<false, true>(x3, b, st);
