@@ -1,7 +1,7 @@
 // Standalone timing of the MDX23C TFC 3x3 convolution (conv3x3_db_kernel) on the vocals config's
 // level shapes (diagnostic, not product).  Compiles sesa_tapgemm.hip into this translation unit so
 // kernel variants / ablations can be launched directly; median of 10 HIP-event-timed launches.
-//   ./tools/conv_bench [batch=57]
+//   ./tools/conv_bench [batch=57] [tdf]
 #include "../sesa-audio-separation_amd/csrc/sesa_tapgemm.hip"
 
 #include <algorithm>
@@ -77,7 +77,8 @@ float time_ms(F&& launch, int reps = 10) {
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 57;
   printf("batch %d\n%-5s %-26s %9s %9s\n", B, "level", "variant", "ms", "TF/s(alg)");
-  for (int lvl = 0; lvl < 4; ++lvl) {
+  const bool only_tdf = argc > 2 && strcmp(argv[2], "tdf") == 0;  // ./tools/conv_bench 57 tdf
+  for (int lvl = 0; lvl < (only_tdf ? 0 : 4); ++lvl) {
     const int C = 128 * (lvl + 1), T = 256 >> lvl, F = 1024 >> lvl;
     const int64_t n_act = (int64_t)B * T * F * C;
     uint16_t *hi, *lo, *w;
