@@ -44,49 +44,39 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Exact (erf) GELU, torch.nn.GELU(approximate='none'), branch-free:
 //   Phi(v) = 1 - erfc(z)/2 (v >= 0) or erfc(z)/2 (v < 0), z = |v|/sqrt(2), with
-//   erfc(z) = t * exp(-z^2 + P9(t)), t = 1/(1 + z/2)  (Chebyshev fit, fractional error < 1.2e-7).
-// Max |error| vs the float64 GELU is 3.8e-7 over [-12, 12] -- the same as the float32 erff()
-// form (4.5e-7) and far below the 2^-17 hi/lo bf16 split that follows -- at ~19 VALU ops instead
-// of ~35 with a divergent branch (ocml erff).
+//   erfc(z) = t * P4(t) * exp(-z^2), t = 1/(1 + p z)  (Abramowitz & Stegun 7.1.26, |erf error| < 1.5e-7).
+// Max |error| vs the float64 GELU over [-12, 12] in float32 is 4.2e-7 -- the float32 resolution of the
+// result there (the 9-term Chebyshev erfc form used before: 3.8e-7; ocml erff: 4.5e-7) and far below the
+// 2^-17 hi/lo bf16 split that follows -- at ~14 VALU ops (5 fewer than that form; the TDF staging and the
+// FF1 epilogue that use it are VALU-issue-bound).
 __device__ __forceinline__ float gelu_erf(float v) {
   const float z = fabsf(v) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
-  float p = 0.17087277f;
-  p = fmaf(p, t, -0.82215223f);
-  p = fmaf(p, t, 1.48851587f);
-  p = fmaf(p, t, -1.13520398f);
-  p = fmaf(p, t, 0.27886807f);
-  p = fmaf(p, t, -0.18628806f);
-  p = fmaf(p, t, 0.09678418f);
-  p = fmaf(p, t, 0.37409196f);
-  p = fmaf(p, t, 1.00002368f);
-  p = fmaf(p, t, -1.26551223f);
-  const float e = t * __builtin_amdgcn_exp2f((p - z * z) * 1.4426950408889634f);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = 1.061405429f;
+  p = fmaf(p, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = p * t * __builtin_amdgcn_exp2f(-(z * z) * 1.4426950408889634f);  // erfc(z)
   const float phi = v >= 0.f ? fmaf(-0.5f, e, 1.0f) : 0.5f * e;
   return v * phi;
 }
 
 // gelu_erf on two values at once: the same sequence of fmas on float2, which gfx950 issues as
 // packed v_pk_fma_f32 / v_pk_mul_f32 (half the VALU issue slots of the scalar form; the rcp / exp2
-// stay per component).  Used by the HBM-streaming act_split pass, where the scalar form made the
-// kernel issue-bound below the HBM rate.
+// stay per component).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_erf2(f32x2 v) {
   const f32x2 z = __builtin_elementwise_abs(v) * 0.70710678118654752440f;
-  const f32x2 d = __builtin_elementwise_fma(z, f32x2{0.5f, 0.5f}, f32x2{1.0f, 1.0f});
+  const f32x2 d = __builtin_elementwise_fma(z, f32x2{0.3275911f, 0.3275911f}, f32x2{1.0f, 1.0f});
   const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
-  f32x2 p = {0.17087277f, 0.17087277f};
-  p = __builtin_elementwise_fma(p, t, f32x2{-0.82215223f, -0.82215223f});
-  p = __builtin_elementwise_fma(p, t, f32x2{1.48851587f, 1.48851587f});
-  p = __builtin_elementwise_fma(p, t, f32x2{-1.13520398f, -1.13520398f});
-  p = __builtin_elementwise_fma(p, t, f32x2{0.27886807f, 0.27886807f});
-  p = __builtin_elementwise_fma(p, t, f32x2{-0.18628806f, -0.18628806f});
-  p = __builtin_elementwise_fma(p, t, f32x2{0.09678418f, 0.09678418f});
-  p = __builtin_elementwise_fma(p, t, f32x2{0.37409196f, 0.37409196f});
-  p = __builtin_elementwise_fma(p, t, f32x2{1.00002368f, 1.00002368f});
-  p = __builtin_elementwise_fma(p, t, f32x2{-1.26551223f, -1.26551223f});
-  const f32x2 a = __builtin_elementwise_fma(-z, z, p) * 1.4426950408889634f;
-  const f32x2 e = t * f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])};
+  f32x2 p = {1.061405429f, 1.061405429f};
+  p = __builtin_elementwise_fma(p, t, f32x2{-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, f32x2{1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.254829592f, 0.254829592f});
+  const f32x2 a = (z * z) * -1.4426950408889634f;
+  const f32x2 e = p * t * f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])};
   const f32x2 one_minus = __builtin_elementwise_fma(e, f32x2{-0.5f, -0.5f}, f32x2{1.0f, 1.0f});
   const f32x2 half = e * 0.5f;
   const f32x2 phi = {v[0] >= 0.f ? one_minus[0] : half[0], v[1] >= 0.f ? one_minus[1] : half[1]};
