@@ -334,7 +334,7 @@ struct Fwd {
 
   // transposed_io 0: first Linear (NHWC in, U^T [B][T][C][F/bn] out); 1: second Linear (U^T in, NHWC out)
   void tdf(const TdfW& w, const GemmIn& in, int T, float* out, const float* residual, double* out_stats, int C,
-           int transposed_io) {
+           int transposed_io, uint16_t* u_planes = nullptr) {
     if (dry || rc) return;
     TdfArgs a{};
     a.in = in;
@@ -344,6 +344,7 @@ struct Fwd {
     a.K = w.K;
     a.M = w.M;
     a.n_chunks = (w.K + kTdfBK - 1) / kTdfBK;
+    a.u_planes = u_planes;
     void* tok = profile_begin(st);
     rc = launch_tdf(x3, a, B, st, transposed_io);
     profile_end(tok, st, SESA_KCLASS_TDF, 2.0 * B * T * (double)w.M * w.K * C);
@@ -406,8 +407,10 @@ struct Fwd {
       // x = x + tdf(x)
       tdf(bk.lin1, input(Tensor{H, st_h1, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf0, L.T, L.F), L.T, U, nullptr, st_u,
           c, 0);
+      // act(U) B images for the second Linear (same size as U; released with the block's temporaries)
+      uint16_t* Up = reinterpret_cast<uint16_t*>(buf(tdf_u_floats((int64_t)B * L.T * c, L.F / bnf)));
       tdf(bk.lin2, input(Tensor{U, st_u, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf3, L.T, L.F / bnf), L.T, H, H, st_h2,
-          c, 1);
+          c, 1, Up);
       // x = tfc2(x) + shortcut(block input): the 1x1 shortcut rides along as extra K (raw input)
       if (!pre_sc) xs = input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F);
       conv(bk.conv2, act(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F), L.T, L.F, L.T, L.F, S, nullptr, st_out, 0,

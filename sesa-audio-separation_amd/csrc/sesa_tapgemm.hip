@@ -1440,6 +1440,63 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// tdf_u_split_kernel: act(U) of the second TDF Linear (InstanceNorm affine of tdf[3], exact GELU, bf16
+// hi / lo) once per element, written as the B images tdf_dma_kernel<.., PRE> copies by LDS-DMA
+// ([column tile][chunk][hi: 128 n x 32 k][lo], the image swizzle included).  Without it the second
+// Linear converts every U element once per 256-row block of its output (4x at level 0), and its
+// staging is VALU-issue-bound.  One workgroup per (column tile, chunk); thread = column x 8 k.
+__global__ void __launch_bounds__(512) tdf_u_split_kernel(TdfArgs a) {
+  constexpr int BN = 128, ROWB = kTdfBK * 2;
+  const int64_t ntile = blockIdx.x;
+  const int kc = blockIdx.y;
+  const Src src = pick_src(a.in, 0);
+  const int C = src.C;
+  const int n = threadIdx.x & (BN - 1), kq = threadIdx.x >> 7;
+  const int64_t col = ntile * BN + n;
+  const int64_t bt = col / C;
+  const int c = (int)(col - bt * C), b = (int)(bt / a.T);
+  float csc = 1.f, csh = 0.f;
+  const bool act = src.mode == SRC_NORM_GELU;
+  if (act) {
+    const double* st = src.stats + ((int64_t)b * C + c) * 2;
+    const double mean = st[0] * a.in.inv_count;
+    double var = st[1] * a.in.inv_count - mean * mean;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + 1e-5));
+    const float gm = a.in.gamma ? a.in.gamma[c] : 1.f;
+    const float be = a.in.beta ? a.in.beta[c] : 0.f;
+    csc = gm * rstd;
+    csh = be - (float)mean * csc;
+  }
+  const int64_t blk = ntile * a.n_chunks + kc;
+  const float* u = src.ptr + blk * (kTdfBK * BN);
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = __builtin_nontemporal_load(u + (8 * kq + e) * BN + n);
+  if (act) {
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const f32x2 y = gelu_erf2(__builtin_elementwise_fma(f32x2{v[e], v[e + 1]}, f32x2{csc, csc}, f32x2{csh, csh}));
+      v[e] = y[0];
+      v[e + 1] = y[1];
+    }
+  }
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    __bf16 h0, l0, h1, l1;
+    split_bf16(v[e], h0, l0);
+    split_bf16(v[e + 1], h1, l1);
+    hw[e / 2] = pack2(h0, h1);
+    lw[e / 2] = pack2(l0, l1);
+  }
+  char* dst = reinterpret_cast<char*>(a.u_planes) + blk * (kTdfBK * BN * 4);
+  const int off = n * ROWB + ((kq ^ ((n >> 2) & 3)) << 4);
+  *reinterpret_cast<uint4*>(dst + off) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+  *reinterpret_cast<uint4*>(dst + BN * ROWB + off) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+}
+
+// ---------------------------------------------------------------------------------------------
 // tdf_dma_kernel: the TDF Linears (mdx23c_tfc_tdf_v3.py:113-120) with every operand staged by LDS-DMA
 // so each chunk's HBM latency is covered by several chunks of MFMAs (tdf_kernel covers it with one).
 //   * 512 threads (8 waves, WM x WN), tile BM rows x 128 columns (one (b, t) x 128 channels; C % 128 == 0),
@@ -1454,8 +1511,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
 //   * epilogue without LDS transposes: the 32x32 D layout has consecutive lanes on consecutive columns
 //     (channels), so U rows (U_OUT) and NHWC rows (+ the residual, prefetched into registers under the
 //     last chunk) are written as full 128-B lines; fp64 per-column statistics reduced through LDS.
-template <bool X3, bool U_IN, bool U_OUT, int BM>
+template <bool X3, bool U_IN, bool U_OUT, int BM, bool PRE = false>
 __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
+  static_assert(!PRE || U_IN, "pre-split B images exist for the tiled U input only");
   constexpr int BN = 128;
   constexpr int WM = BM / 64, WN = 8 / WM;
   constexpr int MI = 2, NI = BN / WN / 32;
@@ -1510,7 +1568,10 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   };
   const uint16_t* wblk = a.w + (int64_t)mb * nk * (2 * W_PLANE / 2);
   const __amdgpu_buffer_rsrc_t rw = rsrc(wblk, (uint32_t)((int64_t)nk * 2 * W_PLANE));
-  const float* xbase = U_IN ? src.ptr + (n0 >> 7) * (int64_t)nk * (kTdfBK * BN) : src.ptr + bt * (int64_t)a.K * C + c0;
+  // PRE: the X ring carries the B images tdf_u_split_kernel wrote (same 16 KiB per chunk as fp32 U)
+  const float* xbase = PRE    ? reinterpret_cast<const float*>(a.u_planes) + (n0 >> 7) * (int64_t)nk * (kTdfBK * BN)
+                       : U_IN ? src.ptr + (n0 >> 7) * (int64_t)nk * (kTdfBK * BN)
+                              : src.ptr + bt * (int64_t)a.K * C + c0;
   const __amdgpu_buffer_rsrc_t rx =
       rsrc(xbase, U_IN ? (uint32_t)(nk * X_STAGE) : (uint32_t)(((int64_t)(a.K - 1) * C + BN) * 4));
   auto issue_w = [&](int kc) {
@@ -1556,6 +1617,7 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   }
   const int b_off = ncol * ROWB + ((kq ^ ((ncol >> 2) & 3)) << 4);
   auto convert = [&](int kc) {
+    if constexpr (PRE) return;
     const float* xs = reinterpret_cast<const float*>(smem + X_OFF + (kc % NXS) * X_STAGE);
     float v[8];
 #pragma unroll
@@ -1629,7 +1691,7 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
     if (more_x) issue_x(kc + NXS - 1);
     if (!U_OUT && kc + 1 == nk) load_res();
     const char* W = smem + W_OFF + (kc % NWS) * W_STAGE;
-    const char* Bh = smem + B_OFF + (kc & 1) * B_IMG;
+    const char* Bh = PRE ? smem + X_OFF + (kc % NXS) * X_STAGE : smem + B_OFF + (kc & 1) * B_IMG;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
@@ -1648,7 +1710,7 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
         bh[j] = *reinterpret_cast<const bf16x8*>(Bh + off);
         if (X3) bl[j] = *reinterpret_cast<const bf16x8*>(Bh + B_PLANE + off);
       }
-      if (ks == 0 && more_w) convert(kc + 1);  // VALU / LDS work between this chunk's MFMAs
+      if (!PRE && ks == 0 && more_w) convert(kc + 1);  // VALU / LDS work between this chunk's MFMAs
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -2000,6 +2062,19 @@ int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transpos
       if (transposed_io == 0) {
         if (bm == 256) SESA_TDF_DMA(false, true, 256);
         else SESA_TDF_DMA(false, true, 128);
+      } else if (b.u_planes && (a.M + bm - 1) / bm >= 3) {
+        // act(U) once per element, then the GEMM copies B images (measured: a win where the in-kernel
+        // conversion would run >= 3x per element -- level 0 -- neutral at 2x, a loss at 1x)
+        hipLaunchKernelGGL(tdf_u_split_kernel, dim3((unsigned)n_tiles, (unsigned)a.n_chunks), dim3(512), 0, st, b);
+        SESA_CHECK_LAUNCH();
+#define SESA_TDF_PRE(BMV)                                                                       \
+  do {                                                                                          \
+    if (x3) hipLaunchKernelGGL((tdf_dma_kernel<true, true, false, BMV, true>), g, blk, 0, st, b);  \
+    else hipLaunchKernelGGL((tdf_dma_kernel<false, true, false, BMV, true>), g, blk, 0, st, b);    \
+  } while (0)
+        if (bm == 256) SESA_TDF_PRE(256);
+        else SESA_TDF_PRE(128);
+#undef SESA_TDF_PRE
       } else {
         if (bm == 256) SESA_TDF_DMA(true, false, 256);
         else SESA_TDF_DMA(true, false, 128);

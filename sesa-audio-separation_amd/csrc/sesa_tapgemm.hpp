@@ -59,6 +59,8 @@ struct TdfArgs {
   int T, K, M;               // F_in = K, F_out = M
   int n_chunks;              // ceil(K / 32)
   int batch;                 // set by launch_tdf
+  uint16_t* u_planes;        // second Linear: scratch of tdf_u_floats(..) floats for the pre-split act(U)
+                             // B images (nullable: the kernel then converts U itself)
 };
 
 // conv kinds

@@ -206,12 +206,41 @@ int main(int argc, char** argv) {
     const TdfArgs t1 = mk(x, st_x, F, Fb, u, nullptr, w1, 1.0 / ((double)T * F));
     const TdfArgs t2 = mk(u, st_u, Fb, F, h, x, w2, 1.0 / ((double)T * Fb));
     const double b1 = (double)n_act * 4 + (double)B * T * C * Fb * 4, b2 = (double)n_act * 8 + (double)B * T * C * Fb * 4;
+    uint16_t* up;
+    CK(hipMalloc(&up, n_u * 4));
+    TdfArgs t2p = t2;
+    t2p.u_planes = up;
     const float ms1 = time_ms([&] { launch_tdf(1, t1, B, 0, 0); });
     const float ms2 = time_ms([&] { launch_tdf(1, t2, B, 0, 1); });
+    const float ms2p = time_ms([&] { launch_tdf(1, t2p, B, 0, 1); });
+    {  // agreement of the two second-Linear paths
+      float* h2;
+      unsigned int* dm;
+      CK(hipMalloc(&h2, n_act * 4));
+      CK(hipMalloc(&dm, 8));
+      CK(hipMemset(dm, 0, 8));
+      TdfArgs ta = t2, tb = t2p;
+      tb.out.ptr = h2;
+      launch_tdf(1, ta, B, 0, 1);
+      launch_tdf(1, tb, B, 0, 1);
+      hipLaunchKernelGGL(max_diff, dim3(2048), dim3(256), 0, 0, h, h2, n_act, dm);
+      unsigned int hh[2];
+      CK(hipMemcpy(hh, dm, 8, hipMemcpyDeviceToHost));
+      float d, m;
+      memcpy(&d, &hh[0], 4);
+      memcpy(&m, &hh[1], 4);
+      printf("L%-4d tdf2 pre-split vs in-kernel: max|diff| %.3e max|out| %.3e %s\n", lvl, d, m,
+             d <= 1e-5f * m ? "OK" : "MISMATCH");
+      CK(hipFree(h2));
+      CK(hipFree(dm));
+    }
+    CK(hipFree(up));
     printf("L%-4d tdf1 (F %d -> %d)          %9.3f %9.1f  HBM-alg %.0f GB/s\n", lvl, F, Fb, ms1, flop / ms1 * 1e-9,
            b1 / ms1 * 1e-6);
     printf("L%-4d tdf2 (%d -> %d, +res)     %9.3f %9.1f  HBM-alg %.0f GB/s\n", lvl, Fb, F, ms2, flop / ms2 * 1e-9,
            b2 / ms2 * 1e-6);
+    printf("L%-4d tdf2 pre-split U (+split) %9.3f %9.1f  HBM-alg %.0f GB/s\n", lvl, ms2p, flop / ms2p * 1e-9,
+           b2 / ms2p * 1e-6);
     CK(hipFree(x));
     CK(hipFree(h));
     CK(hipFree(u));
