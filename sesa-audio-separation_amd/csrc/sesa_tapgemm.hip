@@ -1917,6 +1917,11 @@ int set_conv3x3_variant(int v) {
   return prev;
 }
 
+bool tap_bn128_enabled() {
+  static const bool v = !(getenv("SESA_TAP_BN128") && std::string(getenv("SESA_TAP_BN128")) == "0");
+  return v;
+}
+
 bool conv3x3_m16_selected(int T_out, int C_in, int C_out, int C_shortcut) {
   return conv_variant() == 1 && T_out >= 32 && C_in % 32 == 0 && C_out % 16 == 0 && C_shortcut % 32 == 0;
 }
@@ -1980,8 +1985,10 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
       if (bn == 32) return launch_conv_t<1, 1, 1, 0, 8, 32, 4, false, false, false>(x3, a, batch, st);
       return launch_conv_t<1, 1, 1, 0, 8, 64, 4, false, false, false>(x3, a, batch, st);
     case CONV2X2S2:
+      if (bn == 128) return launch_conv_t<2, 2, 2, 0, 4, 128, 4, false, false, true>(x3, a, batch, st);
       return launch_conv_t<2, 2, 2, 0, 4, 64, 4, false, false, true>(x3, a, batch, st);
     case DECONV2X2S2:
+      if (bn == 128) return launch_conv_t<1, 1, 1, 0, 8, 128, 4, true, false, true>(x3, a, batch, st);
       return launch_conv_t<1, 1, 1, 0, 8, 64, 4, true, false, true>(x3, a, batch, st);
   }
   set_error("conv: unknown kind %d", kind);
