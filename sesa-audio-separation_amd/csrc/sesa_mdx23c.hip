@@ -129,7 +129,8 @@ ConvW add_conv(sesa_mdx23c* m, const std::string& name, int kind, int c_out, int
   w.bn = (kind == CONV1X1 && w.n_cols <= 32) ? 32 : 64;
   // down / up convolutions: 128 output columns per workgroup (half the input re-reads, twice the MFMAs
   // per staged chunk) where N allows
-  if ((kind == CONV2X2S2 || kind == DECONV2X2S2) && w.n_cols % 128 == 0 && tap_bn128_enabled()) w.bn = 128;
+  if ((kind == CONV2X2S2 || kind == DECONV2X2S2 || kind == CONV1X1) && w.n_cols % 128 == 0 && tap_bn128_enabled())
+    w.bn = 128;
   return w;
 }
 

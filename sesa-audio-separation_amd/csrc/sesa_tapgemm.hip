@@ -1983,6 +1983,7 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
       return launch_conv_t<3, 3, 1, 1, 8, 64, 4, false, false, true>(x3, a, batch, st);
     case CONV1X1:
       if (bn == 32) return launch_conv_t<1, 1, 1, 0, 8, 32, 4, false, false, false>(x3, a, batch, st);
+      if (bn == 128) return launch_conv_t<1, 1, 1, 0, 8, 128, 4, false, false, false>(x3, a, batch, st);
       return launch_conv_t<1, 1, 1, 0, 8, 64, 4, false, false, false>(x3, a, batch, st);
     case CONV2X2S2:
       if (bn == 128) return launch_conv_t<2, 2, 2, 0, 4, 128, 4, false, false, true>(x3, a, batch, st);
