@@ -687,8 +687,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     return;
   }
   // ---- epilogue: fp32 store + per-channel sum / sum-of-squares for the next InstanceNorm ----
-  // InstanceNorm statistics in fp64 from the first add on: E[x^2] - E[x]^2 is formed in double at the
-  // consumer, so channels whose |mean| >> std (large norm beta, DC offsets) keep their precision
+  // Statistics: fp32 partial sums over each lane's 16-value runs (relative error ~ a few ulp of a
+  // 16-term sum), fp64 from there on -- E[x^2] - E[x]^2 is formed in double at the consumer, so channels
+  // whose |mean| >> std (large norm beta, DC offsets) keep their precision (stress golden
+  // mdx23c_small_stress.npz).  (Per-value fp64 accumulation cost ~3 % of the level-0 conv.)
   double ssum[NI], ssq[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) { ssum[j] = 0.0; ssq[j] = 0.0; }
@@ -701,16 +703,19 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     for (int i = 0; i < MI; ++i) {
       const int t = t0 + wm * MI + i;
       if (t >= a.T_out) continue;
+      float ps = 0.f, pq = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int f = f0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int64_t idx = (((int64_t)b * a.T_out + t) * a.F_out + f) * C_out + co;
         const float v = acc[i][j][r];
         a.out.ptr[idx] = v;
-        if constexpr (EPI == 1) continue;
-        ssum[j] += (double)v;
-        ssq[j] = fma((double)v, (double)v, ssq[j]);
+        ps += v;
+        pq = fmaf(v, v, pq);
       }
+      if constexpr (EPI == 1) continue;
+      ssum[j] += (double)ps;
+      ssq[j] += (double)pq;
     }
   }
   if (EPI == 0 && a.out.stats) {
