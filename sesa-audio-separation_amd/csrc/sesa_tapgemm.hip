@@ -1515,7 +1515,8 @@ __global__ void __launch_bounds__(512) tdf_u_split_kernel(TdfArgs a) {
 //     chunk kc's MFMAs run: one barrier per chunk.
 //   * epilogue without LDS transposes: the 32x32 D layout has consecutive lanes on consecutive columns
 //     (channels), so U rows (U_OUT) and NHWC rows (+ the residual, prefetched into registers under the
-//     last chunk) are written as full 128-B lines; fp64 per-column statistics reduced through LDS.
+//     last chunk) are written as full 128-B lines; per-column statistics (fp32 over 16-value runs, fp64
+//     beyond) reduced through LDS.
 template <bool X3, bool U_IN, bool U_OUT, int BM, bool PRE = false>
 __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   static_assert(!PRE || U_IN, "pre-split B images exist for the tiled U input only");
@@ -1737,15 +1738,16 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
     asm volatile("" ::: "memory");
   }
 
-  // ---- epilogue: output rows (full 128-B lines) + fp64 per-column statistics ----
+  // ---- epilogue: output rows (full 128-B lines) + per-column statistics ----
   double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2] (every LDS read retired by the last barrier)
   const int64_t u_base = U_OUT ? (int64_t)ntile * ((a.M + 31) >> 5) * 4096 : 0;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int jl = (wn * NI + j) * 32 + l32;
-    double s0 = 0.0, s1 = 0.0;
+    double s0 = 0.0, s1 = 0.0;  // fp32 partial sums over each 16-value run, fp64 from there
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i) {
+      float ps = 0.f, pq = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mb * BM + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -1757,9 +1759,12 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
           v += res[i][j][r];
           a.out.ptr[(bt * a.M + m) * C + c0 + jl] = v;
         }
-        s0 += (double)v;
-        s1 = fma((double)v, (double)v, s1);
+        ps += v;
+        pq = fmaf(v, v, pq);
       }
+      s0 += (double)ps;
+      s1 += (double)pq;
+    }
     s0 += __shfl_xor(s0, 32);
     s1 += __shfl_xor(s1, 32);
     if (h == 0) {
