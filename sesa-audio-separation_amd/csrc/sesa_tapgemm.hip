@@ -1662,6 +1662,19 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   float res[U_OUT ? 1 : MI][U_OUT ? 1 : NI][U_OUT ? 1 : 16];
   auto load_res = [&]() {
     if constexpr (!U_OUT) {
+      if (a.out.residual && (mb + 1) * BM <= a.M) {  // full row block (uniform): unguarded, 32-bit offsets
+        const float* rb = a.out.residual + (bt * a.M + mb * BM) * C + c0;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int jl = (wn * NI + j) * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              res[i][j][r] = rb[((wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * C + jl];
+          }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1741,37 +1754,46 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   // ---- epilogue: output rows (full 128-B lines) + per-column statistics ----
   double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2] (every LDS read retired by the last barrier)
   const int64_t u_base = U_OUT ? (int64_t)ntile * ((a.M + 31) >> 5) * 4096 : 0;
+  // full row blocks (M % BM == 0 for every real shape): no per-element guards, 32-bit offsets from a
+  // uniform tile base (the guarded form compiled to ~100 exec-mask branches and 64-bit math per store)
+  auto epilogue = [&](auto FULLT) {
+    constexpr bool FULL = decltype(FULLT)::value;
+    float* obase = U_OUT ? a.out.ptr + u_base + (int64_t)((mb * BM) >> 5) * 4096
+                         : a.out.ptr + (bt * a.M + mb * BM) * C + c0;
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int jl = (wn * NI + j) * 32 + l32;
-    double s0 = 0.0, s1 = 0.0;  // fp32 partial sums over each 16-value run, fp64 from there
+    for (int j = 0; j < NI; ++j) {
+      const int jl = (wn * NI + j) * 32 + l32;
+      double s0 = 0.0, s1 = 0.0;  // fp32 partial sums over each 16-value run, fp64 from there
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      float ps = 0.f, pq = 0.f;
+      for (int i = 0; i < MI; ++i) {
+        float ps = 0.f, pq = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mb * BM + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m >= a.M) continue;
-        float v = acc[i][j][r];
-        if constexpr (U_OUT) {
-          a.out.ptr[u_base + ((m >> 5) << 12) + (m & 31) * 128 + jl] = v;
-        } else {
-          v += res[i][j][r];
-          a.out.ptr[(bt * a.M + m) * C + c0 + jl] = v;
+        for (int r = 0; r < 16; ++r) {
+          const int ml = (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;  // row within the block
+          if (!FULL && mb * BM + ml >= a.M) continue;
+          float v = acc[i][j][r];
+          if constexpr (U_OUT) {
+            obase[((ml >> 5) << 12) + (ml & 31) * 128 + jl] = v;
+          } else {
+            v += res[i][j][r];
+            obase[ml * C + jl] = v;
+          }
+          ps += v;
+          pq = fmaf(v, v, pq);
         }
-        ps += v;
-        pq = fmaf(v, v, pq);
+        s0 += (double)ps;
+        s1 += (double)pq;
       }
-      s0 += (double)ps;
-      s1 += (double)pq;
+      s0 += __shfl_xor(s0, 32);
+      s1 += __shfl_xor(s1, 32);
+      if (h == 0) {
+        red[(wm * BN + jl) * 2 + 0] = s0;
+        red[(wm * BN + jl) * 2 + 1] = s1;
+      }
     }
-    s0 += __shfl_xor(s0, 32);
-    s1 += __shfl_xor(s1, 32);
-    if (h == 0) {
-      red[(wm * BN + jl) * 2 + 0] = s0;
-      red[(wm * BN + jl) * 2 + 1] = s1;
-    }
-  }
+  };
+  if ((mb + 1) * BM <= a.M) epilogue(std::true_type{});
+  else epilogue(std::false_type{});
   if (a.out.stats) {
     __syncthreads();
     if (tid < BN) {
