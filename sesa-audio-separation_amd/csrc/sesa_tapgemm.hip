@@ -1662,19 +1662,6 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   float res[U_OUT ? 1 : MI][U_OUT ? 1 : NI][U_OUT ? 1 : 16];
   auto load_res = [&]() {
     if constexpr (!U_OUT) {
-      if (a.out.residual && (mb + 1) * BM <= a.M) {  // full row block (uniform): unguarded, 32-bit offsets
-        const float* rb = a.out.residual + (bt * a.M + mb * BM) * C + c0;
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NI; ++j) {
-            const int jl = (wn * NI + j) * 32 + l32;
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              res[i][j][r] = rb[((wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * C + jl];
-          }
-        return;
-      }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
