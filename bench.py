@@ -83,6 +83,42 @@ KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_3
          "attn": "attn_kernel (flash attention, S^T = K Q^T, bf16x3 v_mfma_f32_32x32x16_bf16)"}
 
 
+# Sources that compile each kernel class: a committed PMC summary (profiles/pmc_<class>.json) counts only
+# when it was measured on these exact sources (sha256 over their bytes; the GPU box has no .git).
+_CSRC = os.path.join(REPO, "sesa-audio-separation_amd", "csrc")
+_MDX_SRC = ("sesa_tapgemm.hip", "sesa_tapgemm.hpp", "sesa_common.hpp", "sesa_mdx23c.hip")
+_TOK_SRC = ("sesa_tokgemm.hip", "sesa_tokgemm.hpp", "sesa_common.hpp")
+KSRC = {"conv3x3": _MDX_SRC, "tdf": _MDX_SRC, "act": _MDX_SRC, "conv1x1": _MDX_SRC, "down": _MDX_SRC,
+        "up": _MDX_SRC, "tokgemm": _TOK_SRC + ("sesa_bsroformer.hip",), "attn": _TOK_SRC + ("sesa_bsroformer.hip",),
+        "hconv": _TOK_SRC + ("sesa_htdemucs.hip",), "lstm": ("sesa_scnet.hip", "sesa_tokgemm.hpp", "sesa_common.hpp")}
+
+
+def kernel_sources_sha16(kclass):
+    import hashlib
+    h = hashlib.sha256()
+    for fn in KSRC[kclass]:
+        with open(os.path.join(_CSRC, fn), "rb") as f:
+            h.update(fn.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kclass):
+    """(HBM bytes per launch, provenance) from profiles/pmc_<class>.json when its ``src_sha16`` matches
+    the kernel sources in this tree; (None, reason) otherwise -- a stale counter figure is not reported."""
+    pmc = os.path.join(REPO, "profiles", f"pmc_{kclass}.json")
+    if not os.path.exists(pmc):
+        return None, f"no profiles/pmc_{kclass}.json"
+    with open(pmc) as f:
+        d = json.load(f)
+    cur = kernel_sources_sha16(kclass)
+    if d.get("src_sha16") != cur:
+        return None, (f"profiles/pmc_{kclass}.json measured on sources {d.get('src_sha16')} (git "
+                      f"{d.get('git_sha', '?')}), this tree has {cur}: stale, not reported")
+    return d.get("hbm_bytes_per_launch"), {"file": f"profiles/pmc_{kclass}.json", "src_sha16": cur,
+                                           "git_sha": d.get("git_sha"), "algorithmic_bytes_per_launch":
+                                           d.get("algorithmic_bytes_per_launch")}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -107,7 +143,7 @@ def host_cpu():
     return threads, os.cpu_count(), model
 
 
-def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chunks):
+def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chunks, config0=True):
     """Oracle (PyTorch-CPU fp32) forward on `sample_chunks` chunks of the workload; extrapolated to
     the track (OLA < 1 % of CPU time)."""
     threads, ncpu, cpu_model = host_cpu()
@@ -146,6 +182,30 @@ def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chu
         chunk = int(cfg["audio"]["chunk_size"])
     rng = np.random.default_rng(0)
     x = torch.from_numpy((0.1 * rng.standard_normal((1, 2, chunk))).astype(np.float32))
+    if model_name == "mdx23c" and config0:
+        # BASELINE.json configs[0] / BASELINE.md §4: the 10 s track timed END TO END on the CPU path --
+        # chunker + forwards + windowed OLA (oracle/demix.py, inference_pytorch.py:55-186), batch_size 1
+        # as the vocals config sets it; the per-chunk wall of that run then prices the 4-min workload
+        from oracle.demix import demix as odemix
+        mix10 = (0.1 * np.random.default_rng(0).standard_normal((2, int(10 * 44100)))).astype(np.float32)
+        with torch.inference_mode():
+            fwd(params, cfg, x)                   # warm-up (allocator, oneDNN primitives)
+            t0 = time.time()
+            n_seen = []
+            odemix(cfg, lambda xb: fwd(params, cfg, xb), mix10, on_batch=lambda ch, y: n_seen.append(len(ch)))
+            wall10 = time.time() - t0
+        n10 = sum(n_seen)
+        per_chunk = wall10 / n10
+        return {"value": round(track_seconds / (per_chunk * n_chunks_track), 4), "unit": "separated-audio sec/sec",
+                "cores": threads, "kind": "port",
+                "host": {"cpu_model": cpu_model, "os_cpu_count": ncpu, "threads_used": threads},
+                "config0_end_to_end": {"track_seconds": 10.0, "chunks": n10, "wall_s": round(wall10, 2),
+                                       "value": round(10.0 / wall10, 4)},
+                "sample": f"BASELINE configs[0]: 10 s 44.1 kHz stereo track (seed 0) separated end to end on the CPU "
+                          f"path (oracle/demix.py chunker + OLA around oracle/mdx23c.py PyTorch-CPU fp32, full-width "
+                          f"vocals config, {n10} chunks, {threads} threads) in {wall10:.1f} s = {10.0 / wall10:.4f}x "
+                          f"real-time; value = that run's {per_chunk:.2f} s/chunk applied to the {n_chunks_track} "
+                          f"chunks of the {track_seconds:.0f} s workload"}
     with torch.inference_mode():
         fwd(params, cfg, x)                       # warm-up (allocator, oneDNN primitives)
         t0 = time.time()
@@ -204,14 +264,26 @@ def main():
     ap.add_argument("--cpu-sample-chunks", type=int, default=8)
     ap.add_argument("--blend", default="avg_wave", help="ensemble blend method (ensemble.py --type)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-chunks-only", action="store_true",
+                    help="mdx23c: time --cpu-sample-chunks forwards instead of the configs[0] 10 s end-to-end run")
     args = ap.parse_args()
     track_seconds = args.track_seconds or TRACK_SECONDS.get(args.model, 240.0)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from sesa.launch import needs_spawn, spawn_world, world_from_env
+    if needs_spawn(args.gpus):
+        # `python bench.py --gpus N` without torchrun: this parent has not touched HIP; it starts N
+        # fresh rank processes under torch.distributed.run as a child and exits with its code
+        log(f"bench: launching {args.gpus} ranks (torch.distributed.run, RCCL)")
+        sys.exit(spawn_world(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    rank, local_rank, world = world_from_env()
+    if world != args.gpus:
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report a mismatched run")
+        sys.exit(3)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if dist.get_world_size() != args.gpus:
+            log(f"bench: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+            sys.exit(3)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
@@ -244,6 +316,8 @@ def main():
 
     batches = [args.exec_batch or plan_exec_batch(m, c, chunk_len(cfg, md), dev, world=world)
                for (m, cfg, _), c, md in zip(members, chunks, modes)]
+    from sesa.parallel import shard_plan
+    shard_ranges = [shard_plan(cfg, n, world, md)["ranges"] for (_, cfg, _), md in zip(members, modes)]
     path_flop = sum(c * MODELS[nm][1] for c, nm in zip(chunks, names))
     stems_host = None
 
@@ -297,15 +371,11 @@ def main():
     note = f"2.5 PF/s dense bf16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
     if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
         peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", f"pmc_{kclass}.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    traffic, traffic_src = pmc_traffic(kclass)
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": KDESC[kclass],
             "launches": launches, "avg_launch_ms": round(ms / max(launches, 1), 4),
-            "flop_per_launch": round(work / max(launches, 1)), "peak_note": note}
+            "flop_per_launch": round(work / max(launches, 1)), "peak_note": note, "traffic_source": traffic_src}
     path_tflops = path_flop * args.steps / elapsed / 1e12
 
     value = track_seconds * args.steps / elapsed
@@ -328,6 +398,9 @@ def main():
                        "model": args.model, "chunks": n_chunks,
                        "exec_batch": batches[0] if len(batches) == 1 else batches,
                        "parallelism": f"chunk-shard x{world} + RCCL all_gather" if world > 1 else "1 GPU",
+                       "shard": {"world_size": dist.get_world_size() if world > 1 else 1,
+                                 "backend": dist.get_backend() if world > 1 else None,
+                                 "chunk_ranges": shard_ranges[0] if len(shard_ranges) == 1 else shard_ranges},
                        "path_tflops_algorithmic": round(path_tflops, 2)},
             "roofline": roof,
         }
@@ -353,8 +426,24 @@ def main():
             line["attention"] = {"kernel": KDESC["attn"],
                                  "achieved_tflops": round(awork / (ams * 1e-3) / 1e12, 2) if ams > 0 else 0.0,
                                  "launches": alaunch, "avg_launch_ms": round(ams / max(alaunch, 1), 4)}
+        if args.model == "mdx23c":
+            # north_star parity, measured by the bench itself: the same model (same weights) on the
+            # reference's own full-chunk output (tests/golden/mdx23c_full_chunk.npz, the reference
+            # TFC_TDF_net run in fp32 on CPU by tests/golden/make_golden.py), per-sample RMS
+            gp = os.path.join(REPO, "tests", "golden", "mdx23c_full_chunk.npz")
+            if os.path.exists(gp):
+                g = np.load(gp, allow_pickle=False)
+                with torch.no_grad():
+                    y = members[0][0](torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+                err = float(np.sqrt(np.mean((y.astype(np.float64) - g["y"]) ** 2)))
+                line["parity_rms"] = err
+                line["parity"] = {"rms_vs_reference": err, "gate": 1e-4, "within_gate": err <= 1e-4,
+                                  "precision": args.precision,
+                                  "fixture": "tests/golden/mdx23c_full_chunk.npz (reference TFC_TDF_net, fp32 CPU, "
+                                             "one 261120-sample chunk, same name-keyed weights)"}
         if world == 1 and not args.no_cpu_baseline:
-            parts = [cpu_baseline(nm, cp, c, track_seconds, args.cpu_sample_chunks if len(names) == 1 else 2)
+            parts = [cpu_baseline(nm, cp, c, track_seconds, args.cpu_sample_chunks if len(names) == 1 else 2,
+                                  config0=len(names) == 1 and not args.cpu_chunks_only)
                      for nm, (_, _, cp), c in zip(names, members, chunks)]
             if len(parts) == 1:
                 line["cpu_baseline"] = parts[0]

@@ -641,6 +641,7 @@ TokGemmArgs gemm_args(const sesa_bsr* m, const Gemm& gm, const float* x, int64_t
   a.n_groups = (int)gm.groups.size();
   a.n_tiles_n = gm.n_tiles_n;
   a.k8 = gm.k8;
+  a.n4 = gm.n4;
   a.M = M;
   a.act = TOK_ACT_NONE;
   a.dim_head = m->cfg.dim_head;

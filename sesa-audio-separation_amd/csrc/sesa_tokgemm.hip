@@ -981,7 +981,7 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
     int ep = -1;
     if (glds && x3 && a.k8 && a.a_ld % 8 == 0 && !a.glu && !a.conv && a.o_ld % 4 == 0 &&
         (a.act == TOK_ACT_NONE || a.act == TOK_ACT_GELU) && (!a.rope || (a.dim_head == 64 && !a.residual)) &&
-        (!a.out_hi || a.out_lo)) {
+        (!a.out_hi || a.out_lo) && (!a.residual || a.n4)) {
       ep = (a.rownorm ? EP_RS : 0) | (a.rope ? EP_ROPE : 0) | (a.act == TOK_ACT_GELU ? EP_GELU : 0) |
            (a.residual ? EP_RES : 0) | (a.out_hi ? EP_SPLIT : 0);
     }

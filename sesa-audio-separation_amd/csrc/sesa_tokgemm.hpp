@@ -70,6 +70,8 @@ struct TokGemmArgs {
   int64_t a_ld;
   const float* row_scale;
   int k8;                     // every group's K % 8 == 0 (Gemm::k8): pre-split A may take the LDS-DMA kernel
+  int n4;                     // every group's N % 4 == 0 and o_off % 4 == 0 (Gemm::n4): the LDS-DMA
+                              // kernel's residual epilogue stages 16-B pieces and needs it
   // Split epilogue: write bf16 planes out_hi / out_lo [.][o_ld] instead of fp32 `out` (the result
   // only feeds another tok_gemm; no residual).  out_lo may be null (bf16).
   uint16_t* out_hi;
@@ -125,6 +127,7 @@ struct Gemm {          // one packed (possibly grouped) GEMM
   TokGroup* d_groups = nullptr;
   int n_tiles_n = 0;
   int k8 = 0;          // every group's K % 8 == 0
+  int n4 = 0;          // every group's N % 4 == 0 and o_off % 4 == 0
 };
 
 // Pack W[n][k] (row accessor) of an N x K GEMM for one group; returns the TokGroup with w_off/b_off set.
@@ -170,9 +173,11 @@ inline int upload_groups(Gemm& gm) {
   SESA_CHECK_HIP(hipMemcpy(gm.d_groups, gm.groups.data(), gm.groups.size() * sizeof(TokGroup), hipMemcpyHostToDevice));
   gm.n_tiles_n = 0;
   gm.k8 = 1;
+  gm.n4 = 1;
   for (auto& g : gm.groups) {
     gm.n_tiles_n = std::max(gm.n_tiles_n, (g.N + kTokBN - 1) / kTokBN);
     if (g.K % 8) gm.k8 = 0;
+    if (g.N % 4 || g.o_off % 4) gm.n4 = 0;
   }
   return SESA_OK;
 }

@@ -67,6 +67,16 @@ def _lib():
     return N
 
 
+def flac_max_samples(data, channels):
+    """Upper bound on the samples per channel a FLAC stream of ``len(data)`` bytes can decode to
+    (RFC 9639): every frame holds at most STREAMINFO's maximum block size and takes at least a
+    6-byte header, a 2-byte CRC-16 and a 2-byte CONSTANT subframe per channel.  Guards the
+    preallocation against a corrupt or hostile 36-bit total_samples."""
+    max_block = struct.unpack(">H", data[10:12])[0] if len(data) >= 12 else 65535
+    min_frame = 6 + 2 + 2 * max(1, channels)
+    return (len(data) // min_frame + 1) * max(16, max_block or 65535)
+
+
 def read_flac(path):
     N = _lib()
     with open(path, "rb") as f:
@@ -75,6 +85,10 @@ def read_flac(path):
     ch, sr, bits, frames = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
     N.check(N.lib().sesa_flac_info(buf, len(data), ctypes.byref(ch), ctypes.byref(sr), ctypes.byref(bits),
                                    ctypes.byref(frames)), f"FLAC {path}")
+    bound = flac_max_samples(data, ch.value)
+    if frames.value < 0 or frames.value > bound:
+        raise ValueError(f"FLAC {path}: STREAMINFO declares {frames.value} samples, more than the "
+                         f"{len(data)}-byte file can hold (<= {bound}); corrupt header")
     out = np.zeros((frames.value, ch.value), np.float32)
     got = ctypes.c_int64()
     N.check(N.lib().sesa_flac_decode(buf, len(data), out.ctypes.data, frames.value, ctypes.byref(got)),

@@ -63,10 +63,22 @@ def chunk_plan(L, chunk_size, num_overlap, batch_size):
 EXEC_CAP = {"TFC_TDF_net": 64, "BSRoformer": 4, "MelBandRoformer": 4, "SCNet": 48, "HTDemucs": 32}
 
 
+def unwrap_model(model):
+    """The network behind a backend (HipBackend.compiled_model / .model), else ``model`` itself."""
+    for attr in ("compiled_model", "model"):
+        inner = getattr(model, attr, None)
+        if inner is not None and not isinstance(inner, (str, bytes)) and callable(inner):
+            return inner
+    return model
+
+
 def plan_exec_batch(model, n_chunks, chunk, device=None, world=1, cap=None):
     """Execution batch for ``n_chunks`` chunks of length ``chunk`` spread over ``world`` ranks: the
     model's cap (EXEC_CAP), halved while its workspace would exceed half the free HBM, then balanced
-    so a rank's last forward is not a small remainder (169 chunks at cap 64 -> 3 forwards of 57)."""
+    so a rank's last forward is not a small remainder (169 chunks at cap 64 -> 3 forwards of 57).
+    ``model`` may be the network or a backend wrapping it (HipBackend: the CLI and utils.demix pass
+    the backend), so the CLI plans the same batch as bench.py."""
+    model = unwrap_model(model)
     cap = int(cap or EXEC_CAP.get(type(model).__name__, 8))
     if hasattr(model, "workspace_bytes") and torch.cuda.is_available():
         try:

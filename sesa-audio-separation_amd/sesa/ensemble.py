@@ -19,7 +19,7 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .audio_io import read_wav, write_audio
+from .audio_io import quantize_pcm, read_wav, write_audio
 
 METHODS = ["avg_wave", "median_wave", "max_wave", "min_wave", "max_fft", "min_fft", "median_fft"]
 _SPECIAL = "[]()|&; "
@@ -95,7 +95,9 @@ class AudioEnsembleEngine:
     def _load(self, path):
         data, sr = read_wav(path)                       # float32 [ch, frames], soundfile scaling
         if self.requantize_special_paths and any(c in os.path.abspath(path) for c in _SPECIAL):
-            data = (np.round(np.clip(data, -1.0, 1.0 - 1.0 / 32768) * 32768.0) / 32768.0).astype(np.float32)
+            # librosa.load + sf.write(temp) at soundfile's default PCM_16, read back (ensemble.py:70-79):
+            # libsndfile's float -> PCM_16 write is lrintf(x * 0x7FFF) (no clipping), its read x / 0x8000
+            data = (quantize_pcm(data, 16) / 32768.0).astype(np.float32)
         return data, sr
 
     def validate_inputs(self, files, method):

@@ -53,16 +53,15 @@ class TFC_TDF_net(NativeModule):
         finally:
             self._fn("destroy")(h)
         self._register_params([(n, shapes[n]) for n in names])
-        self._ws_bytes = {}
 
     def _config(self, chunk):
         return N.SesaMdx23cConfig(**self._ccfg,
                                   precision=N.SESA_PREC_BF16 if self.precision == "bf16" else N.SESA_PREC_BF16X3)
 
     def workspace_bytes(self, batch, chunk=None):
-        if batch not in self._ws_bytes:
-            self._ws_bytes[batch] = super().workspace_bytes(batch, self._ccfg["chunk_size"])
-        return self._ws_bytes[batch]
+        # not cached: the size depends on the precision (bf16x3 adds lo planes) and on the process-wide
+        # conv3x3 variant as well as on the batch; the host-side dry run costs well under a millisecond
+        return super().workspace_bytes(batch, self._ccfg["chunk_size"])
 
     def _out_shape(self, B, ch, C):
         return (B, self.num_target_instruments, ch, C)

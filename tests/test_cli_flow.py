@@ -147,3 +147,22 @@ def test_pcm_quantize_matches_libsndfile_rule():
     assert q[:5].tolist() == [0, 16384, -16384, 32767, -32767]   # lrintf(x * 0x7FFF), half to even
     assert q[5] == 2 and q[6] == 2
     assert q[7] == ((int(np.rint(np.float32(1.2) * np.float32(32767))) + 32768) % 65536) - 32768  # wraps
+
+
+def test_flac_rejects_oversized_streaminfo_total(tmp_path):
+    """A corrupt STREAMINFO total_samples (36-bit field) must not size the decode buffer: the reader
+    bounds it by what the file's bytes can hold and raises before allocating."""
+    from sesa.audio_io import flac_max_samples, read_any, write_audio
+    x = np.full((2, 5000), 0.25, np.float32)
+    p = tmp_path / "ok.flac"
+    write_audio(str(p), x.T, 44100, subtype="PCM_16")
+    data = bytearray(p.read_bytes())
+    assert read_any(str(p))[0].shape == (2, 5000)
+    # STREAMINFO body at byte 8; total_samples = low 4 bits of byte 21 + bytes 22..25
+    data[21] = (data[21] & 0xF0) | 0x0F
+    data[22:26] = b"\xff\xff\xff\xff"
+    bad = tmp_path / "bad.flac"
+    bad.write_bytes(bytes(data))
+    assert flac_max_samples(bytes(data), 2) < (1 << 36) - 1
+    with pytest.raises(Exception, match="corrupt header|STREAMINFO|FLAC"):
+        read_any(str(bad))

@@ -5,8 +5,11 @@ in SEPARATE passes (TCC slots), both in KiB; on gfx950 FETCH_SIZE reports exactl
 of a wide coalesced streaming read, so it is doubled before comparing with byte counts.
 
 usage: python tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> <kernel-substring[|substring...]> [out.json]
+                                    [kernel-class]
 (a dispatch matches if its name contains any of the '|'-separated substrings: one kernel CLASS, as
-bench.py's roofline times it)
+bench.py's roofline times it).  With a kernel class (bench.py KSRC key) the summary is stamped with
+``src_sha16`` of that class's sources in this tree and ``git_sha`` from $GIT_SHA, so bench.py reports
+the figure only for the sources it was measured on.
 """
 import csv
 import glob
@@ -47,7 +50,7 @@ def read_counter(d, counter):
     return per, names
 
 
-def main(fetch_dir, write_dir, substr, out=None):
+def main(fetch_dir, write_dir, substr, out=None, kclass=None):
     f, fn = read_counter(fetch_dir, "FETCH_SIZE")
     w, wn = read_counter(write_dir, "WRITE_SIZE")
     subs = substr.split("|")
@@ -62,6 +65,15 @@ def main(fetch_dir, write_dir, substr, out=None):
            "hbm_bytes_per_launch": round((2 * fetch_kib + write_kib) * 1024),
            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts half of "
                          "wide coalesced reads; MI355X_MICROARCH.md §HBM)"}
+    if kclass:
+        import importlib.util
+        here = os.path.dirname(os.path.abspath(__file__))
+        spec = importlib.util.spec_from_file_location("bench", os.path.join(here, "..", "bench.py"))
+        bench = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(bench)
+        res["kernel_class"] = kclass
+        res["src_sha16"] = bench.kernel_sources_sha16(kclass)
+        res["git_sha"] = os.environ.get("GIT_SHA", "unknown")
     print(json.dumps(res, indent=1))
     if out:
         with open(out, "w") as fo:
