@@ -453,7 +453,14 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 // Weight image and A-image layouts are exactly tap_gemm_kernel's (same host packing).
 // EPI (ablation knob for tools/conv_bench.hip; the product uses 0): 1 = store without statistics,
 // 2 = no epilogue.
-template <bool X3, bool XTRA, int EPI = 0>
+// ACT: the main input is the RAW fp32 producer output (one or two channel-concatenated sources, mode
+// SRC_NORM_GELU) and the consumer's InstanceNorm affine + exact GELU + bf16 hi/lo split run in the
+// staging step (same arithmetic as act_split_kernel, so the operands are bit-identical), instead of a
+// separate act_split pass over HBM (8 B per element).  The per-channel affine of this batch item is
+// built once per workgroup into LDS (kActMaxC channels).  Each thread stages a fixed 8-channel half of
+// every chunk (tid & 1), so its 8 (scale, shift) pairs are two ds_read_b128 per chunk.
+constexpr int kActMaxC = 1024;
+template <bool X3, bool XTRA, int EPI = 0, bool ACT = false>
 __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   constexpr int NT = 512;
   constexpr int TM = 16, WM = 8, MI = 2, NI = 2, BN = 64;
@@ -463,6 +470,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   constexpr int W1_BYTES = BN * 32;
   constexpr int STAGE = 2 * A_BYTES + 2 * W_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) float act_sc[ACT ? kActMaxC : 1], act_sh[ACT ? kActMaxC : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -495,6 +503,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   const uint16_t* wblk = a.w + (int64_t)nb * (n_main * W_BYTES + (XTRA ? a.x_chunks * W1_BYTES : 0));
   const Src src = pick_src(a.in, 0);
   const int C = src.C;
+  if constexpr (ACT) build_affine(a.in, b, act_sc, act_sh);   // ordered before use by the first barrier
 
   f32x16 acc[MI][NI];
 #pragma unroll
@@ -514,6 +523,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   u32x4 wreg[W_ITEMS];
   uint32_t avalid = 0;  // per staging item: inside the input image (else stored as zeros)
 
+  int act_c = 0;  // ACT: first (global, concatenated) channel of this thread's 8-channel half of the staged chunk
   auto load_main = [&](int kc) {
     const u32x4* wsrc = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * W_BYTES);
     Unroll<0, W_ITEMS>::run([&](auto I) {
@@ -521,6 +531,12 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       wreg[I] = wsrc[e < W16 ? e : W16 - 1];
     });
     const int cl0 = kc * kConvBK;
+    // ACT: the chunk's source (chunks never straddle the concatenation: C_split % 16 == 0)
+    const int s1 = ACT && cl0 >= a.in.C_split;
+    const float* xp = ACT ? (s1 ? a.in.src[1].ptr : a.in.src[0].ptr) : nullptr;
+    const int xc = ACT ? (s1 ? a.in.src[1].C : a.in.src[0].C) : 0;
+    const int xl0 = ACT ? cl0 - (s1 ? a.in.C_split : 0) : 0;
+    if (ACT) act_c = cl0 + 8 * (tid & 1);
     Unroll<0, P_ITEMS>::run([&](auto I) {
       constexpr int i = decltype(I)::value;
       // straight-line (no branches, so the scheduler can spread it under the MFMAs): surplus
@@ -531,9 +547,17 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       const int ti = t_in0 + hr, fi = f_in0 + hc;
       const bool ok = ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in;
       const int tc = min(max(ti, 0), a.T_in - 1), fc = min(max(fi, 0), a.F_in - 1);
-      const int64_t idx = (((int64_t)b * a.T_in + tc) * a.F_in + fc) * C + cl0 + 8 * hf;
-      areg[2 * i] = *reinterpret_cast<const f32x4*>(src.hi + idx);
-      areg[2 * i + 1] = *reinterpret_cast<const f32x4*>(src.lo + idx);
+      if constexpr (ACT) {
+        // raw fp32: 8 channels = 32 contiguous bytes (the same 4 B per element as the hi + lo planes)
+        const f32x4* xq = reinterpret_cast<const f32x4*>(
+            xp + (((int64_t)b * a.T_in + tc) * a.F_in + fc) * xc + xl0 + 8 * hf);
+        areg[2 * i] = xq[0];
+        areg[2 * i + 1] = xq[1];
+      } else {
+        const int64_t idx = (((int64_t)b * a.T_in + tc) * a.F_in + fc) * C + cl0 + 8 * hf;
+        areg[2 * i] = *reinterpret_cast<const f32x4*>(src.hi + idx);
+        areg[2 * i + 1] = *reinterpret_cast<const f32x4*>(src.lo + idx);
+      }
       if (i == 0) avalid = 0;
       avalid |= (uint32_t)ok << i;  // zeroing is applied at store time, so nothing waits on the load here
     });
@@ -546,15 +570,42 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       const int e = min(tid + I * NT, W16 - 1);  // duplicates write identical values
       wdst[e] = wreg[I];
     });
+    f32x2 asc[4], ash[4];
+    if constexpr (ACT) {
+      const f32x4 s0 = *reinterpret_cast<const f32x4*>(act_sc + act_c);
+      const f32x4 s1 = *reinterpret_cast<const f32x4*>(act_sc + act_c + 4);
+      const f32x4 h0 = *reinterpret_cast<const f32x4*>(act_sh + act_c);
+      const f32x4 h1 = *reinterpret_cast<const f32x4*>(act_sh + act_c + 4);
+      asc[0] = f32x2{s0[0], s0[1]}; asc[1] = f32x2{s0[2], s0[3]}; asc[2] = f32x2{s1[0], s1[1]}; asc[3] = f32x2{s1[2], s1[3]};
+      ash[0] = f32x2{h0[0], h0[1]}; ash[1] = f32x2{h0[2], h0[3]}; ash[2] = f32x2{h1[0], h1[1]}; ash[3] = f32x2{h1[2], h1[3]};
+    }
     Unroll<0, P_ITEMS>::run([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int e = min(tid + i * NT, NPOS * 2 - 1);
       const int p = e >> 1, hf = e & 1;
       const int off = p * 32 + ((hf ^ ((p >> 3) & 1)) << 4);
       const bool ok = (avalid >> i) & 1u;
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f32x4*>(A_hi + off) = ok ? areg[2 * i] : z;
-      if (X3) *reinterpret_cast<f32x4*>(A_lo + off) = ok ? areg[2 * i + 1] : z;
+      if constexpr (ACT) {
+        // act_split_kernel's arithmetic: y = GELU(fma(x, scale, shift)) on float2 pairs, then hi / lo
+        const f32x4 x0 = areg[2 * i], x1 = areg[2 * i + 1];
+        const f32x2 v[4] = {f32x2{x0[0], x0[1]}, f32x2{x0[2], x0[3]}, f32x2{x1[0], x1[1]}, f32x2{x1[2], x1[3]}};
+        uint32_t hw[4], lw[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 y = gelu_erf2(__builtin_elementwise_fma(v[q], asc[q], ash[q]));
+          __bf16 h0, l0, h1, l1;
+          split_bf16(y[0], h0, l0);
+          split_bf16(y[1], h1, l1);
+          hw[q] = ok ? pack2(h0, h1) : 0u;
+          lw[q] = ok ? pack2(l0, l1) : 0u;
+        }
+        *reinterpret_cast<u32x4*>(A_hi + off) = u32x4{hw[0], hw[1], hw[2], hw[3]};
+        if (X3) *reinterpret_cast<u32x4*>(A_lo + off) = u32x4{lw[0], lw[1], lw[2], lw[3]};
+      } else {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(A_hi + off) = ok ? areg[2 * i] : z;
+        if (X3) *reinterpret_cast<f32x4*>(A_lo + off) = ok ? areg[2 * i + 1] : z;
+      }
     });
   };
   // ext chunk kx (0-based over the shortcut input's channels): raw fp32, inner positions only
@@ -639,6 +690,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
 
   // ---- main chunks: straight-line pipelined body, clamped (redundant) prefetch at the tail ----
   load_main(0);
+  if constexpr (ACT) __syncthreads();   // the LDS affine table, before the first staging step reads it
   store_main(smem);
   load_main(min(1, n_main - 1));
   __syncthreads();
@@ -1941,6 +1993,13 @@ bool tap_bn128_enabled() {
   return v;
 }
 
+// conv3x3_db_kernel<ACT>: the consumer's norm + GELU + split fused into the staging (no act_split pass);
+// SESA_CONV_FUSED_ACT=0 keeps the act_split + pre-activated kernel everywhere (A/B).
+bool conv3x3_fused_act_ok(int T_out, int C_in) {
+  static const bool on = !(getenv("SESA_CONV_FUSED_ACT") && std::string(getenv("SESA_CONV_FUSED_ACT")) == "0");
+  return on && conv_variant() == 0 && T_out >= 32 && C_in <= kActMaxC && C_in % kConvBK == 0;
+}
+
 bool conv3x3_m16_selected(int T_out, int C_in, int C_out, int C_shortcut) {
   return conv_variant() == 1 && T_out >= 32 && C_in % 32 == 0 && C_out % 16 == 0 && C_shortcut % 32 == 0;
 }
@@ -1978,19 +2037,36 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
       }
       if (a.T_out >= 32 && a.out.residual == nullptr && a.out.gelu == 0) {
         // double-buffered 16-row tile (levels with T >= 32); tile rows past T_out are masked
-        SESA_REQUIRE(a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && a.in.src[0].lo && a.in.C_split == a.in.C_in,
-                     SESA_ERR_INVALID, "conv3x3: needs a single pre-activated (act_split) input");
+        const bool act = a.in.src[0].mode == SRC_NORM_GELU;
+        if (act) {
+          SESA_REQUIRE(conv3x3_fused_act_ok(a.T_out, a.in.C_in) && a.in.src[0].ptr && a.in.src[0].stats &&
+                           (a.in.C_split == a.in.C_in ||
+                            (a.in.src[1].mode == SRC_NORM_GELU && a.in.src[1].ptr && a.in.src[1].stats)) &&
+                           a.in.src[0].C % 8 == 0 && (a.in.C_split == a.in.C_in || a.in.src[1].C % 8 == 0),
+                       SESA_ERR_INVALID, "conv3x3: fused-activation input must be normalised fp32 sources, C <= %d",
+                       kActMaxC);
+        } else {
+          SESA_REQUIRE(a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && a.in.src[0].lo && a.in.C_split == a.in.C_in,
+                       SESA_ERR_INVALID, "conv3x3: needs a single pre-activated (act_split) input");
+        }
         dim3 grid((unsigned)(((a.T_out + 15) / 16) * (a.F_out / kTF) * ((a.n_cols + 63) / 64)), 1u, (unsigned)batch);
-        if (a.x_chunks > 0) {
+        if (a.x_chunks > 0)
           SESA_REQUIRE(a.xin.C_in % kConvBK == 0 && a.xin.C_split % kConvBK == 0 && a.xin.src[0].mode == SRC_RAW &&
                            a.xin.src[1].mode == SRC_RAW,
                        SESA_ERR_INVALID, "conv3x3: fused shortcut must be a raw input, C_in multiple of %d", kConvBK);
-          if (x3) hipLaunchKernelGGL((conv3x3_db_kernel<true, true>), grid, dim3(512), 0, st, a);
-          else hipLaunchKernelGGL((conv3x3_db_kernel<false, true>), grid, dim3(512), 0, st, a);
+#define SESA_DB(X3V, XTRAV)                                                                              \
+  do {                                                                                                  \
+    if (act) hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, true>), grid, dim3(512), 0, st, a);    \
+    else hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, false>), grid, dim3(512), 0, st, a);       \
+  } while (0)
+        if (a.x_chunks > 0) {
+          if (x3) SESA_DB(true, true);
+          else SESA_DB(false, true);
         } else {
-          if (x3) hipLaunchKernelGGL((conv3x3_db_kernel<true, false>), grid, dim3(512), 0, st, a);
-          else hipLaunchKernelGGL((conv3x3_db_kernel<false, false>), grid, dim3(512), 0, st, a);
+          if (x3) SESA_DB(true, false);
+          else SESA_DB(false, false);
         }
+#undef SESA_DB
         SESA_CHECK_LAUNCH();
         return SESA_OK;
       }
