@@ -469,8 +469,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   constexpr int W_BYTES = 9 * BN * 32;
   constexpr int W1_BYTES = BN * 32;
   constexpr int STAGE = 2 * A_BYTES + 2 * W_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  __shared__ __attribute__((aligned(16))) float act_sc[ACT ? kActMaxC : 1], act_sh[ACT ? kActMaxC : 1];
+  // (one LDS array: the ACT affine table sits past the two stages)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (ACT ? 2 * kActMaxC * 4 : 0)];
+  float* act_sc = reinterpret_cast<float*>(smem + 2 * STAGE);
+  float* act_sh = act_sc + kActMaxC;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
