@@ -390,8 +390,8 @@ struct Fwd {
 
   // Input of a TFC 3x3 conv (norm + GELU of `a` [++ `b`]): the raw normalised sources when the conv
   // kernel fuses the activation into its staging (T >= 32 levels), else one act_split pass.
-  GemmIn conv3_input(Tensor a, Tensor b, const Norm* nrm, int T, int F) {
-    if (conv3x3_fused_act_ok(T, a.C + (b.C > 0 ? b.C : 0)))
+  GemmIn conv3_input(Tensor a, Tensor b, const Norm* nrm, int T, int F, int C_out) {
+    if (conv3x3_fused_act_ok(T, a.C + (b.C > 0 ? b.C : 0), C_out))
       return input(a, b, SRC_NORM_GELU, SRC_NORM_GELU, nrm, T, F);
     return act(a, b, nrm, T, F);
   }
@@ -414,7 +414,7 @@ struct Fwd {
       // x = tfc1(x); the shortcut's operand is split here too when conv2 runs on conv3x3_m16_kernel
       const bool pre_sc = conv3x3_m16_selected(L.T, c, c, x0.C + (x1.C > 0 ? x1.C : 0));
       GemmIn xs{};
-      conv(bk.conv1, pre_sc ? act(x0, x1, &bk.tfc1, L.T, L.F, &xs) : conv3_input(x0, x1, &bk.tfc1, L.T, L.F), L.T, L.F,
+      conv(bk.conv1, pre_sc ? act(x0, x1, &bk.tfc1, L.T, L.F, &xs) : conv3_input(x0, x1, &bk.tfc1, L.T, L.F, c), L.T, L.F,
            L.T, L.F, H, nullptr, st_h1, 0);
       // x = x + tdf(x)
       tdf(bk.lin1, input(Tensor{H, st_h1, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf0, L.T, L.F), L.T, U, nullptr, st_u,
@@ -425,7 +425,7 @@ struct Fwd {
           c, 1, Up);
       // x = tfc2(x) + shortcut(block input): the 1x1 shortcut rides along as extra K (raw input)
       if (!pre_sc) xs = input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F);
-      conv(bk.conv2, conv3_input(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F), L.T, L.F, L.T, L.F, S, nullptr,
+      conv(bk.conv2, conv3_input(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F, c), L.T, L.F, L.T, L.F, S, nullptr,
            st_out, 0, &xs);
       x0 = Tensor{S, st_out, c};
       x1 = Tensor{};

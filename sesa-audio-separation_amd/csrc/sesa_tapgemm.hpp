@@ -77,7 +77,7 @@ bool conv3x3_m16_selected(int T_out, int C_in, int C_out, int C_shortcut);
 // True when a same-size 3x3 conv at T_out with C_in normalised input channels runs conv3x3_db_kernel with
 // the InstanceNorm + GELU + split fused into its staging: its input is then given as the raw fp32
 // sources (SRC_NORM_GELU) instead of act_split planes.
-bool conv3x3_fused_act_ok(int T_out, int C_in);
+bool conv3x3_fused_act_ok(int T_out, int C_in, int C_out);
 int set_conv3x3_variant(int v);
 bool tap_bn128_enabled();  // SESA_TAP_BN128=0 disables the 128-column down / up tiles (A/B)  // 0 = conv3x3_db_kernel, 1 = conv3x3_m16_kernel; returns the previous
 int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io);

@@ -78,6 +78,91 @@ int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 57;
   printf("batch %d\n%-5s %-26s %9s %9s\n", B, "level", "variant", "ms", "TF/s(alg)");
   const bool only_tdf = argc > 2 && strcmp(argv[2], "tdf") == 0;  // ./tools/conv_bench 57 tdf
+  const bool only_act = argc > 2 && strcmp(argv[2], "act") == 0;  // ./tools/conv_bench 57 act
+  if (only_act) {
+    // act_split + pre-activated conv3x3_db_kernel vs conv3x3_db_kernel<ACT> (norm + GELU + split fused
+    // into the staging) on the level shapes; cat: two channel-concatenated sources (decoder tfc1)
+    for (int lvl = 0; lvl < 4; ++lvl)
+      for (int cat = 0; cat < 2; ++cat) {
+        const int Co = 128 * (lvl + 1), C = cat ? 2 * Co : Co, T = 256 >> lvl, F = 1024 >> lvl;
+        const int64_t n_act = (int64_t)B * T * F * C, n_out = (int64_t)B * T * F * Co;
+        float *x, *out, *out2;
+        uint16_t *hi, *lo, *w;
+        double *st_x, *st_o;
+        const int nblk = Co / 64, nch = C / kConvBK;
+        const int64_t w_elems = (int64_t)nblk * nch * 2 * 9 * 64 * 16;
+        CK(hipMalloc(&x, n_act * 4));
+        CK(hipMalloc(&hi, n_act * 2));
+        CK(hipMalloc(&lo, n_act * 2));
+        CK(hipMalloc(&w, w_elems * 2));
+        CK(hipMalloc(&out, n_out * 4));
+        CK(hipMalloc(&out2, n_out * 4));
+        CK(hipMalloc(&st_x, (size_t)B * C * 16));
+        CK(hipMalloc(&st_o, (size_t)B * Co * 16));
+        hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint16_t*>(x), n_act * 2, 4u, 1.f);
+        hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, w, w_elems, 3u, 0.03f);
+        std::vector<double> sth((size_t)B * C * 2);
+        for (size_t i = 0; i < sth.size(); i += 2) { sth[i] = 0.1 * (double)T * F; sth[i + 1] = 0.8 * (double)T * F; }
+        CK(hipMemcpy(st_x, sth.data(), sth.size() * 8, hipMemcpyHostToDevice));
+        GemmIn gin{};
+        const int c0 = cat ? Co : C;
+        gin.src[0] = Src{x, st_x, nullptr, c0, SRC_NORM_GELU, nullptr, nullptr};
+        gin.src[1] = cat ? Src{x + (int64_t)B * T * F * c0, st_x + (size_t)B * c0 * 2, nullptr, C - c0, SRC_NORM_GELU,
+                               nullptr, nullptr}
+                         : gin.src[0];
+        gin.C_split = c0;
+        gin.C_in = C;
+        gin.inv_count = 1.0 / ((double)T * F);
+        ConvArgs a{};
+        a.out.ptr = out;
+        a.out.stats = st_o;
+        a.out.C_out = Co;
+        a.w = w;
+        a.T_in = a.T_out = T;
+        a.F_in = a.F_out = F;
+        a.n_cols = Co;
+        a.n_chunks = nch;
+        ConvArgs ap = a;     // pre-activated operands from act_split
+        ap.in = GemmIn{};
+        ap.in.src[0] = Src{nullptr, nullptr, nullptr, C, SRC_PRE, hi, lo};
+        ap.in.src[1] = ap.in.src[0];
+        ap.in.C_split = C;
+        ap.in.C_in = C;
+        ConvArgs af = a;     // fused
+        af.in = gin;
+        af.out.ptr = out2;
+        const double flop = 2.0 * B * T * F * (double)Co * C * 9;
+        const dim3 grid((unsigned)(((T + 15) / 16) * (F / kTF) * ((Co + 63) / 64)), 1u, (unsigned)B);
+        const float ms_split = time_ms([&] { launch_act_split(gin, (int64_t)T * F, B, hi, lo, 0); });
+        const float ms_pre = time_ms([&] { hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0, false>), grid, dim3(512), 0, 0, ap); });
+        const float ms_act = time_ms([&] { hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0, true>), grid, dim3(512), 0, 0, af); });
+        unsigned int* dm;
+        CK(hipMalloc(&dm, 8));
+        CK(hipMemset(dm, 0, 8));
+        launch_act_split(gin, (int64_t)T * F, B, hi, lo, 0);
+        hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0, false>), grid, dim3(512), 0, 0, ap);
+        hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0, true>), grid, dim3(512), 0, 0, af);
+        hipLaunchKernelGGL(max_diff, dim3(2048), dim3(256), 0, 0, out, out2, n_out, dm);
+        unsigned int hh[2];
+        CK(hipMemcpy(hh, dm, 8, hipMemcpyDeviceToHost));
+        float d, m;
+        memcpy(&d, &hh[0], 4);
+        memcpy(&m, &hh[1], 4);
+        printf("L%d%s C_in %4d: act_split %7.3f + db %7.3f = %7.3f ms | fused %7.3f ms (%6.1f TF/s) | max|diff| "
+               "%.2e (max|out| %.2e) %s\n", lvl, cat ? " cat" : "    ", C, ms_split, ms_pre, ms_split + ms_pre, ms_act,
+               flop / ms_act * 1e-9, d, m, d == 0.f ? "IDENTICAL" : "DIFFERENT");
+        CK(hipFree(dm));
+        CK(hipFree(x));
+        CK(hipFree(hi));
+        CK(hipFree(lo));
+        CK(hipFree(w));
+        CK(hipFree(out));
+        CK(hipFree(out2));
+        CK(hipFree(st_x));
+        CK(hipFree(st_o));
+      }
+    return 0;
+  }
   for (int lvl = 0; lvl < (only_tdf ? 0 : 4); ++lvl) {
     const int C = 128 * (lvl + 1), T = 256 >> lvl, F = 1024 >> lvl;
     const int64_t n_act = (int64_t)B * T * F * C;
