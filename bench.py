@@ -70,7 +70,9 @@ WORKLOAD = {"ensemble": "ensemble.py flow: mdx23c vocals + bs_roformer vocals + 
             "bs_roformer": "bs_roformer (viperx 1297: dim 512, depth 12, 8x64 heads, 62 bands) vocals config",
             "scnet": "scnet musdb18 config (dims 4/32/64/128, 6 dual-path bi-LSTM layers, 4 sources)",
             "htdemucs": "demucs4ht htdemucs musdb18 config (channels 48, depth 4, bottom 512, 5 cross-transformer "
-                        "layers, 4 sources), utils.demix demucs mode (segment 11 s, overlap 4)"}
+                        "layers, 4 sources)"}
+HTD_MODE = {"generic": "live CLI chunker (inference.py -> demix_pytorch_optimized generic mode, chunk 485100, overlap 4)",
+            "demucs": "utils.demix demucs mode (segment 11 s, overlap 4, no fades / border pad)"}
 TRACK_SECONDS = {"htdemucs": 1800.0}
 # chunks per forward: sesa.demix.plan_exec_batch (the CLI's planner): the model's cap, balanced so a
 # rank's last forward is not a small remainder (169 chunks at N=1 -> 3 forwards of 57; 22 per rank at
@@ -263,6 +265,8 @@ def main():
     ap.add_argument("--track-seconds", type=float, default=0.0, help="0: 240 (1800 for htdemucs)")
     ap.add_argument("--cpu-sample-chunks", type=int, default=8)
     ap.add_argument("--blend", default="avg_wave", help="ensemble blend method (ensemble.py --type)")
+    ap.add_argument("--htdemucs-mode", default="generic", choices=["generic", "demucs"],
+                    help="htdemucs chunker: generic (the live CLI path, default) or utils.demix demucs mode")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-chunks-only", action="store_true",
                     help="mdx23c: time --cpu-sample-chunks forwards instead of the configs[0] 10 s end-to-end run")
@@ -297,7 +301,9 @@ def main():
     n = int(round(track_seconds * SR))
     rng = np.random.default_rng(0)
     mix_host = torch.from_numpy((0.1 * rng.standard_normal((2, n))).astype(np.float32)).pin_memory()
-    modes = ["demucs" if nm == "htdemucs" else "generic" for nm in names]
+    # htdemucs: "generic" = the live CLI path (inference.py -> demix_pytorch_optimized, generic chunker for
+    # every model type, inference_pytorch.py:226); "demucs" = utils.demix(model_type='htdemucs')
+    modes = [args.htdemucs_mode if nm == "htdemucs" else "generic" for nm in names]
 
     def n_chunks_of(cfg, mode):
         if mode == "demucs":
@@ -383,7 +389,8 @@ def main():
         desc = []
         for nm, (_, cfg, _), c, eb, md in zip(names, members, chunks, batches, modes):
             C = int(cfg.training.samplerate * cfg.training.segment) if md == "demucs" else int(cfg.audio.chunk_size)
-            desc.append(f"{WORKLOAD[nm]} (C={C}, overlap {int(cfg.inference.num_overlap)}, {c} chunks, "
+            mdesc = f", {HTD_MODE[md]}" if nm == "htdemucs" else ""
+            desc.append(f"{WORKLOAD[nm]}{mdesc} (C={C}, overlap {int(cfg.inference.num_overlap)}, {c} chunks, "
                         f"exec batch {eb})")
         if args.model == "ensemble":
             desc = [WORKLOAD["ensemble"] + f" [{args.blend}]: " + "; ".join(desc)]

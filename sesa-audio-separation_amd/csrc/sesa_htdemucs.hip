@@ -217,6 +217,86 @@ __device__ __forceinline__ void gn_stats(const double* st, double n, float& mean
   rstd = (float)(1.0 / sqrt(var + 1e-5));
 }
 
+// DConv dilated k3 conv (the first layer of a DConv block, demucs DConv: Conv1d(C, h, 3, dilation,
+// padding = dilation)) for small hidden widths (h <= 16: levels 0 / 1 at dconv_comp 8) on the VALU in
+// exact fp32, instead of a 128-column MFMA tile that would be >= 87 % padding (N = h): one thread per
+// position (row, t) holds its H accumulators; the weights [3][C][H] (zero-padded to H) are uniform
+// across the wave (scalar loads); x rows are read as 16-B channel quads.  Memory-bound (reads C floats
+// x 3 taps, mostly L1/L2 hits, writes h floats per position).  The epilogue also accumulates the
+// row's GroupNorm(1, h) sums (fp64), replacing a separate statistics pass over U.
+constexpr int kDcVMaxH = 16;
+template <int H>
+__global__ void __launch_bounds__(kT) htd_dc_conv_valu_kernel(const float* __restrict__ X, int T, int C, int dil,
+                                                              int h, const float* __restrict__ w,
+                                                              const float* __restrict__ b1, float* __restrict__ U,
+                                                              double* __restrict__ st1) {
+  __shared__ double red[2 * (kT / 64)];
+  const int row = blockIdx.y;
+  const int t = blockIdx.x * kT + threadIdx.x;
+  float acc[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) acc[j] = b1[j];
+  const float* xr = X + (int64_t)row * T * C;
+  double s = 0.0, ss = 0.0;
+  if (t < T) {
+    // 16-channel groups: the 12 quad loads of a group (3 taps x 4 quads) are issued together, and the
+    // next group's before this group's FMAs, so the loop is not one memory latency per quad
+    const float* xp[3];
+    bool ok[3];
+#pragma unroll
+    for (int tap = 0; tap < 3; ++tap) {
+      const int tt = t + (tap - 1) * dil;
+      ok[tap] = tt >= 0 && tt < T;   // zero padding
+      xp[tap] = xr + (int64_t)(ok[tap] ? tt : t) * C;
+    }
+    f32x4 cur[3][4], nxt[3][4];
+    auto load = [&](f32x4 (&r)[3][4], int c0) {
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap)
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          const int c = min(c0 + 4 * qd, C - 4);
+          r[tap][qd] = *reinterpret_cast<const f32x4*>(xp[tap] + c);
+        }
+    };
+    load(cur, 0);
+    for (int c0 = 0; c0 < C; c0 += 16) {
+      if (c0 + 16 < C) load(nxt, c0 + 16);
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap) {
+        if (!ok[tap]) continue;
+        const float* wt = w + ((size_t)tap * C + c0) * H;
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (c0 + 4 * qd + q >= C) continue;   // (C % 4 == 0: whole quads)
+#pragma unroll
+            for (int j = 0; j < H; ++j) acc[j] = fmaf(wt[(4 * qd + q) * H + j], cur[tap][qd][q], acc[j]);
+          }
+      }
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap)
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) cur[tap][qd] = nxt[tap][qd];
+    }
+    float* up = U + ((int64_t)row * T + t) * h;
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+      if (j < h) {
+        up[j] = acc[j];
+        s += (double)acc[j];
+        ss += (double)acc[j] * (double)acc[j];
+      }
+  }
+  block_sum2(s, ss, red);
+  if (threadIdx.x == 0) {
+    atomicAdd(&st1[2 * row], s);
+    atomicAdd(&st1[2 * row + 1], ss);
+  }
+}
+int dc_valu_h(int h) { return h > kDcVMaxH ? 0 : h <= 6 ? 6 : h <= 8 ? 8 : h <= 12 ? 12 : 16; }
+
 // Per (t-block, row): G = gelu(gn1(U)) into LDS, then entry e of (sum G | sum G G^T) summed over the
 // block's positions in fp64 and added to the row's totals.
 __global__ void __launch_bounds__(kT) htd_dc_gram_kernel(DcArgs a) {
@@ -469,6 +549,7 @@ struct Param {
 
 struct DcLayer {  // float offsets into the packed fp32 blob
   int64_t b1, g1, be1, w2t, b2, g2, be2, scale;
+  int64_t w1v = -1, b1v = -1;   // VALU k3 conv (h <= kDcVMaxH): W1 as [3][C][Hv] and b1 as [Hv], zero-padded
   int64_t gc;     // double offset of the Gram constants (htd_dc_apply_kernel)
   int dil;
   Gemm conv;      // the dilated k3 conv: N = h, K = 3 C (k = tap * C + c), bias b1
@@ -853,6 +934,15 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                          },
                          true, [&](int n) { return B1[n]; }, blob, bias));
       L.b1 = putp(q + ".0.bias");
+      if (const int Hv = dc_valu_h(h)) {
+        std::vector<float> wv((size_t)3 * C * Hv, 0.f), bv((size_t)Hv, 0.f);
+        for (int tap = 0; tap < 3; ++tap)
+          for (int ci = 0; ci < C; ++ci)
+            for (int j = 0; j < h; ++j) wv[((size_t)tap * C + ci) * Hv + j] = W1[((size_t)j * C + ci) * 3 + tap];
+        for (int j = 0; j < h; ++j) bv[j] = B1[j];
+        L.w1v = put(wv);
+        L.b1v = put(bv);
+      }
       L.g1 = putp(q + ".1.weight");
       L.be1 = putp(q + ".1.bias");
       const auto& W2 = P(m, q + ".3.weight");   // [2C][h][1] -> [h][2C]
@@ -1227,9 +1317,35 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     const int nS = dc_ns(h);
     const int P1 = rows / B;   // frequency rows per item (1 for the time branch)
     for (const DcLayer& Ly : layers) {
-      // dilated k3 conv over T (padding = dilation) -> U [rows][T][h] (+ bias), bf16x3 MFMA
-      conv_gemm(Ly.conv, X, C, nullptr, U, h, P1, Tn, P1, Tn, 1, C, {0, 0, 0}, {-Ly.dil, 0, Ly.dil}, TOK_ACT_NONE, 0,
-                1, 0, 0);
+      static const bool valu_on = !(getenv("SESA_HTD_DCONV_VALU") && std::string(getenv("SESA_HTD_DCONV_VALU")) == "0");
+      const int Hv = valu_on && Ly.w1v >= 0 && C % 4 == 0 ? dc_valu_h(h) : 0;
+      if (hipMemsetAsync(rowst, 0, (size_t)rows * (2 + nS) * sizeof(double), st) != hipSuccess) {
+        rc = SESA_ERR_HIP;
+        set_error("htdemucs: memset");
+        return;
+      }
+      if (Hv) {
+        // dilated k3 conv over T on the VALU (fp32) + GroupNorm(1, h) sums -> U [rows][T][h]
+        void* t0 = profile_begin(st);
+        const dim3 g((unsigned)((Tn + kT - 1) / kT), (unsigned)rows);
+#define SESA_DCV(HV) hipLaunchKernelGGL(htd_dc_conv_valu_kernel<HV>, g, dim3(kT), 0, st, X, Tn, C, Ly.dil, h, \
+                                        Wb + Ly.w1v, Wb + Ly.b1v, U, rowst)
+        if (Hv == 6) SESA_DCV(6);
+        else if (Hv == 8) SESA_DCV(8);
+        else if (Hv == 12) SESA_DCV(12);
+        else SESA_DCV(16);
+#undef SESA_DCV
+        if (hipGetLastError() != hipSuccess) {
+          rc = SESA_ERR_HIP;
+          set_error("htdemucs: DConv conv launch failed");
+          return;
+        }
+        profile_end(t0, st, SESA_KCLASS_HCONV, 2.0 * rows * Tn * (double)h * 3.0 * C);
+      } else {
+        // dilated k3 conv over T (padding = dilation) -> U [rows][T][h] (+ bias), bf16x3 MFMA
+        conv_gemm(Ly.conv, X, C, nullptr, U, h, P1, Tn, P1, Tn, 1, C, {0, 0, 0}, {-Ly.dil, 0, Ly.dil}, TOK_ACT_NONE,
+                  0, 1, 0, 0);
+      }
       if (rc) return;
       void* tok = profile_begin(st);
       DcArgs a{};
@@ -1250,15 +1366,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       a.st1 = rowst;
       a.gram = rowst + 2 * (size_t)rows;
       a.gc = m->d_f64 + Ly.gc;
-      if (hipMemsetAsync(rowst, 0, (size_t)rows * (2 + nS) * sizeof(double), st) != hipSuccess) {
-        rc = SESA_ERR_HIP;
-        set_error("htdemucs: memset");
-        return;
-      }
       const int64_t n_item = (int64_t)Tn * h;
-      hipLaunchKernelGGL(htd_item_stats_kernel, dim3((unsigned)std::min<int64_t>((n_item + kT * 8 - 1) / (kT * 8), 512),
-                                                     (unsigned)rows),
-                         dim3(kT), 0, st, U, n_item, rowst);
+      if (!Hv)   // (the VALU conv accumulated these already)
+        hipLaunchKernelGGL(htd_item_stats_kernel,
+                           dim3((unsigned)std::min<int64_t>((n_item + kT * 8 - 1) / (kT * 8), 512), (unsigned)rows),
+                           dim3(kT), 0, st, U, n_item, rowst);
       hipLaunchKernelGGL(htd_dc_gram_kernel, dim3((unsigned)((Tn + kDcG - 1) / kDcG), (unsigned)rows), dim3(kT), 0, st,
                          a);
       const dim3 ga((unsigned)((Tn + kDcP - 1) / kDcP), (unsigned)rows);

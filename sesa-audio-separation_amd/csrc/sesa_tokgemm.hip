@@ -970,8 +970,17 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
                      !a.rownorm && (int64_t)c.P1 * c.P2 > 0 && (c.phases == 1 || !a.glu),
                  SESA_ERR_INVALID, "tok_gemm conv: bad geometry");
     SESA_REQUIRE(!a.a_hi, SESA_ERR_INVALID, "tok_gemm conv: pre-split A is for token rows");
-    if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, true, false>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true, false>), grid, dim3(256), 0, st, a);
+    // SESA_HCONV_VARIANT=1: the double-buffered 512-thread 256 x 128 tile for the implicit-GEMM convs (A/B)
+    static const int hv = getenv("SESA_HCONV_VARIANT") ? atoi(getenv("SESA_HCONV_VARIANT")) : 0;
+    if (hv == 1) {
+      const dim3 g2((unsigned)(((a.M + 255) / 256) * a.n_tiles_n));
+      if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 512, 256, 2, 2, 2, true, true, false>), g2, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 2, true, true, false>), g2, dim3(512), 0, st, a);
+    } else if (x3) {
+      hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, true, false>), grid, dim3(256), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true, false>), grid, dim3(256), 0, st, a);
+    }
   } else if (a.a_hi) {
     SESA_REQUIRE(a.a_ld % 4 == 0 && (!x3 || a.a_lo) && (!a.rownorm || a.row_scale), SESA_ERR_INVALID,
                  "tok_gemm: pre-split A needs a_ld %% 4 == 0, the lo plane for bf16x3, row_scale for rownorm");

@@ -172,3 +172,24 @@ def test_mel_forward_full_chunk_matches_reference(golden, dev):
     err = rms(y, g["y"])
     print(f"mel-band vocals full chunk rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
     assert err <= RMS_GATE
+
+
+@pytest.mark.gpu
+def test_full_size_4min_properties(dev):
+    """configs[2] at full size (4-min track, BS-Roformer vocals config, 62 chunks at overlap 2): the
+    sharded path at world 1 equals demix_device bit-for-bit, the vocals stem is finite, shaped
+    [1, 2, L] and not degenerate (size-independent properties; the oracle would need ~20 min of CPU).
+    Mirrors tests/test_gpu_parity.py::test_full_size_4min_properties."""
+    from sesa.demix import demix_device
+    from sesa.parallel import demix_sharded
+    m, c = _model("config_bs_roformer_vocals.yaml", "random")
+    L = 240 * 44100
+    rng = np.random.default_rng(0)
+    mix = torch.from_numpy((0.1 * rng.standard_normal((2, L))).astype(np.float32)).to(dev)
+    with contextlib.redirect_stdout(io.StringIO()):
+        a = demix_device(c, m, mix, dev, exec_batch=4)
+    b = demix_sharded(c, m, mix, dev, rank=0, world=1, exec_batch=4)
+    assert a.shape == b.shape == (1, 2, L)
+    assert torch.isfinite(a).all().item()
+    assert torch.equal(a, b)
+    assert float(a[0].std()) > 1e-5 and float((a[0, 0] - a[0, 1]).abs().max()) > 1e-5

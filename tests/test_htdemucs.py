@@ -179,3 +179,32 @@ def test_demix_demucs_mode_matches_oracle(dev):
         err = rms(got[k], ref[k])
         print(f"demix {k}: rms {err:.3e}")
         assert err <= RMS_GATE
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["demucs", "generic"])
+def test_full_size_30min_properties(dev, mode):
+    """configs[3] at full size (30-min mix, musdb18 config): demucs mode (utils.demix for model_type
+    'htdemucs', 655 segments) and generic mode (the live CLI's demix_pytorch_optimized, 661 chunks).
+    The sharded path at world 1 equals the single-device chunker bit-for-bit, the stems are finite and
+    shaped [4, 2, L], and they are not degenerate (size-independent properties: the oracle would need
+    hours of CPU).  Mirrors tests/test_gpu_parity.py::test_full_size_4min_properties."""
+    import contextlib
+    import io
+    from sesa.demix import demix_device, demix_device_demucs
+    from sesa.parallel import demix_sharded
+    m, c = _model("config_musdb18_htdemucs.yaml")
+    L = 1800 * 44100
+    rng = np.random.default_rng(0)
+    mix = torch.from_numpy((0.1 * rng.standard_normal((2, L))).astype(np.float32)).to(dev)
+    with contextlib.redirect_stdout(io.StringIO()):
+        a = demix_device_demucs(c, m, mix, dev, exec_batch=32) if mode == "demucs" else \
+            demix_device(c, m, mix, dev, exec_batch=32)
+    b = demix_sharded(c, m, mix, dev, rank=0, world=1, exec_batch=32, mode=mode)
+    ni = len(c.training.instruments)
+    assert a.shape == b.shape == (ni, 2, L)
+    assert torch.isfinite(a).all().item()
+    assert torch.equal(a, b)
+    for s in range(ni):
+        assert float(a[s].std()) > 1e-5
+    assert float((a[0] - a[3]).abs().max()) > 1e-4
