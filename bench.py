@@ -121,6 +121,33 @@ def pmc_traffic(kclass):
                                            d.get("algorithmic_bytes_per_launch")}
 
 
+def mdx23c_conv3x3_alg_bytes(cfg, batch):
+    """Algorithmic HBM bytes of the conv3x3 class over one MDX23C forward of `batch` chunks, and its launch
+    count: each TFC 3x3 conv reads its input once (4 B per element: fp32 for the fused-activation
+    kernel, bf16 hi + lo planes otherwise -- the same bytes), the fused 1x1 shortcut's raw input (4 B)
+    for conv2, and writes its fp32 output (4 B); weights as bf16 hi + lo (4 B per coefficient)
+    (mdx23c_tfc_tdf_v3.py:100-138; levels as TFC_TDF_net.__init__ :141-203)."""
+    m = cfg.model
+    n, nb, c0, g = int(m.num_scales), int(m.num_blocks_per_scale), int(m.num_channels), int(m.growth)
+    T0, F0 = int(cfg.audio.dim_t), int(cfg.audio.dim_f) // int(m.num_subbands)
+    total, launches = 0.0, 0
+
+    def stack(T, F, in_c, c):
+        nonlocal total, launches
+        pos = batch * T * F
+        for i in range(nb):
+            ic = in_c if i == 0 else c
+            total += pos * (ic + c) * 4.0 + 9 * ic * c * 4.0                  # conv1
+            total += pos * (c + c + ic) * 4.0 + (9 * c + ic) * c * 4.0        # conv2 (+ shortcut operand)
+            launches += 2
+    for lv in range(n):
+        stack(T0 >> lv, F0 >> lv, c0 + g * lv, c0 + g * lv)
+    stack(T0 >> n, F0 >> n, c0 + g * n, c0 + g * n)
+    for lv in reversed(range(n)):
+        stack(T0 >> lv, F0 >> lv, 2 * (c0 + g * lv), c0 + g * lv)
+    return total, launches
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -242,6 +269,14 @@ def synth_weights(model):
         b = 1.0 / np.sqrt(fan_in)
         sd[pname] = torch.from_numpy(rng.uniform(-b, b, size=shape).astype(np.float32))
     return sd
+
+
+def _forward_sizes(n_chunks, exec_batch, world):
+    """Chunks per forward on rank 0: its contiguous share of the track, in exec_batch groups
+    (sesa/parallel.py local_accumulate_device)."""
+    per = -(-n_chunks // world)
+    share = min(per, n_chunks)
+    return [list(range(i, min(share, i + exec_batch))) for i in range(0, share, exec_batch)]
 
 
 def build_model(name, precision):
@@ -378,10 +413,21 @@ def main():
     if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
         peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
     traffic, traffic_src = pmc_traffic(kclass)
+    alg_bytes = None
+    if kclass == "conv3x3":
+        m0, cfg0, _ = members[0]
+        per_fwd, l_fwd = 0.0, 0
+        for nb_ in [len(x) for x in _forward_sizes(chunks[0], batches[0], world)]:
+            b_, l_ = mdx23c_conv3x3_alg_bytes(cfg0, nb_)
+            per_fwd += b_
+            l_fwd += l_
+        alg_bytes = round(per_fwd / max(l_fwd, 1))
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": KDESC[kclass],
             "launches": launches, "avg_launch_ms": round(ms / max(launches, 1), 4),
-            "flop_per_launch": round(work / max(launches, 1)), "peak_note": note, "traffic_source": traffic_src}
+            "flop_per_launch": round(work / max(launches, 1)), "peak_note": note, "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic and alg_bytes else None}
     path_tflops = path_flop * args.steps / elapsed / 1e12
 
     value = track_seconds * args.steps / elapsed

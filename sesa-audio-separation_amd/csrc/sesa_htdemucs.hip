@@ -1293,23 +1293,10 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     rc = launch_tok_gemm(a, x3, st);
     profile_end(t0, st, kclass, gemm_flops(gm, M));
   };
+  // 1x1 rewrite + GLU (:114-118 of HEncLayer) as a one-tap implicit-GEMM conv over the M / B positions of
+  // each item, so every launch of the hconv class is a conv-mode dispatch (one kernel name for the PMC)
   auto rewrite_glu = [&](const Gemm& gm, const float* xin, float* o, int64_t M, int C) {
-    if (rc) return;
-    TokGemmArgs a{};
-    a.x = xin;
-    a.x_ld = C;
-    a.out = o;
-    a.o_ld = C;
-    a.w = m->d_w;
-    a.bias = m->d_bias;
-    a.groups = gm.d_groups;
-    a.n_groups = 1;
-    a.n_tiles_n = gm.n_tiles_n;
-    a.M = (int)M;
-    a.glu = 1;
-    void* t0 = profile_begin(st);
-    rc = launch_tok_gemm(a, x3, st);
-    profile_end(t0, st, SESA_KCLASS_HCONV, gemm_flops(gm, M));
+    conv_gemm(gm, xin, C, nullptr, o, C, (int)(M / B), 1, (int)(M / B), 1, 1, C, {0}, {}, TOK_ACT_NONE, 1, 1, 0, 0);
   };
   auto dconv = [&](const std::vector<DcLayer>& layers, float* X, int rows, int Tn, int C, int h) {
     if (rc) return;

@@ -1,0 +1,18 @@
+#!/bin/bash
+# HBM traffic per launch of the dominant kernel classes, on THIS tree, for bench.py's roofline.traffic:
+#   bash tools/pmc_refresh.sh MODEL "CLASS=SUBSTR[|SUBSTR..]" ...   (run on the GPU box; GIT_SHA from the caller)
+# One bench step of the real workload (same exec batch as the timed run) under two separate rocprofv3 --pmc
+# passes (FETCH_SIZE, then WRITE_SIZE: MI355X_MICROARCH.md HBM section; FETCH_SIZE doubled for gfx950 in
+# tools/pmc_traffic.py), each under its own time limit; the summaries are stamped with the kernel sources'
+# sha (bench.py KSRC) and written to gpurun_out/pmc_<class>.json.
+set -e
+M=$1; shift
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+B="python3 bench.py --model $M --steps 1 --warmup 0 --no-cpu-baseline"
+O=gpurun_out
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_${M}_f -o run -- $B > $O/pmc_${M}_f.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_${M}_w -o run -- $B > $O/pmc_${M}_w.log 2>&1
+for spec in "$@"; do
+  K=${spec%%=*}; S=${spec#*=}
+  python3 tools/pmc_traffic.py $O/pmc_${M}_f $O/pmc_${M}_w "$S" $O/pmc_${K}.json $K
+done
