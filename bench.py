@@ -303,6 +303,7 @@ def main():
     ap.add_argument("--htdemucs-mode", default="generic", choices=["generic", "demucs"],
                     help="htdemucs chunker: generic (the live CLI path, default) or utils.demix demucs mode")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the parity forward (PMC passes: one workload only)")
     ap.add_argument("--cpu-chunks-only", action="store_true",
                     help="mdx23c: time --cpu-sample-chunks forwards instead of the configs[0] 10 s end-to-end run")
     args = ap.parse_args()
@@ -479,7 +480,7 @@ def main():
             line["attention"] = {"kernel": KDESC["attn"],
                                  "achieved_tflops": round(awork / (ams * 1e-3) / 1e12, 2) if ams > 0 else 0.0,
                                  "launches": alaunch, "avg_launch_ms": round(ams / max(alaunch, 1), 4)}
-        if args.model == "mdx23c":
+        if args.model == "mdx23c" and not args.no_parity:
             # north_star parity, measured by the bench itself: the same model (same weights) on the
             # reference's own full-chunk output (tests/golden/mdx23c_full_chunk.npz, the reference
             # TFC_TDF_net run in fp32 on CPU by tests/golden/make_golden.py), per-sample RMS

@@ -8,7 +8,7 @@
 set -e
 M=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B="python3 bench.py --model $M --steps 1 --warmup 0 --no-cpu-baseline"
+B="python3 bench.py --model $M --steps 1 --warmup 0 --no-cpu-baseline --no-parity"
 O=gpurun_out
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_${M}_f -o run -- $B > $O/pmc_${M}_f.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_${M}_w -o run -- $B > $O/pmc_${M}_w.log 2>&1
