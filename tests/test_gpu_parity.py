@@ -135,13 +135,23 @@ def test_forward_full_chunk_matches_reference(golden, dev):
     assert rms(yb[0], y[0]) < 1e-7 and rms(yb[2], y[0]) < 1e-7
 
 
-def test_forward_full_chunk_bf16_reports_deviation(golden, dev):
-    """Throughput precision: measured, not gated (expected ~6e-4, outside the 1e-4 gate)."""
+def test_forward_full_chunk_bf16_reports_deviation(golden, dev, record_property):
+    """Throughput precision (--enable_amp / bench.py --precision bf16): measured and recorded, gated only
+    loosely at 5e-3 (single-pass bf16 is expected near 6e-4, outside the 1e-4 parity gate -- the reference's
+    own fp16 autocast is 1.35e-4).  The value is written to the junit report
+    (record_property) and to gpurun_out/parity_bf16.json when that directory exists."""
     g = golden("mdx23c_full_chunk.npz")
     m, _ = _model("config_vocals_mdx23c.yaml", "unit", precision="bf16")
     y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
     err = rms(y, g["y"])
     print(f"full chunk bf16: rms={err:.3e}")
+    record_property("mdx23c_full_chunk_bf16_rms", err)
+    out_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(out_dir):
+        import json
+        with open(os.path.join(out_dir, "parity_bf16.json"), "w") as f:
+            json.dump({"fixture": "mdx23c_full_chunk.npz", "precision": "bf16", "rms_vs_reference": err,
+                       "gate_bf16x3": RMS_GATE}, f)
     assert np.isfinite(y).all() and err < 5e-3
 
 
