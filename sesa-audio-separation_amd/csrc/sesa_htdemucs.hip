@@ -436,7 +436,10 @@ __global__ void __launch_bounds__(kT) htd_dc_apply_kernel(DcArgs a) {
 __global__ void __launch_bounds__(kT) htd_layernorm_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                            int64_t rows, int D, const float* __restrict__ g,
                                                            const float* __restrict__ be,
-                                                           const float* __restrict__ tab, int n_tok) {
+                                                           const float* __restrict__ tab, int n_tok,
+                                                           uint16_t* __restrict__ ohi, uint16_t* __restrict__ olo) {
+  // ohi (nullable): write the normalised rows as bf16 hi / lo planes [rows][D] instead of fp32 `out` --
+  // the pre-split A operand of the following token GEMM (tok_gemm_glds_kernel); olo null for bf16
   const int64_t r = (int64_t)blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int lane = threadIdx.x & 63;
@@ -457,7 +460,14 @@ __global__ void __launch_bounds__(kT) htd_layernorm_kernel(const float* __restri
   for (int i = lane; i < D; i += 64) {
     float o = (x[i] - mean) * rstd * g[i] + be[i];
     if (tr) o += tr[i];
-    y[i] = o;
+    if (ohi) {
+      __bf16 hi, lo;
+      split_bf16(o, hi, lo);
+      ohi[r * D + i] = __builtin_bit_cast(uint16_t, hi);
+      if (olo) olo[r * D + i] = __builtin_bit_cast(uint16_t, lo);
+    } else {
+      y[i] = o;
+    }
   }
 }
 
@@ -1293,10 +1303,30 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     rc = launch_tok_gemm(a, x3, st);
     profile_end(t0, st, kclass, gemm_flops(gm, M));
   };
-  // 1x1 rewrite + GLU (:114-118 of HEncLayer) as a one-tap implicit-GEMM conv over the M / B positions of
-  // each item, so every launch of the hconv class is a conv-mode dispatch (one kernel name for the PMC)
+  // 1x1 rewrite + GLU (:114-118 of HEncLayer): the plain token GEMM (2 % faster end to end than the
+  // one-tap conv-mode GEMM, profiles/r03_htd_rw_*.json; SESA_HTD_REWRITE_CONV=1 selects the latter)
+  static const bool rw_conv = getenv("SESA_HTD_REWRITE_CONV") && std::string(getenv("SESA_HTD_REWRITE_CONV")) == "1";
   auto rewrite_glu = [&](const Gemm& gm, const float* xin, float* o, int64_t M, int C) {
-    conv_gemm(gm, xin, C, nullptr, o, C, (int)(M / B), 1, (int)(M / B), 1, 1, C, {0}, {}, TOK_ACT_NONE, 1, 1, 0, 0);
+    if (rw_conv) {
+      conv_gemm(gm, xin, C, nullptr, o, C, (int)(M / B), 1, (int)(M / B), 1, 1, C, {0}, {}, TOK_ACT_NONE, 1, 1, 0, 0);
+      return;
+    }
+    if (rc) return;   // (A/B: the plain token GEMM)
+    TokGemmArgs a{};
+    a.x = xin;
+    a.x_ld = C;
+    a.out = o;
+    a.o_ld = C;
+    a.w = m->d_w;
+    a.bias = m->d_bias;
+    a.groups = gm.d_groups;
+    a.n_groups = 1;
+    a.n_tiles_n = gm.n_tiles_n;
+    a.M = (int)M;
+    a.glu = 1;
+    void* t0 = profile_begin(st);
+    rc = launch_tok_gemm(a, x3, st);
+    profile_end(t0, st, SESA_KCLASS_HCONV, gemm_flops(gm, M));
   };
   auto dconv = [&](const std::vector<DcLayer>& layers, float* X, int rows, int Tn, int C, int h) {
     if (rc) return;
@@ -1436,7 +1466,49 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     float* FF = F32(pl.ff);
     auto ln = [&](const float* in, float* o, int64_t rows, int64_t g, int64_t b, const float* tab, int ntok) {
       hipLaunchKernelGGL(htd_layernorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(kT), 0, st, in, o, rows, D,
-                         Wb + g, Wb + b, tab, ntok);
+                         Wb + g, Wb + b, tab, ntok, (uint16_t*)nullptr, (uint16_t*)nullptr);
+    };
+    // Transformer GEMM operands as bf16 hi / lo planes written once by their producer (LayerNorm,
+    // attention, FF1 epilogue) into the same buffers (4 B per element either way), so every Linear of the
+    // cross transformer runs on the LDS-DMA kernel (tok_gemm_glds_kernel) instead of splitting fp32 rows
+    // per N tile.  SESA_HTD_PRESPLIT=0: the fp32 path (A/B).
+    static const bool presplit = !(getenv("SESA_HTD_PRESPLIT") && std::string(getenv("SESA_HTD_PRESPLIT")) == "0");
+    const bool ps = presplit && x3 && D % 8 == 0 && hid % 8 == 0;
+    auto hi_of = [&](float* buf) { return reinterpret_cast<uint16_t*>(buf); };
+    auto lo_of = [&](float* buf, int64_t n) { return reinterpret_cast<uint16_t*>(buf) + n; };
+    // LayerNorm -> planes of `o` (rows x D)
+    auto lnp = [&](const float* in, float* o, int64_t rows, int64_t g, int64_t b) {
+      if (!ps) return ln(in, o, rows, g, b, nullptr, 1);
+      hipLaunchKernelGGL(htd_layernorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(kT), 0, st, in, o, rows, D,
+                         Wb + g, Wb + b, (const float*)nullptr, 1, hi_of(o), lo_of(o, rows * D));
+    };
+    // Linear with a pre-split A (planes of `xin`, rows x K = x_ld); optional split output (planes of o)
+    auto plin = [&](const Gemm& gm, float* xin, int64_t x_ld, float* o, int64_t o_ld, int64_t M, int act,
+                    const float* residual, bool split_out) {
+      if (rc) return;
+      if (!ps) return lin(gm, xin, x_ld, o, o_ld, M, act, residual, SESA_KCLASS_TOKGEMM);
+      TokGemmArgs a{};
+      a.x = nullptr;
+      a.a_hi = hi_of(xin);
+      a.a_lo = lo_of(xin, M * x_ld);
+      a.a_ld = x_ld;
+      a.out = split_out ? nullptr : o;
+      a.out_hi = split_out ? hi_of(o) : nullptr;
+      a.out_lo = split_out ? lo_of(o, M * o_ld) : nullptr;
+      a.o_ld = o_ld;
+      a.residual = residual;
+      a.w = m->d_w;
+      a.bias = m->d_bias;
+      a.groups = gm.d_groups;
+      a.n_groups = 1;
+      a.n_tiles_n = gm.n_tiles_n;
+      a.k8 = gm.k8;
+      a.n4 = gm.n4;
+      a.M = (int)M;
+      a.act = act;
+      void* t0 = profile_begin(st);
+      rc = launch_tok_gemm(a, x3, st);
+      profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(gm, M));
     };
     {
       void* tok = profile_begin(st);
@@ -1469,6 +1541,10 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       a.Lk = kv ? Lk : 0;
       a.kv_smul = Lk;
       a.dh = dh;
+      if (ps) {                // planes for the following out-projection's pre-split A
+        a.out_hi = hi_of(o);
+        a.out_lo = lo_of(o, (int64_t)B * Lq * D);
+      }
       void* t0 = profile_begin(st);
       rc = launch_attention(a, x3, st);
       profile_end(t0, st, SESA_KCLASS_ATTN, 4.0 * (double)B * heads * (double)Lq * Lk * dh);
@@ -1490,39 +1566,43 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     const int act = c.t_gelu ? TOK_ACT_GELU : TOK_ACT_RELU;
     auto ff_block = [&](const TLayer& Ly, float* Xs, float* Hs, int64_t M, int64_t ng, int64_t nb) {
       if (rc) return;
-      ln(Xs, Hs, M, ng, nb, nullptr, 1);
-      lin(Ly.ff1, Hs, D, FF, hid, M, act, nullptr, SESA_KCLASS_TOKGEMM);
-      lin(Ly.ff2, FF, hid, Xs, D, M, TOK_ACT_NONE, Xs, SESA_KCLASS_TOKGEMM);   // x += gamma_2 (linear2(..))
+      lnp(Xs, Hs, M, ng, nb);
+      plin(Ly.ff1, Hs, D, FF, hid, M, act, nullptr, act == TOK_ACT_GELU);   // FF1 epilogue writes planes
+      if (ps && act != TOK_ACT_GELU) {   // (ReLU has no split epilogue: fp32 path for FF2's A)
+        lin(Ly.ff2, FF, hid, Xs, D, M, TOK_ACT_NONE, Xs, SESA_KCLASS_TOKGEMM);
+        return;
+      }
+      plin(Ly.ff2, FF, hid, Xs, D, M, TOK_ACT_NONE, Xs, false);   // x += gamma_2 (linear2(..))
     };
     for (int l = 0; l < c.t_layers; ++l) {
       const TLayer& Lx = m->tl[l];
       const TLayer& Lt = m->tlt[l];
       if (!Lx.cross) {  // MyTransformerEncoderLayer (norm_first): x += g1 SA(n1(x)); x += g2 FF(n2(x)); norm_out
-        ln(X, Hx, Mx, Lx.n1g, Lx.n1b, nullptr, 1);
-        ln(XT, Ht, Mt, Lt.n1g, Lt.n1b, nullptr, 1);
-        lin(Lx.qkv, Hx, D, Qx, 3 * D, Mx, TOK_ACT_NONE, nullptr, SESA_KCLASS_TOKGEMM);
-        lin(Lt.qkv, Ht, D, Qt, 3 * D, Mt, TOK_ACT_NONE, nullptr, SESA_KCLASS_TOKGEMM);
+        lnp(X, Hx, Mx, Lx.n1g, Lx.n1b);
+        lnp(XT, Ht, Mt, Lt.n1g, Lt.n1b);
+        plin(Lx.qkv, Hx, D, Qx, 3 * D, Mx, TOK_ACT_NONE, nullptr, false);
+        plin(Lt.qkv, Ht, D, Qt, 3 * D, Mt, TOK_ACT_NONE, nullptr, false);
         attn(Qx, 3 * D, nullptr, 0, D, 2 * D, Ax, m->Nx, m->Nx);
         attn(Qt, 3 * D, nullptr, 0, D, 2 * D, At, m->Nt, m->Nt);
-        lin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, SESA_KCLASS_TOKGEMM);
-        lin(Lt.out, At, D, XT, D, Mt, TOK_ACT_NONE, XT, SESA_KCLASS_TOKGEMM);
+        plin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, false);
+        plin(Lt.out, At, D, XT, D, Mt, TOK_ACT_NONE, XT, false);
         ff_block(Lx, X, Hx, Mx, Lx.n2g, Lx.n2b);
         ff_block(Lt, XT, Ht, Mt, Lt.n2g, Lt.n2b);
       } else {          // CrossTransformerEncoderLayer: x += g1 CA(n1(x), n2(xt_old)); xt += g1' CA(n1'(xt), n2'(x_old))
-        ln(X, Hx, Mx, Lx.n1g, Lx.n1b, nullptr, 1);      // query of x
-        ln(XT, Ht2, Mt, Lx.n2g, Lx.n2b, nullptr, 1);    // keys / values of x's layer (from xt)
-        ln(XT, Ht, Mt, Lt.n1g, Lt.n1b, nullptr, 1);     // query of xt
-        ln(X, Hx2, Mx, Lt.n2g, Lt.n2b, nullptr, 1);     // keys / values of xt's layer (from old x)
-        float* KVt = Qx + (size_t)Mx * D;               // [Mx][2D]: xt-layer keys / values (from x)
-        float* KVx = Qt + (size_t)Mt * D;               // [Mt][2D]: x-layer keys / values (from xt)
-        lin(Lx.q, Hx, D, Qx, D, Mx, TOK_ACT_NONE, nullptr, SESA_KCLASS_TOKGEMM);
-        lin(Lx.kv, Ht2, D, KVx, 2 * D, Mt, TOK_ACT_NONE, nullptr, SESA_KCLASS_TOKGEMM);
-        lin(Lt.q, Ht, D, Qt, D, Mt, TOK_ACT_NONE, nullptr, SESA_KCLASS_TOKGEMM);
-        lin(Lt.kv, Hx2, D, KVt, 2 * D, Mx, TOK_ACT_NONE, nullptr, SESA_KCLASS_TOKGEMM);
+        lnp(X, Hx, Mx, Lx.n1g, Lx.n1b);      // query of x
+        lnp(XT, Ht2, Mt, Lx.n2g, Lx.n2b);    // keys / values of x's layer (from xt)
+        lnp(XT, Ht, Mt, Lt.n1g, Lt.n1b);     // query of xt
+        lnp(X, Hx2, Mx, Lt.n2g, Lt.n2b);     // keys / values of xt's layer (from old x)
+        float* KVt = Qx + (size_t)Mx * D;    // [Mx][2D]: xt-layer keys / values (from x)
+        float* KVx = Qt + (size_t)Mt * D;    // [Mt][2D]: x-layer keys / values (from xt)
+        plin(Lx.q, Hx, D, Qx, D, Mx, TOK_ACT_NONE, nullptr, false);
+        plin(Lx.kv, Ht2, D, KVx, 2 * D, Mt, TOK_ACT_NONE, nullptr, false);
+        plin(Lt.q, Ht, D, Qt, D, Mt, TOK_ACT_NONE, nullptr, false);
+        plin(Lt.kv, Hx2, D, KVt, 2 * D, Mx, TOK_ACT_NONE, nullptr, false);
         attn(Qx, D, KVx, 2 * D, 0, D, Ax, m->Nx, m->Nt);
         attn(Qt, D, KVt, 2 * D, 0, D, At, m->Nt, m->Nx);
-        lin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, SESA_KCLASS_TOKGEMM);
-        lin(Lt.out, At, D, XT, D, Mt, TOK_ACT_NONE, XT, SESA_KCLASS_TOKGEMM);
+        plin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, false);
+        plin(Lt.out, At, D, XT, D, Mt, TOK_ACT_NONE, XT, false);
         ff_block(Lx, X, Hx, Mx, Lx.n3g, Lx.n3b);
         ff_block(Lt, XT, Ht, Mt, Lt.n3g, Lt.n3b);
       }
