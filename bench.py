@@ -304,6 +304,7 @@ def main():
                     help="htdemucs chunker: generic (the live CLI path, default) or utils.demix demucs mode")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the parity forward (PMC passes: one workload only)")
+    ap.add_argument("--streams", type=int, default=1, help="forwards in flight on separate HIP streams")
     ap.add_argument("--cpu-chunks-only", action="store_true",
                     help="mdx23c: time --cpu-sample-chunks forwards instead of the configs[0] 10 s end-to-end run")
     args = ap.parse_args()
@@ -356,7 +357,7 @@ def main():
     def chunk_len(cfg, mode):
         return int(cfg.training.samplerate * cfg.training.segment) if mode == "demucs" else int(cfg.audio.chunk_size)
 
-    batches = [args.exec_batch or plan_exec_batch(m, c, chunk_len(cfg, md), dev, world=world)
+    batches = [args.exec_batch or plan_exec_batch(m, c, chunk_len(cfg, md), dev, world=world, streams=args.streams)
                for (m, cfg, _), c, md in zip(members, chunks, modes)]
     from sesa.parallel import shard_plan
     shard_ranges = [shard_plan(cfg, n, world, md)["ranges"] for (_, cfg, _), md in zip(members, modes)]
@@ -371,7 +372,8 @@ def main():
                                     world=world, exec_batch=batches)[0]
         else:
             m, cfg, _ = members[0]
-            est = demix_sharded(cfg, m, mix_d, dev, rank=rank, world=world, exec_batch=batches[0], mode=modes[0])
+            est = demix_sharded(cfg, m, mix_d, dev, rank=rank, world=world, exec_batch=batches[0], mode=modes[0],
+                                streams=args.streams)
         if rank == 0:                                                         # stems D2H (one copy of the result)
             if stems_host is None or stems_host.shape != est.shape or stems_host.dtype != est.dtype:
                 stems_host = torch.empty(est.shape, dtype=est.dtype, pin_memory=True)

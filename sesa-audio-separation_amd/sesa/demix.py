@@ -72,7 +72,7 @@ def unwrap_model(model):
     return model
 
 
-def plan_exec_batch(model, n_chunks, chunk, device=None, world=1, cap=None):
+def plan_exec_batch(model, n_chunks, chunk, device=None, world=1, cap=None, streams=1):
     """Execution batch for ``n_chunks`` chunks of length ``chunk`` spread over ``world`` ranks: the
     model's cap (EXEC_CAP), halved while its workspace would exceed half the free HBM, then balanced
     so a rank's last forward is not a small remainder (169 chunks at cap 64 -> 3 forwards of 57).
@@ -83,7 +83,7 @@ def plan_exec_batch(model, n_chunks, chunk, device=None, world=1, cap=None):
     if hasattr(model, "workspace_bytes") and torch.cuda.is_available():
         try:
             free, _ = torch.cuda.mem_get_info(device)
-            while cap > 1 and model.workspace_bytes(cap, chunk) > 0.5 * free:
+            while cap > 1 and model.workspace_bytes(cap, chunk) * max(1, streams) > 0.5 * free:
                 cap //= 2
         except Exception:  # noqa: BLE001 -- planning only; the forward itself reports real errors
             pass

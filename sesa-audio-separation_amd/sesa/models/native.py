@@ -116,11 +116,13 @@ class NativeModule(torch.nn.Module):
         return self
 
     def workspace(self, device, h, batch):
+        """Per (device, stream) workspace: forwards enqueued on different streams may run concurrently."""
         need = self._fn("workspace_size")(h, batch)
-        ws = self._ws.get(device.index)
+        key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+        ws = self._ws.get(key)
         if ws is None or ws.numel() < need:
-            self._ws.pop(device.index, None)
-            self._ws[device.index] = ws = torch.empty(need, dtype=torch.uint8, device=device)
+            self._ws.pop(key, None)
+            self._ws[key] = ws = torch.empty(need, dtype=torch.uint8, device=device)
         return ws
 
     def workspace_bytes(self, batch, chunk):

@@ -74,8 +74,13 @@ def _runs(group):
         j = k
 
 
-def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch):
-    """gather -> forward -> OLA of this rank's chunks into a [rows, span_max] result buffer (HIP)."""
+def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, streams=1):
+    """gather -> forward -> OLA of this rank's chunks into a [rows, span_max] result buffer (HIP).
+
+    ``streams`` > 1: consecutive forwards alternate between the current stream and side streams (each
+    with its own input buffer and model workspace) so that one forward's memory-bound phases can overlap
+    another's MFMA-bound ones; the OLA of every forward stays on the current stream, in chunk order,
+    after an event on its forward's stream (the result is bit-identical to streams = 1)."""
     from . import ops
     C = plan["chunk"]
     n_ch = mix_d.shape[0]
@@ -86,22 +91,42 @@ def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch):
     s0 = plan["spans"][rank][0]
     flat = plan["flat"]
     win = _Windows(plan, device)
-    xbuf = None
-    pos = lo
+    main = torch.cuda.current_stream(device)
+    pool = [main] + [torch.cuda.Stream(device) for _ in range(max(1, int(streams)) - 1)]
+    xbufs = [None] * len(pool)
+    freed = [None] * len(pool)    # event on main after the OLA that consumed the stream's last forward
+    for st in pool[1:]:
+        st.wait_stream(main)      # the mix upload and buffer zeroing happen-before every side stream
+    pos, gi = lo, 0
     while pos < hi:
         grp = flat[pos:min(hi, pos + exec_batch)]
-        if xbuf is None or xbuf.shape[0] != len(grp):
-            xbuf = torch.empty(len(grp), n_ch, C, device=device, dtype=torch.float32)
-        starts = [g[0] for g in grp]
-        if plan["mode"] == "demucs":
-            ops.chunk_gather_constant(mix_d, starts, C, out=xbuf)
-        else:
-            ops.chunk_gather(mix_d, plan["border"], starts, C, out=xbuf)
-        y = model(xbuf).reshape(len(grp), rows, C)
+        si = gi % len(pool)
+        st = pool[si]
+        if st is not main and freed[si] is not None:
+            st.wait_event(freed[si])          # its input buffer / workspace are free again
+        with torch.cuda.stream(st):
+            if xbufs[si] is None or xbufs[si].shape[0] != len(grp):
+                xbufs[si] = torch.empty(len(grp), n_ch, C, device=device, dtype=torch.float32)
+            xbuf = xbufs[si]
+            starts = [g[0] for g in grp]
+            if plan["mode"] == "demucs":
+                ops.chunk_gather_constant(mix_d, starts, C, out=xbuf)
+            else:
+                ops.chunk_gather(mix_d, plan["border"], starts, C, out=xbuf)
+            y = model(xbuf).reshape(len(grp), rows, C)
+        if st is not main:
+            main.wait_stream(st)
+            y.record_stream(main)
         for j, k in _runs(grp):
             ops.ola_accumulate(y[j:k], [g[0] - s0 for g in grp[j:k]], [g[1] for g in grp[j:k]],
                                win.pick(*grp[j][2:]), local, scratch)
+        if st is not main:
+            freed[si] = torch.cuda.Event()
+            freed[si].record(main)
         pos += len(grp)
+        gi += 1
+    for st in pool[1:]:
+        main.wait_stream(st)
     return local
 
 
@@ -135,7 +160,7 @@ def exchange_and_assemble(local, plan, rank, world, group=None):
 
 
 def demix_sharded(config, model, mix_d, device=None, rank=None, world=None, exec_batch=8, group=None,
-                  local_fn=None, finalize_fn=None, counter_fn=None, mode="generic"):
+                  local_fn=None, finalize_fn=None, counter_fn=None, mode="generic", streams=1):
     """Separate the device-resident mix [2, L] with chunks sharded across the process group.
     ``mode``: "generic" (inference_pytorch.demix_pytorch_optimized / utils.demix generic) or
     "demucs" (utils.demix for model_type 'htdemucs').  Returns est [n_instr, 2, L] on every rank.
@@ -151,7 +176,7 @@ def demix_sharded(config, model, mix_d, device=None, rank=None, world=None, exec
         return torch.zeros(ni, n_ch, 0, device=mix_d.device, dtype=torch.float32)
     plan = shard_plan(config, L, world, mode)
     if local_fn is None:
-        local = local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch)
+        local = local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, streams)
     else:
         local = local_fn(config, model, mix_d, plan, rank, rows)
     full = exchange_and_assemble(local, plan, rank, world, group)
