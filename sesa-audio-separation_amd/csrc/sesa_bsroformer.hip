@@ -740,6 +740,13 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
     a.a_ld = ld;
     a.row_scale = RSC;
   };
+  // q / k / v / gate logits as bf16 planes written by the QKV epilogue (the attention then stages K / V
+  // by plain copies); SESA_BSR_QKV_PLANES=0 keeps the fp32 QKV buffer (A/B)
+  static const bool qkv_planes =
+      !(getenv("SESA_BSR_QKV_PLANES") && std::string(getenv("SESA_BSR_QKV_PLANES")) == "0");
+  const bool qp = qkv_planes && m->qkv_ld % 8 == 0 && c.dim_head % 8 == 0;
+  uint16_t* QKVhi = reinterpret_cast<uint16_t*>(QKV);
+  uint16_t* QKVlo = x3 ? QKVhi + (int64_t)M * m->qkv_ld : nullptr;
   for (size_t li = 0; li < m->layers.size(); ++li) {
     const Layer& L = m->layers[li];
     // attention: QKV + gates (RMSNorm, rotary on q/k)
@@ -753,6 +760,10 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
       a.pos_F = nb;
       a.pos_T = T;
       a.pos_time = L.time;
+      if (qp) {
+        a.out_hi = QKVhi;
+        a.out_lo = QKVlo;
+      }
       gemm(a, L.qkv, M);
     }
     if (rc) return rc;
@@ -767,6 +778,10 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
       a.out_hi = AOhi;
       a.out_lo = AOlo;
       a.o_ld = m->inner;
+      if (qp) {
+        a.qkv_hi = QKVhi;
+        a.qkv_lo = QKVlo;
+      }
       a.heads = c.heads;
       if (L.time) {  // sequences (b, band) over t
         a.L = T;

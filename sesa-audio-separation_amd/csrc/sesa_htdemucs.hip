@@ -1544,6 +1544,13 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       if (ps) {                // planes for the following out-projection's pre-split A
         a.out_hi = hi_of(o);
         a.out_lo = lo_of(o, (int64_t)B * Lq * D);
+        // q / k / v from the planes the projection GEMMs wrote (plin split_out)
+        a.qkv_hi = hi_of(const_cast<float*>(q));
+        a.qkv_lo = lo_of(const_cast<float*>(q), (int64_t)B * Lq * q_ld);
+        if (kv) {
+          a.kv_hi = hi_of(const_cast<float*>(kv));
+          a.kv_lo = lo_of(const_cast<float*>(kv), (int64_t)B * Lk * kv_ld);
+        }
       }
       void* t0 = profile_begin(st);
       rc = launch_attention(a, x3, st);
@@ -1580,8 +1587,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       if (!Lx.cross) {  // MyTransformerEncoderLayer (norm_first): x += g1 SA(n1(x)); x += g2 FF(n2(x)); norm_out
         lnp(X, Hx, Mx, Lx.n1g, Lx.n1b);
         lnp(XT, Ht, Mt, Lt.n1g, Lt.n1b);
-        plin(Lx.qkv, Hx, D, Qx, 3 * D, Mx, TOK_ACT_NONE, nullptr, false);
-        plin(Lt.qkv, Ht, D, Qt, 3 * D, Mt, TOK_ACT_NONE, nullptr, false);
+        plin(Lx.qkv, Hx, D, Qx, 3 * D, Mx, TOK_ACT_NONE, nullptr, true);
+        plin(Lt.qkv, Ht, D, Qt, 3 * D, Mt, TOK_ACT_NONE, nullptr, true);
         attn(Qx, 3 * D, nullptr, 0, D, 2 * D, Ax, m->Nx, m->Nx);
         attn(Qt, 3 * D, nullptr, 0, D, 2 * D, At, m->Nt, m->Nt);
         plin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, false);
@@ -1595,10 +1602,10 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         lnp(X, Hx2, Mx, Lt.n2g, Lt.n2b);     // keys / values of xt's layer (from old x)
         float* KVt = Qx + (size_t)Mx * D;    // [Mx][2D]: xt-layer keys / values (from x)
         float* KVx = Qt + (size_t)Mt * D;    // [Mt][2D]: x-layer keys / values (from xt)
-        plin(Lx.q, Hx, D, Qx, D, Mx, TOK_ACT_NONE, nullptr, false);
-        plin(Lx.kv, Ht2, D, KVx, 2 * D, Mt, TOK_ACT_NONE, nullptr, false);
-        plin(Lt.q, Ht, D, Qt, D, Mt, TOK_ACT_NONE, nullptr, false);
-        plin(Lt.kv, Hx2, D, KVt, 2 * D, Mx, TOK_ACT_NONE, nullptr, false);
+        plin(Lx.q, Hx, D, Qx, D, Mx, TOK_ACT_NONE, nullptr, true);
+        plin(Lx.kv, Ht2, D, KVx, 2 * D, Mt, TOK_ACT_NONE, nullptr, true);
+        plin(Lt.q, Ht, D, Qt, D, Mt, TOK_ACT_NONE, nullptr, true);
+        plin(Lt.kv, Hx2, D, KVt, 2 * D, Mx, TOK_ACT_NONE, nullptr, true);
         attn(Qx, D, KVx, 2 * D, 0, D, Ax, m->Nx, m->Nt);
         attn(Qt, D, KVt, 2 * D, 0, D, At, m->Nt, m->Nx);
         plin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, false);

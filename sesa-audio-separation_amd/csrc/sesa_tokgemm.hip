@@ -712,7 +712,7 @@ constexpr int kKB = 64;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
-template <bool X3>
+template <bool X3, bool PRE = false>
 __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[4 * kKB * kHD * 2];
   char* Khi = smem;
@@ -739,7 +739,31 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
 
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16 ks + 8 hl + j] / sqrt(dh), split
   bf16x8 qh[4], ql[4];
-  {
+  if constexpr (PRE) {
+    // planes: hi + lo of q, then (q * qscale) split again -- for dh = 64 (qscale = 2^-3) exactly the
+    // fp32 path's operands, since the split commutes with a power-of-two scale
+    const int64_t qo = token(q_ok ? q_pos : 0) * a.ld + head * dh;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int d0 = 16 * ks + 8 * hl;
+      uint4 hv = make_uint4(0u, 0u, 0u, 0u), lv = make_uint4(0u, 0u, 0u, 0u);
+      if (q_ok && d0 < dh) {   // dh % 8 == 0 on this path (host check)
+        hv = *reinterpret_cast<const uint4*>(a.qkv_hi + qo + d0);
+        if (a.qkv_lo) lv = *reinterpret_cast<const uint4*>(a.qkv_lo + qo + d0);
+      }
+      const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w}, lw[4] = {lv.x, lv.y, lv.z, lv.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float vh = __uint_as_float((j & 1) ? (hw[j >> 1] & 0xffff0000u) : (hw[j >> 1] << 16));
+        const float vl = __uint_as_float((j & 1) ? (lw[j >> 1] & 0xffff0000u) : (lw[j >> 1] << 16));
+        const float v = (vh + vl) * qscale;
+        __bf16 hi, lo;
+        split_bf16(v, hi, lo);
+        qh[ks][j] = hi;
+        ql[ks][j] = lo;
+      }
+    }
+  } else {
     const float* qp = a.qkv + token(q_ok ? q_pos : 0) * a.ld + head * dh;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -764,8 +788,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
     for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  // staging: 64 keys x 64 d of K and of V (fp32) = 2 x 1024 f32x4; 8 per thread
-  f32x4 kreg[4], vreg[4];
+  // staging: 64 keys x 64 d of K and of V (fp32) = 2 x 1024 f32x4; 8 per thread.  PRE: the same
+  // (key, 4-d quad) items as bf16 hi / lo pairs (8 B each), copied to LDS without a split
+  f32x4 kreg[PRE ? 1 : 4], vreg[PRE ? 1 : 4];
+  uint2 kh2[PRE ? 4 : 1], kl2[PRE ? 4 : 1], vh2[PRE ? 4 : 1], vl2[PRE ? 4 : 1];
+  const uint16_t* kvh = a.kv ? a.kv_hi : a.qkv_hi;
+  const uint16_t* kvl = a.kv ? a.kv_lo : a.qkv_lo;
   auto load_block = [&](int kb) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -773,9 +801,20 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
       const int key = e >> 4, dq = (e & 15) * 4;
       const int p = kb * kKB + key;
       const bool ok = p < Lk && dq < dh;
-      const float* row = kvb + ktoken(ok ? p : 0) * kv_ld + head * dh + (ok ? dq : 0);
-      kreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.k_off) : f32x4{0.f, 0.f, 0.f, 0.f};
-      vreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.v_off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int64_t ro = ktoken(ok ? p : 0) * kv_ld + head * dh + (ok ? dq : 0);
+      if constexpr (PRE) {
+        const uint2 z = make_uint2(0u, 0u);
+        kh2[i] = ok ? *reinterpret_cast<const uint2*>(kvh + ro + a.k_off) : z;
+        vh2[i] = ok ? *reinterpret_cast<const uint2*>(kvh + ro + a.v_off) : z;
+        if (X3) {
+          kl2[i] = ok && kvl ? *reinterpret_cast<const uint2*>(kvl + ro + a.k_off) : z;
+          vl2[i] = ok && kvl ? *reinterpret_cast<const uint2*>(kvl + ro + a.v_off) : z;
+        }
+      } else {
+        const float* row = kvb + ro;
+        kreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.k_off) : f32x4{0.f, 0.f, 0.f, 0.f};
+        vreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.v_off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   };
   auto store_block = [&]() {
@@ -783,13 +822,22 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
     for (int i = 0; i < 4; ++i) {
       const int e = tid + i * kThreads;
       const int key = e >> 4, dq = (e & 15) * 4;
+      const int off = swz(key, dq >> 3) + ((dq & 4) << 1);
+      if constexpr (PRE) {
+        *reinterpret_cast<uint2*>(Khi + off) = kh2[i];
+        *reinterpret_cast<uint2*>(Vhi + off) = vh2[i];
+        if (X3) {
+          *reinterpret_cast<uint2*>(Klo + off) = kl2[i];
+          *reinterpret_cast<uint2*>(Vlo + off) = vl2[i];
+        }
+        continue;
+      }
       __bf16 hi[4], lo[4], vh[4], vl[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         split_bf16(kreg[i][q], hi[q], lo[q]);
         split_bf16(vreg[i][q], vh[q], vl[q]);
       }
-      const int off = swz(key, dq >> 3) + ((dq & 4) << 1);
       *reinterpret_cast<uint2*>(Khi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
       *reinterpret_cast<uint2*>(Vhi + off) = make_uint2(pack2(vh[0], vh[1]), pack2(vh[2], vh[3]));
       if (X3) {
@@ -897,7 +945,17 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
 
   if (!q_ok) return;
   const int64_t tq = token(q_pos);
-  const float gate = a.g_off >= 0 ? sigmoidf_(a.qkv[tq * a.ld + a.g_off + head]) : 1.f;
+  float glogit = 0.f;
+  if (a.g_off >= 0) {
+    if constexpr (PRE) {
+      const int64_t go = tq * a.ld + a.g_off + head;
+      glogit = __uint_as_float((uint32_t)a.qkv_hi[go] << 16) +
+               (a.qkv_lo ? __uint_as_float((uint32_t)a.qkv_lo[go] << 16) : 0.f);
+    } else {
+      glogit = a.qkv[tq * a.ld + a.g_off + head];
+    }
+  }
+  const float gate = a.g_off >= 0 ? sigmoidf_(glogit) : 1.f;
   const float scale = gate / l_run;
   const int64_t obase = tq * a.o_ld + head * dh;
 #pragma unroll
@@ -1005,6 +1063,8 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
       case EP_RES: SESA_GLDS(EP_RES) break;
       case EP_RS | EP_GELU | EP_SPLIT: SESA_GLDS(EP_RS | EP_GELU | EP_SPLIT) break;
       case EP_GELU | EP_SPLIT: SESA_GLDS(EP_GELU | EP_SPLIT) break;
+      case EP_SPLIT: SESA_GLDS(EP_SPLIT) break;                       // q / k / v planes for attention
+      case EP_RS | EP_ROPE | EP_SPLIT: SESA_GLDS(EP_RS | EP_ROPE | EP_SPLIT) break;
       default: ep = -1;
     }
 #undef SESA_GLDS
@@ -1045,8 +1105,18 @@ int launch_attention(const AttnArgs& a, int x3, hipStream_t st) {
                SESA_ERR_INVALID, "attention: bad shape");
   SESA_REQUIRE(a.n_seq < 65536 * 4 && a.heads < 65536, SESA_ERR_INVALID, "attention: grid too large");
   dim3 grid((unsigned)((a.L + 127) / 128), (unsigned)a.heads, (unsigned)a.n_seq);
-  if (x3) hipLaunchKernelGGL(attn_kernel<true>, grid, dim3(kThreads), 0, st, a);
-  else hipLaunchKernelGGL(attn_kernel<false>, grid, dim3(kThreads), 0, st, a);
+  const bool pre = a.qkv_hi != nullptr;
+  SESA_REQUIRE(!pre || ((!a.kv || a.kv_hi) && (a.dh == 0 || a.dh % 8 == 0) && a.ld % 8 == 0 && a.k_off % 4 == 0 &&
+                        a.v_off % 4 == 0 && (!x3 || (a.qkv_lo && (!a.kv || a.kv_lo)))),
+               SESA_ERR_INVALID, "attention: pre-split planes need dh %% 8, 8-B aligned offsets and the lo planes");
+  if (pre) {
+    if (x3) hipLaunchKernelGGL((attn_kernel<true, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((attn_kernel<false, true>), grid, dim3(kThreads), 0, st, a);
+  } else if (x3) {
+    hipLaunchKernelGGL((attn_kernel<true, false>), grid, dim3(kThreads), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((attn_kernel<false, false>), grid, dim3(kThreads), 0, st, a);
+  }
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }

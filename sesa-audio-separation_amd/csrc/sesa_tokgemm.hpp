@@ -104,6 +104,13 @@ struct AttnArgs {
   int dh;                     // head dim, <= 64 and % 4 == 0 (0: 64); scale 1 / sqrt(dh)
   uint16_t* out_hi;           // nullable: write bf16 planes (o_ld) instead of fp32 `out` (pre-split A of
   uint16_t* out_lo;           //   the following to_out tok_gemm); out_lo may be null (bf16)
+  // nullable: q / k / v / gate logits as the bf16 hi / lo planes the projection GEMM's split epilogue
+  // wrote (same strides and column offsets as qkv / kv); the kernel then stages K / V with plain copies
+  // (no fp32 -> hi / lo split per query block) and takes Q from the planes.  *_lo null for bf16.
+  const uint16_t* qkv_hi;
+  const uint16_t* qkv_lo;
+  const uint16_t* kv_hi;
+  const uint16_t* kv_lo;
 };
 
 
