@@ -543,12 +543,16 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  // waves whose 64 columns all lie past the group's N (the partial last tile, e.g. BS-Roformer's
+  // 8 gate columns after q / k / v) skip their MFMAs (wave-uniform); they still issue their DMA pieces
+  const bool busy = n0 + wn * 64 < g.N;
   for (int kc = 0; kc < n_chunks; ++kc) {
     char* cur = smem + (kc & 1) * STAGE;
     // chunk kc + 1 into the other stage: its last fragment reads (iteration kc - 1) were retired
     // by the lgkmcnt(0) before that iteration's barrier
     if (kc + 1 < n_chunks) issue(kc + 1, smem + ((kc + 1) & 1) * STAGE);
-    if constexpr (M16) {
+    if (!busy) {
+    } else if constexpr (M16) {
       Frags f0;
       read_frags(f0, cur, 0);
       mfmas(f0);
