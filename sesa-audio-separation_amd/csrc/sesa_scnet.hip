@@ -343,6 +343,146 @@ __global__ void __launch_bounds__(kST) scn_cm_out_kernel(CmArgs a) {
   }
 }
 
+// ---- ConvolutionModule for wide levels (SCNet-large / XL: C = 256, h = 64, or h not dividing 512),
+// where a row's conv1d weight [C][3][2h] (393 KB at C = 256) or its [T][h] hidden planes exceed LDS.
+// Same arithmetic as scn_cm_in_kernel / scn_cm_out_kernel, restaged:
+//   in:  one workgroup per (b, f) row; GroupNorm(1, C) stats once per row, then per tile of kGenTT
+//        positions the weight is walked in 16-channel slices ([16][3][2h] in LDS) with the normalised
+//        [TT + 2][16] input slice beside it; each thread accumulates up to 8 (t, j) GLU pairs.
+//   out: one workgroup per row; pass 1 recomputes the depthwise k3 conv from U (global, L2-resident)
+//        for the GroupNorm(1, h) sums, pass 2 per tile of kGenTO positions: depthwise conv, GN, Swish
+//        into LDS, then the 1x1 conv h -> C from the LDS-resident W3 [h][C], residual, optional GELU.
+constexpr int kGenCC = 16;   // channels per weight slice
+constexpr int kGenNQ = 8;    // (t, j) outputs per thread per tile
+constexpr int kGenTO = 16;   // positions per output tile
+inline int gen_tt(int h) { return kGenNQ * (kST / h); }
+size_t cm_in_gen_lds(int h) { return (size_t)(kGenCC * 6 * h + (gen_tt(h) + 2) * kGenCC) * 4 + 16 * 8 + 16; }
+size_t cm_out_gen_lds(int C, int h) { return (size_t)(kGenTO * h + h * C) * 4 + 16 * 8 + 16; }
+
+__global__ void __launch_bounds__(kST) scn_cm_in_gen_kernel(CmArgs a) {
+  extern __shared__ __align__(16) float sm[];
+  const int C = a.C, h = a.h, T = a.T;
+  const int G = kST / h;                        // thread groups; thread (g, j) owns unit j
+  const int TT = kGenNQ * G;                    // positions per tile: tl = g + G * r, r < kGenNQ
+  float* Ws = sm;                               // [16][3][2h]
+  float* xs = Ws + kGenCC * 6 * h;              // [TT + 2][16]
+  double* red = reinterpret_cast<double*>(xs + (TT + 2) * kGenCC + 2);
+  const int row = blockIdx.x;
+  const int64_t b = row / a.n_f;
+  const int f = a.f_off + row % a.n_f;
+  const float* xr = a.X + ((b * a.F_all + f) * T) * C;
+  double s = 0, ss = 0;
+  for (int i = threadIdx.x; i < T * C; i += kST) {
+    const double v = xr[i];
+    s += v;
+    ss += v * v;
+  }
+  block_sum2(s, ss, red);
+  const double n = (double)T * C;
+  const double mu = s / n;
+  const double var = fmax(ss / n - mu * mu, 0.0);
+  const float mean = (float)mu, rstd = (float)(1.0 / sqrt(var + 1e-5));
+  float* U = a.U + (int64_t)row * T * h;
+  const int g = threadIdx.x / h, j = threadIdx.x - g * h;
+  const bool active = g < G;
+  for (int t0 = 0; t0 < T; t0 += TT) {
+    float ga[kGenNQ], gg[kGenNQ];
+#pragma unroll
+    for (int r = 0; r < kGenNQ; ++r) {
+      ga[r] = active ? a.b1[j] : 0.f;
+      gg[r] = active ? a.b1[j + h] : 0.f;
+    }
+    for (int c0 = 0; c0 < C; c0 += kGenCC) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < kGenCC * 6 * h; i += kST) {
+        const int cl = i / (6 * h), e = i - cl * 6 * h;
+        Ws[i] = c0 + cl < C ? a.W1[(int64_t)(c0 + cl) * 6 * h + e] : 0.f;
+      }
+      for (int i = threadIdx.x; i < (TT + 2) * kGenCC; i += kST) {
+        const int tl = i / kGenCC, cl = i - tl * kGenCC;
+        const int t = t0 - 1 + tl, c = c0 + cl;
+        xs[i] = (t >= 0 && t < T && c < C) ? (xr[(int64_t)t * C + c] - mean) * rstd * a.g1[c] + a.be1[c] : 0.f;
+      }
+      __syncthreads();
+      if (!active) continue;
+#pragma unroll 1
+      for (int dt = 0; dt < 3; ++dt) {
+#pragma unroll 4
+        for (int c = 0; c < kGenCC; ++c) {
+          const float wa = Ws[(c * 3 + dt) * 2 * h + j], wg = Ws[(c * 3 + dt) * 2 * h + h + j];
+#pragma unroll
+          for (int r = 0; r < kGenNQ; ++r) {
+            const float xv = xs[(g + G * r + dt) * kGenCC + c];
+            ga[r] = fmaf(wa, xv, ga[r]);
+            gg[r] = fmaf(wg, xv, gg[r]);
+          }
+        }
+      }
+    }
+    if (active) {
+#pragma unroll
+      for (int r = 0; r < kGenNQ; ++r) {
+        const int t = t0 + g + G * r;
+        if (t < T) U[(int64_t)t * h + j] = ga[r] * sigm(gg[r]);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kST) scn_cm_out_gen_kernel(CmArgs a) {
+  extern __shared__ __align__(16) float sm[];
+  const int C = a.C, h = a.h, T = a.T;
+  float* W3s = sm;                 // [h][C]
+  float* Vs = W3s + h * C;         // [kGenTO][h]
+  double* red = reinterpret_cast<double*>(Vs + kGenTO * h + ((h * C + kGenTO * h) & 1));
+  const int row = blockIdx.x;
+  const int64_t b = row / a.n_f;
+  const int f = a.f_off + row % a.n_f;
+  float* xr = a.X + ((b * a.F_all + f) * T) * C;
+  const float* U = a.U + (int64_t)row * T * h;
+  for (int i = threadIdx.x; i < h * C; i += kST) W3s[i] = a.W3[i];
+  auto dw = [&](int t, int j) {
+    const int i = t * h + j;
+    float v = a.bdw[j];
+    if (t > 0) v = fmaf(a.wdw[3 * j], U[i - h], v);
+    v = fmaf(a.wdw[3 * j + 1], U[i], v);
+    if (t < T - 1) v = fmaf(a.wdw[3 * j + 2], U[i + h], v);
+    return v;
+  };
+  double s = 0, ss = 0;
+  for (int i = threadIdx.x; i < T * h; i += kST) {
+    const int t = i / h, j = i - t * h;
+    const float v = dw(t, j);
+    s += v;
+    ss += (double)v * v;
+  }
+  block_sum2(s, ss, red);
+  const double n = (double)T * h;
+  const double mu = s / n;
+  const double var = fmax(ss / n - mu * mu, 0.0);
+  const float mean = (float)mu, rstd = (float)(1.0 / sqrt(var + 1e-5));
+  for (int t0 = 0; t0 < T; t0 += kGenTO) {
+    const int nt = min(kGenTO, T - t0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nt * h; i += kST) {
+      const int tl = i / h, j = i - tl * h;
+      const float v = (dw(t0 + tl, j) - mean) * rstd * a.g2[j] + a.be2[j];
+      Vs[i] = v * sigm(v);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nt * C; i += kST) {
+      const int tl = i / C, c = i - tl * C;
+      float acc = a.b3[c];
+      const float* sv = Vs + tl * h;
+      for (int j = 0; j < h; ++j) acc = fmaf(W3s[j * C + c], sv[j], acc);
+      const int64_t o = (int64_t)(t0 + tl) * C + c;
+      float v = xr[o] + acc;
+      if (a.gelu) v = gelu_erf(v);
+      xr[o] = v;
+    }
+  }
+}
+
 __global__ void scn_gelu_rows_kernel(float* X, int F_all, int f_off, int n_f, int64_t row_elems, int64_t total) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
@@ -599,9 +739,10 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, cons
     const int sq = s0 + threadIdx.x;
     rowb[threadIdx.x] = sq < a.n_seq ? (int64_t)(sq / a.sdiv) * a.smul_a + (int64_t)(sq % a.sdiv) * a.smul_b : -1;
   }
-  // H <= 128: the compiler keeps the whole W_hh slice of a wave in registers across steps (<= 256);
-  // H = 256 (512 per wave) streams it from L2 every step: `volatile` stops that hoisting.
-  constexpr bool STREAM = NW >= 8;
+  // H <= 128: the compiler keeps the whole W_hh slice of a wave in registers across steps (<= 256,
+  // one wave per SIMD); H = 160 .. 256 (two waves on a SIMD) streams it from L2 every step: `volatile`
+  // stops that hoisting.
+  constexpr bool STREAM = NW > 4;
   using WP = typename std::conditional<STREAM, const volatile bf16x8*, const bf16x8*>::type;
   WP wb = reinterpret_cast<WP>(Wf) + (int64_t)(dir * NW + w) * KS * 4 * 2 * 64 + lane;
   __syncthreads();
@@ -674,20 +815,144 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, cons
   }
 }
 
+// Wide recurrence (H = 288 .. 512, SCNet-large / XL odd dual-path layers: d = 2 dims[-1]): NW = H / 32
+// waves (up to 1024 threads, 4 waves per SIMD, 128 registers each), the MFMA decomposition of
+// scn_lstm_mfma_kernel.  The register budget is met by starting the accumulators from the
+// input-projection gates (no separate gate registers) and streaming W_hh's B fragments through a
+// one-k-step ring (4 gates x hi / lo = 32 registers): gate q of k-step ks + 1 is requested as soon as
+// gate q of k-step ks has been consumed.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_wide_kernel(LstmArgs a, const uint16_t* __restrict__ Wf) {
+  constexpr int H = 32 * NW, H4 = 4 * H, KS = H / 16, RS = H + 8;
+  extern __shared__ __align__(16) uint16_t lsa[];
+  uint16_t* Ahi = lsa;            // [32 seq][RS]
+  uint16_t* Alo = lsa + 32 * RS;
+  int64_t* rowb = reinterpret_cast<int64_t*>(lsa + 64 * RS);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int dir = blockIdx.y;
+  const int s0 = blockIdx.x * 32;
+  const int j = 32 * w + l32;
+  float c[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) c[r] = 0.f;
+  for (int i = threadIdx.x; i < 64 * RS; i += 64 * NW) lsa[i] = 0;  // h_0 = 0 (hi and lo)
+  if (threadIdx.x < 32) {
+    const int sq = s0 + threadIdx.x;
+    rowb[threadIdx.x] = sq < a.n_seq ? (int64_t)(sq / a.sdiv) * a.smul_a + (int64_t)(sq % a.sdiv) * a.smul_b : -1;
+  }
+  const volatile bf16x8* wb =
+      reinterpret_cast<const volatile bf16x8*>(Wf) + (int64_t)(dir * NW + w) * KS * 4 * 2 * 64 + lane;
+  __syncthreads();
+  for (int step = 0; step < a.L; ++step) {
+    const int pos = dir ? a.L - 1 - step : step;
+    asm volatile("" ::: "memory");  // re-read rowb per step (no 32 hoisted row registers)
+    f32x16 acc[4];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t rb = rowb[(r & 3) + 8 * (r >> 2) + 4 * hh];
+      const float* gp = a.G + (rb >= 0 ? (rb + (int64_t)pos * a.pstride) * a.g_ld + dir * H4 + j : 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q][r] = rb >= 0 ? gp[q * H] : 0.f;
+    }
+    bf16x8 bh[4], bl[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bh[q] = wb[(q * 2 + 0) * 64];
+      bl[q] = wb[(q * 2 + 1) * 64];
+    }
+#pragma unroll 1
+    for (int ks = 0; ks < KS; ++ks) {
+      const int ao = l32 * RS + 16 * ks + 8 * hh;
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ahi + ao);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Alo + ao);
+      const int kn = ks + 1 < KS ? ks + 1 : ks;  // (the last k-step re-reads its own fragments: harmless)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[q] = mfma_bf16(al, bh[q], acc[q]);
+        acc[q] = mfma_bf16(ah, bl[q], acc[q]);
+        acc[q] = mfma_bf16(ah, bh[q], acc[q]);
+        bh[q] = wb[((kn * 4 + q) * 2 + 0) * 64];
+        bl[q] = wb[((kn * 4 + q) * 2 + 1) * 64];
+      }
+    }
+    __syncthreads();  // every wave has read h_{t-1}
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int sl = (r & 3) + 8 * (r >> 2) + 4 * hh;
+      const float ig = sigm_f(acc[0][r]), fg = sigm_f(acc[1][r]);
+      const float gg = tanh_f(acc[2][r]), og = sigm_f(acc[3][r]);
+      c[r] = fg * c[r] + ig * gg;
+      const float hv = og * tanh_f(c[r]);
+      __bf16 hi, lo;
+      split_bf16(hv, hi, lo);
+      Ahi[sl * RS + j] = __builtin_bit_cast(uint16_t, hi);
+      Alo[sl * RS + j] = __builtin_bit_cast(uint16_t, lo);
+      const int64_t rb = rowb[sl];
+      if (rb >= 0) a.HO[(rb + (int64_t)pos * a.pstride) * a.ho_ld + dir * H + j] = hv;
+    }
+    __syncthreads();  // h_t visible
+  }
+}
+
+// Smallest NW = H / 32 that takes scn_lstm_mfma_wide_kernel (SESA_LSTM_WIDE_MIN_NW, default 5: every H > 128).
+// The register-resident kernel (NW <= 4) keeps W_hh in registers; its streamed form (NW 5..8) spills
+// (170 VGPRs at H = 256), which the wide kernel's ring does not: same box, musdb18 SCNet 4-min track,
+// LSTM class 180 -> 134 ms per step, 335.6x -> 359.1x real-time (profiles/r03_scnet_lstm_wide_{A,B,A2}.json).
+int lstm_wide_min_nw() {
+  static const int v = getenv("SESA_LSTM_WIDE_MIN_NW") ? atoi(getenv("SESA_LSTM_WIDE_MIN_NW")) : 5;
+  return v;
+}
+
+size_t lstm_mfma_lds(int H) { return (size_t)64 * (H + 8) * 2 + 32 * 8; }
+
 template <int NW>
 void launch_lstm_mfma_t(const LstmArgs& a, const uint16_t* Wf, hipStream_t st) {
   constexpr int PF = 2;
-  const size_t lds = (size_t)64 * (32 * NW + 8) * 2 + 32 * 8;
+  const size_t lds = lstm_mfma_lds(32 * NW);
   dim3 grid((unsigned)((a.n_seq + 31) / 32), 2);
-  hipLaunchKernelGGL((scn_lstm_mfma_kernel<NW, PF>), grid, dim3(64 * NW), lds, st, a, Wf);
+  if constexpr (NW <= 8) {
+    if (NW < lstm_wide_min_nw()) {
+      hipLaunchKernelGGL((scn_lstm_mfma_kernel<NW, PF>), grid, dim3(64 * NW), lds, st, a, Wf);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((scn_lstm_mfma_wide_kernel<NW>), grid, dim3(64 * NW), lds, st, a, Wf);
+}
+
+// Raise the dynamic-LDS limit of the wide recurrence instances (> 64 KiB at H = 512); finalize time.
+int lstm_mfma_prepare(int H) {
+  if (lstm_mfma_lds(H) <= 64 * 1024) return SESA_OK;
+  const void* fn = nullptr;
+  switch (H / 32) {
+#define SESA_WIDE(n) \
+  case n: fn = (const void*)scn_lstm_mfma_wide_kernel<n>; break;
+    SESA_WIDE(9) SESA_WIDE(10) SESA_WIDE(11) SESA_WIDE(12) SESA_WIDE(13) SESA_WIDE(14) SESA_WIDE(15) SESA_WIDE(16)
+#undef SESA_WIDE
+    default: return SESA_OK;
+  }
+  SESA_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lstm_mfma_lds(H)));
+  return SESA_OK;
 }
 
 void launch_lstm_mfma(const LstmArgs& a, const uint16_t* Wf, hipStream_t st) {
-  switch (a.H) {
-    case 32: launch_lstm_mfma_t<1>(a, Wf, st); break;
-    case 64: launch_lstm_mfma_t<2>(a, Wf, st); break;
-    case 128: launch_lstm_mfma_t<4>(a, Wf, st); break;
-    default: launch_lstm_mfma_t<8>(a, Wf, st); break;
+  switch (a.H / 32) {
+    case 1: launch_lstm_mfma_t<1>(a, Wf, st); break;
+    case 2: launch_lstm_mfma_t<2>(a, Wf, st); break;
+    case 3: launch_lstm_mfma_t<3>(a, Wf, st); break;
+    case 4: launch_lstm_mfma_t<4>(a, Wf, st); break;
+    case 5: launch_lstm_mfma_t<5>(a, Wf, st); break;
+    case 6: launch_lstm_mfma_t<6>(a, Wf, st); break;
+    case 7: launch_lstm_mfma_t<7>(a, Wf, st); break;
+    case 8: launch_lstm_mfma_t<8>(a, Wf, st); break;
+    case 9: launch_lstm_mfma_t<9>(a, Wf, st); break;
+    case 10: launch_lstm_mfma_t<10>(a, Wf, st); break;
+    case 11: launch_lstm_mfma_t<11>(a, Wf, st); break;
+    case 12: launch_lstm_mfma_t<12>(a, Wf, st); break;
+    case 13: launch_lstm_mfma_t<13>(a, Wf, st); break;
+    case 14: launch_lstm_mfma_t<14>(a, Wf, st); break;
+    case 15: launch_lstm_mfma_t<15>(a, Wf, st); break;
+    default: launch_lstm_mfma_t<16>(a, Wf, st); break;
   }
 }
 
@@ -858,6 +1123,7 @@ struct CmLayer {  // float offsets into the packed fp32 blob
 
 struct Level {
   int Fin, Fout, Cin, Cout, h, Cdec;  // Cdec: SU output channels
+  bool cm_gen;                        // ConvolutionModule on the wide-level kernels (scn_cm_*_gen_kernel)
   BandConv sd[3], su[3];
   int64_t sd_w[3], sd_b[3], gc_w, gc_b, fu_w, fu_b, su_w[3], su_b[3];
   std::vector<CmLayer> cm[3];
@@ -922,9 +1188,10 @@ size_t al(size_t floats) { return (floats * 4 + 255) / 256 * 256; }
 // Recurrence kernel choice (measured on MI355X, musdb18 config, 4-min track): bf16x3 MFMA for every
 // H (325.7x real-time) beats MFMA for H <= 128 only (307.6x) and the fp32-FMA kernel (280.8x).
 // SESA_LSTM_MFMA=0: fp32 everywhere; =1: MFMA for H <= 128 only (A/B comparisons).
+// (The fp32 kernel needs 256 % H == 0; wider or odd widths always take the MFMA recurrence.)
 bool lstm_mfma_on(int H) {
   static const int mode = getenv("SESA_LSTM_MFMA") ? atoi(getenv("SESA_LSTM_MFMA")) : 2;
-  return mode == 2 || (mode == 1 && H <= 128);
+  return mode == 2 || (mode == 1 && H <= 128) || H > 256 || kST % H != 0;
 }
 
 Plan plan(const sesa_scnet* m, int B) {
@@ -1049,10 +1316,13 @@ extern "C" int sesa_scnet_create(const sesa_scnet_config* cfg, sesa_scnet** out)
       su.out_off = bc.in_off;
     }
     L.Fout = fo;
-    if (L.h < 1 || (512 % L.h) != 0 || L.h > 64) return fail("ConvolutionModule hidden size must divide 512 and be <= 64", L.h);
+    if (L.h < 1) return fail("ConvolutionModule hidden size must be >= 1", L.h);
     if (L.Cout % 16 || L.Cdec % 4) return fail("dims must be multiples of 16 (decoder output channels of 4)", L.Cout);
-    if (cm_in_lds(L.Cout, L.h) > 160 * 1024 || cm_out_lds(m->T, L.Cout, L.h) > 160 * 1024)
-      return fail("ConvolutionModule row does not fit in LDS", L.Cout);
+    // the row-resident kernels where they fit (base / small configs), else the wide-level kernels
+    L.cm_gen = (512 % L.h) != 0 || L.h > 64 || cm_in_lds(L.Cout, L.h) > 160 * 1024 ||
+               cm_out_lds(m->T, L.Cout, L.h) > 160 * 1024;
+    if (L.cm_gen && (L.h > kST || cm_in_gen_lds(L.h) > 160 * 1024 || cm_out_gen_lds(L.Cout, L.h) > 160 * 1024))
+      return fail("ConvolutionModule too wide for LDS (1x1 weight [h][C] must fit)", L.Cout);
     m->lv.push_back(L);
     Fr = fo;
   }
@@ -1061,7 +1331,7 @@ extern "C" int sesa_scnet_create(const sesa_scnet_config* cfg, sesa_scnet** out)
     DpLayer L{};
     L.d = dlast * (i % 2 ? 2 : 1);
     L.H = L.d * c.expand;
-    if (L.H != 32 && L.H != 64 && L.H != 128 && L.H != 256) return fail("LSTM hidden size must be 32/64/128/256", L.H);
+    if (L.H % 32 || L.H < 32 || L.H > 512) return fail("LSTM hidden size must be a multiple of 32 in [32, 512]", L.H);
     m->dp.push_back(L);
   }
   // parameter registry, reference state_dict order (scnet.py:280-323)
@@ -1323,6 +1593,10 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
   if (!bias.empty()) SESA_CHECK_HIP(hipMemcpyAsync(m->d_bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice, st));
   SESA_CHECK_HIP(hipMemcpyAsync(m->d_twT, twT.data(), twT.size() * sizeof(float2), hipMemcpyHostToDevice, st));
   SESA_CHECK_HIP(hipStreamSynchronize(st));
+  for (auto& L : m->dp) {
+    const int rc = lstm_mfma_prepare(L.H);
+    if (rc) return rc;
+  }
   for (auto& L : m->dp)
     for (int l = 0; l < 2; ++l) {
       int rc = upload_groups(L.ih[l]);
@@ -1332,6 +1606,10 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
   SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_in_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024));
   SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_out_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+  SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_in_gen_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+  SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_out_gen_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024));
   m->finalized = true;
   return SESA_OK;
@@ -1421,10 +1699,17 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         a.W3 = Wb + cl.w3;
         a.b3 = Wb + cl.b3;
         a.gelu = l + 1 == L.cm[b].size();
-        hipLaunchKernelGGL(scn_cm_in_kernel, dim3(rows), dim3(kST), cm_in_lds(L.Cout, L.h), st, a);
-        SESA_CHECK_LAUNCH();
-        hipLaunchKernelGGL(scn_cm_out_kernel, dim3(rows), dim3(kST), cm_out_lds(T, L.Cout, L.h), st, a);
-        SESA_CHECK_LAUNCH();
+        if (L.cm_gen) {
+          hipLaunchKernelGGL(scn_cm_in_gen_kernel, dim3(rows), dim3(kST), cm_in_gen_lds(L.h), st, a);
+          SESA_CHECK_LAUNCH();
+          hipLaunchKernelGGL(scn_cm_out_gen_kernel, dim3(rows), dim3(kST), cm_out_gen_lds(L.Cout, L.h), st, a);
+          SESA_CHECK_LAUNCH();
+        } else {
+          hipLaunchKernelGGL(scn_cm_in_kernel, dim3(rows), dim3(kST), cm_in_lds(L.Cout, L.h), st, a);
+          SESA_CHECK_LAUNCH();
+          hipLaunchKernelGGL(scn_cm_out_kernel, dim3(rows), dim3(kST), cm_out_lds(T, L.Cout, L.h), st, a);
+          SESA_CHECK_LAUNCH();
+        }
         fl += 2.0 * rows * T * (6.0 * L.h * L.Cout + 3.0 * L.h + (double)L.h * L.Cout);
       }
     }

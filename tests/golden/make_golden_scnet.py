@@ -11,6 +11,8 @@ Fixtures:
   scnet_small.npz          SCNet.forward, reduced config, batch 2 x 1 s, random GroupNorm affines
   demix_scnet_small.npz    inference_pytorch.demix_pytorch_optimized on the reduced model (2.5 s mix)
   scnet_full_chunk.npz     (--full) one 485100-sample chunk through the musdb18 config
+  scnet_large_small.npz    SCNet.forward at the SCNet-large widths (dims [4, 64, 128, 256], LSTM H 256 / 512)
+  scnet_wide_small.npz     SCNet.forward at dims [4, 48, 96, 192] (CM hidden 48, LSTM H 192 / 384)
 """
 import argparse
 import contextlib
@@ -86,12 +88,16 @@ def main():
     args = ap.parse_args()
     mg.install_stubs()
     torch.set_num_threads(os.cpu_count())
-    todo = args.only.split(",") if args.only else ["params", "fwd", "demix"]
+    todo = args.only.split(",") if args.only else ["params", "fwd", "demix", "wide"]
     if "params" in todo:
         gen_params("config_musdb18_scnet.yaml", "musdb")
         gen_params("config_scnet_small.yaml", "small")
+        gen_params("config_scnet_large_small.yaml", "large_small")
     if "fwd" in todo:
         gen_forward("config_scnet_small.yaml", "scnet_small.npz", 2, 61, "random")
+    if "wide" in todo:
+        gen_forward("config_scnet_large_small.yaml", "scnet_large_small.npz", 1, 71, "random")
+        gen_forward("config_scnet_wide_small.yaml", "scnet_wide_small.npz", 2, 81, "random")
     if "demix" in todo:
         gen_demix()
     if args.full or "full" in todo:

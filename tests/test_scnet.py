@@ -38,7 +38,9 @@ def _model(cfg_name, affine="random", precision="bf16x3"):
 
 
 @pytest.mark.parametrize("cfg_name,fx", [("config_scnet_small.yaml", "scnet_small.npz"),
-                                         ("config_musdb18_scnet.yaml", "scnet_full_chunk.npz")])
+                                         ("config_musdb18_scnet.yaml", "scnet_full_chunk.npz"),
+                                         ("config_scnet_large_small.yaml", "scnet_large_small.npz"),
+                                         ("config_scnet_wide_small.yaml", "scnet_wide_small.npz")])
 def test_oracle_matches_reference(cfg_name, fx, golden):
     from oracle import scnet as osc
     g = golden(fx)
@@ -50,7 +52,8 @@ def test_oracle_matches_reference(cfg_name, fx, golden):
     assert rms(y, g["y"]) <= 1e-6
 
 
-@pytest.mark.parametrize("cfg_name,tag", [("config_musdb18_scnet.yaml", "musdb"), ("config_scnet_small.yaml", "small")])
+@pytest.mark.parametrize("cfg_name,tag", [("config_musdb18_scnet.yaml", "musdb"), ("config_scnet_small.yaml", "small"),
+                                          ("config_scnet_large_small.yaml", "large_small")])
 def test_registry_matches_reference_state_dict(cfg_name, tag):
     from sesa import _native as N
     from sesa.utils import get_model_from_config
@@ -111,6 +114,21 @@ def test_forward_small_matches_reference(golden, dev):
     y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
     err = rms(y, g["y"])
     print(f"scnet small rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    assert y.shape == g["y"].shape and err <= RMS_GATE
+
+
+# SCNet-large widths (registry "4STEMS-SCNet_Large", model.py:1347-1353; ConvolutionModule rows too wide
+# for LDS, LSTM H = 512 on the odd dual-path layer) and an intermediate width (CM hidden 48, LSTM H 192 /
+# 384): the wide kernels (scn_cm_*_gen_kernel, scn_lstm_mfma_wide_kernel) against the reference.
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_name,fx", [("config_scnet_large_small.yaml", "scnet_large_small.npz"),
+                                         ("config_scnet_wide_small.yaml", "scnet_wide_small.npz")])
+def test_forward_wide_matches_reference(golden, dev, cfg_name, fx):
+    g = golden(fx)
+    m, _ = _model(cfg_name, str(g["affine"]))
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"{cfg_name} rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
     assert y.shape == g["y"].shape and err <= RMS_GATE
 
 
