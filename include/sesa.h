@@ -131,6 +131,10 @@ int sesa_mdx23c_destroy(sesa_mdx23c* m);
  * 1 = conv3x3_m16_kernel (v_mfma_f32_16x16x32_bf16, persistent, LDS-DMA; measured on par).
  * Initialised from SESA_CONV_VARIANT=m16.  A forward picks it up at its next call. */
 int sesa_mdx23c_set_conv_variant(int variant);
+/* Winograd F(2, 3) TFC 3x3 convolutions (conv3x3_wino_kernel; process-wide, returns the previous value):
+ * 0 = off (default), 1 = levels with 32 <= T <= 128, 2 = every level with T >= 32.  Initialised from
+ * SESA_CONV_WINO; decided per convolution when a model is finalized (the weights are packed for it). */
+int sesa_mdx23c_set_wino(int mode);
 
 /* ---------------------------------------------------------------------------------------
  * BS-Roformer (models/bs_roformer/bs_roformer.py:327-587, BSRoformer)

@@ -51,6 +51,7 @@ struct Param {
 struct ConvW {
   int kind = 0, C_in = 0, C_out = 0, n_cols = 0, bn = 64, param = -1;
   int64_t w_off = 0;  // uint16 offset into the packed weight blob
+  bool wino = false;  // packed for conv3x3_wino_kernel (decided at finalize, conv3x3_wino_selected)
 };
 struct TdfW {
   int M = 0, K = 0, param = -1;
@@ -64,7 +65,7 @@ struct Block {
   Norm tfc1, tdf0, tdf3, tfc2;
   ConvW conv1, conv2, shortcut;
   TdfW lin1, lin2;
-  int in_c = 0, c = 0;
+  int in_c = 0, c = 0, T = 0;  // T: frames at this block's level
 };
 struct Stack {
   std::vector<Block> blocks;
@@ -135,13 +136,14 @@ ConvW add_conv(sesa_mdx23c* m, const std::string& name, int kind, int c_out, int
 }
 
 // TFC_TDF.__init__ (mdx23c_tfc_tdf_v3.py:100-129)
-Stack add_stack(sesa_mdx23c* m, const std::string& prefix, int in_c, int c, int f, int l, int bn) {
+Stack add_stack(sesa_mdx23c* m, const std::string& prefix, int in_c, int c, int f, int t, int l, int bn) {
   Stack s;
   for (int i = 0; i < l; ++i) {
     const std::string p = prefix + ".blocks." + std::to_string(i);
     Block b;
     b.in_c = in_c;
     b.c = c;
+    b.T = t;
     b.tfc1 = add_norm(m, p + ".tfc1.0", in_c);
     b.conv1 = add_conv(m, p + ".tfc1.2.weight", CONV3X3, c, in_c, 3, 3);
     b.tdf0 = add_norm(m, p + ".tdf.0", c);
@@ -216,6 +218,70 @@ void pack_conv(const Param& P, ConvW& w, std::vector<uint16_t>& blob, const Para
           const float v = ncol < N ? xs->host[(int64_t)ncol * xs_cin + ci] : 0.f;  // [c_out, c_in, 1, 1]
           put(hi, lo, n, kk, v);
         }
+    }
+  }
+}
+
+// Winograd F(2, 3) images for conv3x3_wino_kernel (sesa_tapgemm.hip): per 64-column block, per
+// 16-channel chunk two stage images -- points {0, 1}, then {2, 3} -- each [hi, lo][tap = point slot x 3
+// + dy][64][16] with the B-image swizzle, U_p from the (dy, dx) row of the kernel in fp64:
+//   U0 = w0, U1 = (w0 + w1 + w2) / 2, U2 = (w0 - w1 + w2) / 2, U3 = w2;
+// then the fused 1x1 shortcut `xs` as one image per chunk, [hi, lo][point slot][64][16] with the centre-
+// tap transforms U1 = w / 2, U2 = -w / 2.
+void pack_conv_wino(const Param& P, ConvW& w, std::vector<uint16_t>& blob, const Param* xs = nullptr, int xs_cin = 0) {
+  constexpr int BN = 64;
+  const int N = w.n_cols;
+  const int nblk = (N + BN - 1) / BN;
+  const int nch = w.C_in / kConvBK;
+  const int xch = xs ? xs_cin / kConvBK : 0;
+  w.bn = BN;
+  w.wino = true;
+  w.w_off = (int64_t)blob.size();
+  const int64_t per_nb = (int64_t)nch * 2 * kWinoMainImg + (int64_t)xch * kWinoShortImg;
+  blob.resize(blob.size() + (size_t)nblk * per_nb, 0);
+  uint16_t* base = blob.data() + w.w_off;
+  const float* W = P.host.data();
+  auto put = [](uint16_t* hi, uint16_t* lo, int p, int kk, double v) {
+    const int64_t o = (int64_t)p * 16 + ((((kk >> 3) ^ ((p >> 3) & 1))) << 3) + (kk & 7);
+    const float f = (float)v;
+    const uint16_t h = f2bf(f);
+    hi[o] = h;
+    lo[o] = f2bf((float)(v - (double)bf2f(h)));
+  };
+  for (int nb = 0; nb < nblk; ++nb) {
+    for (int kc = 0; kc < nch; ++kc)
+      for (int pp = 0; pp < 2; ++pp) {
+        uint16_t* hi = base + nb * per_nb + (int64_t)(2 * kc + pp) * kWinoMainImg;
+        uint16_t* lo = hi + kWinoMainImg / 2;
+        for (int pl = 0; pl < 2; ++pl)
+          for (int dy = 0; dy < 3; ++dy)
+            for (int n = 0; n < BN; ++n)
+              for (int kk = 0; kk < kConvBK; ++kk) {
+                const int co = nb * BN + n, ci = kc * kConvBK + kk;
+                double u = 0.0;
+                if (co < N) {
+                  const float* r = W + (((int64_t)co * w.C_in + ci) * 3 + dy) * 3;
+                  const double w0 = r[0], w1 = r[1], w2 = r[2];
+                  switch (2 * pp + pl) {
+                    case 0: u = w0; break;
+                    case 1: u = 0.5 * (w0 + w1 + w2); break;
+                    case 2: u = 0.5 * (w0 - w1 + w2); break;
+                    default: u = w2; break;
+                  }
+                }
+                put(hi, lo, (pl * 3 + dy) * BN + n, kk, u);
+              }
+      }
+    for (int kx = 0; kx < xch; ++kx) {
+      uint16_t* hi = base + nb * per_nb + (int64_t)nch * 2 * kWinoMainImg + (int64_t)kx * kWinoShortImg;
+      uint16_t* lo = hi + kWinoShortImg / 2;
+      for (int pl = 0; pl < 2; ++pl)
+        for (int n = 0; n < BN; ++n)
+          for (int kk = 0; kk < kConvBK; ++kk) {
+            const int co = nb * BN + n, ci = kx * kConvBK + kk;
+            const double v = co < N ? (double)xs->host[(int64_t)co * xs_cin + ci] : 0.0;  // [c_out, c_in, 1, 1]
+            put(hi, lo, pl * BN + n, kk, pl == 0 ? 0.5 * v : -0.5 * v);
+          }
     }
   }
 }
@@ -388,6 +454,26 @@ struct Fwd {
     return in;
   }
 
+  // GELU(InstanceNorm(a [++ b])) as fp32 -- the input of a Winograd conv (SRC_ACT32)
+  GemmIn act32(Tensor a, Tensor b, const Norm* nrm, int T, int F) {
+    const int C = a.C + (b.C > 0 ? b.C : 0);
+    const int64_t n = (int64_t)B * T * F * C;
+    float* y = buf(n);
+    const GemmIn src = input(a, b, SRC_NORM_GELU, SRC_NORM_GELU, nrm, T, F);
+    if (!dry && !rc) {
+      void* tok = profile_begin(st);
+      rc = launch_act_f32(src, (int64_t)T * F, B, y, st);
+      profile_end(tok, st, SESA_KCLASS_ACT, 8.0 * n);
+    }
+    GemmIn in{};
+    in.src[0] = Src{y, nullptr, nullptr, C, SRC_ACT32, nullptr, nullptr};
+    in.src[1] = in.src[0];
+    in.C_split = C;
+    in.C_in = C;
+    in.inv_count = src.inv_count;
+    return in;
+  }
+
   // Input of a TFC 3x3 conv (norm + GELU of `a` [++ `b`]): the raw normalised sources when the conv
   // kernel fuses the activation into its staging (T >= 32 levels), else one act_split pass.
   GemmIn conv3_input(Tensor a, Tensor b, const Norm* nrm, int T, int F, int C_out) {
@@ -412,10 +498,13 @@ struct Fwd {
       double* st_h2 = stats(c);
       double* st_out = stats(c);
       // x = tfc1(x); the shortcut's operand is split here too when conv2 runs on conv3x3_m16_kernel
-      const bool pre_sc = conv3x3_m16_selected(L.T, c, c, x0.C + (x1.C > 0 ? x1.C : 0));
+      const bool pre_sc = !bk.conv2.wino && conv3x3_m16_selected(L.T, c, c, x0.C + (x1.C > 0 ? x1.C : 0));
       GemmIn xs{};
-      conv(bk.conv1, pre_sc ? act(x0, x1, &bk.tfc1, L.T, L.F, &xs) : conv3_input(x0, x1, &bk.tfc1, L.T, L.F, c), L.T, L.F,
-           L.T, L.F, H, nullptr, st_h1, 0);
+      conv(bk.conv1,
+           bk.conv1.wino ? act32(x0, x1, &bk.tfc1, L.T, L.F)
+           : pre_sc      ? act(x0, x1, &bk.tfc1, L.T, L.F, &xs)
+                         : conv3_input(x0, x1, &bk.tfc1, L.T, L.F, c),
+           L.T, L.F, L.T, L.F, H, nullptr, st_h1, 0);
       // x = x + tdf(x)
       tdf(bk.lin1, input(Tensor{H, st_h1, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf0, L.T, L.F), L.T, U, nullptr, st_u,
           c, 0);
@@ -425,8 +514,10 @@ struct Fwd {
           c, 1, Up);
       // x = tfc2(x) + shortcut(block input): the 1x1 shortcut rides along as extra K (raw input)
       if (!pre_sc) xs = input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F);
-      conv(bk.conv2, conv3_input(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F, c), L.T, L.F, L.T, L.F, S, nullptr,
-           st_out, 0, &xs);
+      conv(bk.conv2,
+           bk.conv2.wino ? act32(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F)
+                         : conv3_input(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F, c),
+           L.T, L.F, L.T, L.F, S, nullptr, st_out, 0, &xs);
       x0 = Tensor{S, st_out, c};
       x1 = Tensor{};
       off = mark;  // release H, U and the act_split planes (stream order keeps reuse safe)
@@ -535,7 +626,7 @@ extern "C" int sesa_mdx23c_create(const sesa_mdx23c_config* cfg, sesa_mdx23c** o
   m->first_conv = add_conv(m, "first_conv.weight", CONV1X1, ch, m->dim_c, 1, 1);
   for (int i = 0; i < n; ++i) {
     m->lv.push_back(Level{t, f, ch});
-    m->enc.push_back(add_stack(m, "encoder_blocks." + std::to_string(i) + ".tfc_tdf", ch, ch, f, l, bn));
+    m->enc.push_back(add_stack(m, "encoder_blocks." + std::to_string(i) + ".tfc_tdf", ch, ch, f, t, l, bn));
     m->down_norm.push_back(add_norm(m, "encoder_blocks." + std::to_string(i) + ".downscale.conv.0", ch));
     m->down.push_back(
         add_conv(m, "encoder_blocks." + std::to_string(i) + ".downscale.conv.2.weight", CONV2X2S2, ch + g, ch, 2, 2));
@@ -544,7 +635,7 @@ extern "C" int sesa_mdx23c_create(const sesa_mdx23c_config* cfg, sesa_mdx23c** o
     ch += g;
   }
   m->lv.push_back(Level{t, f, ch});
-  m->bottleneck = add_stack(m, "bottleneck_block", ch, ch, f, l, bn);
+  m->bottleneck = add_stack(m, "bottleneck_block", ch, ch, f, t, l, bn);
   for (int i = 0; i < n; ++i) {
     m->up_norm.push_back(add_norm(m, "decoder_blocks." + std::to_string(i) + ".upscale.conv.0", ch));
     m->up.push_back(
@@ -552,7 +643,7 @@ extern "C" int sesa_mdx23c_create(const sesa_mdx23c_config* cfg, sesa_mdx23c** o
     f *= 2;
     t *= 2;
     ch -= g;
-    m->dec.push_back(add_stack(m, "decoder_blocks." + std::to_string(i) + ".tfc_tdf", 2 * ch, ch, f, l, bn));
+    m->dec.push_back(add_stack(m, "decoder_blocks." + std::to_string(i) + ".tfc_tdf", 2 * ch, ch, f, t, l, bn));
   }
   m->final0 = add_conv(m, "final_conv.0.weight", CONV1X1, ch, ch + m->dim_c, 1, 1);
   m->final2 = add_conv(m, "final_conv.2.weight", CONV1X1, m->ni * m->dim_c, ch, 1, 1);
@@ -594,8 +685,13 @@ extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
   auto pc = [&](ConvW& w) { pack_conv(m->params[w.param], w, blob); };
   auto pstack = [&](Stack& s) {
     for (auto& b : s.blocks) {
-      pc(b.conv1);
-      pack_conv(m->params[b.conv2.param], b.conv2, blob, &m->params[b.shortcut.param], b.in_c);
+      b.conv1.wino = b.conv2.wino = false;
+      if (conv3x3_wino_selected(b.T, b.in_c, b.c)) pack_conv_wino(m->params[b.conv1.param], b.conv1, blob);
+      else pc(b.conv1);
+      if (conv3x3_wino_selected(b.T, b.c, b.c))
+        pack_conv_wino(m->params[b.conv2.param], b.conv2, blob, &m->params[b.shortcut.param], b.in_c);
+      else
+        pack_conv(m->params[b.conv2.param], b.conv2, blob, &m->params[b.shortcut.param], b.in_c);
       pack_tdf(m->params[b.lin1.param], b.lin1, blob);
       pack_tdf(m->params[b.lin2.param], b.lin2, blob);
       pack_norm(m, b.tfc1, aff);
@@ -680,3 +776,5 @@ extern "C" int sesa_mdx23c_destroy(sesa_mdx23c* m) {
 }
 
 extern "C" int sesa_mdx23c_set_conv_variant(int variant) { return set_conv3x3_variant(variant); }
+
+extern "C" int sesa_mdx23c_set_wino(int mode) { return set_conv3x3_wino(mode); }

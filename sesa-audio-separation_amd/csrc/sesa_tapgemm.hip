@@ -865,6 +865,498 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// conv3x3_wino_kernel: the TFC 3x3 convolutions (mdx23c_tfc_tdf_v3.py:104-112, 121-129) as Winograd
+// F(2, 3) along the frequency axis -- per output pair (f = 2j, 2j + 1) and input row r of the 3-row
+// window, the 4-tap input transform
+//     d_i = x[r][2j - 1 + i]  (i = 0..3, zero padding),   V0 = d0 - d2, V1 = d1 + d2, V2 = d2 - d1, V3 = d1 - d3,
+// the weight transform (per dy, host, fp64: U0 = w0, U1 = (w0 + w1 + w2) / 2, U2 = (w0 - w1 + w2) / 2,
+// U3 = w2) and the output transform y(2j) = M0 + M1 + M2, y(2j + 1) = M1 - M2 - M3 with
+//     M_p[pair][co] = sum_{dy, ci} V_p[row + dy][pair][ci] U_p[dy][ci][co]
+// -- 12 MFMA taps per output pair where the direct form has 18 (2/3 of the MFMA work).  Each M_p is
+// a bf16x3 contraction like the direct kernel's; the transforms are fp32 adds (V) and fp64 (U), so the
+// result is the direct convolution to fp32 rounding (summation order differs).
+//   * Input: the consumer's activation GELU(InstanceNorm(x)) as fp32 (act_split's SRC_ACT32 output).
+//   * 512 threads (8 waves, one workgroup per CU), tile 16 rows (t) x 32 columns (f = 16 pairs) x 64
+//     output channels; wave w owns rows 2w, 2w + 1 as ONE 32-row MFMA block (row = m >> 4, pair =
+//     m & 15) x 64 channels x 4 points: acc[4][2] = 128 registers, and the output transform is in-lane.
+//   * Stages: each 16-channel chunk is two stages, points {0, 1} then {2, 3}; a stage holds V for its
+//     2 points over the 18 halo rows (hi + lo, 36 KB) and the 6-tap (2 points x 3 dy) weight image (24 KB);
+//     two stages (120 KB) double-buffered with one barrier per stage, exactly the staging pipeline of
+//     conv3x3_db_kernel (registers hold stage s + 2 while stage s + 1 is written under stage s's MFMAs).
+//     A stage item is (halo row, pair, 8-channel half): 3 input positions -> 2 V values per channel.
+//   * XTRA (the fused 1x1 shortcut, :126, :137): the centre-tap-only kernel transforms to U1 = w / 2,
+//     U2 = -w / 2, so each 16-channel chunk of the raw block input is one more stage with V1 = x(2j) +
+//     x(2j + 1), V2 = x(2j + 1) - x(2j) on the 16 inner rows (2 k-steps into acc[1], acc[2]).
+//   * Epilogue: output transform, fp32 stores (non-temporal), per-channel sums for the next
+//     InstanceNorm (fp32 over each lane's 32-value runs, fp64 beyond), as conv3x3_db_kernel.
+constexpr int kWinoRows = 18;                             // halo rows of a 16-row tile
+constexpr int kWinoVPlane = 2 * kWinoRows * 16 * 32;      // 2 points x 18 rows x 16 pairs x 16 ch bf16
+constexpr int kWinoWPlane = 6 * 64 * 32;                  // 6 taps (2 points x 3 dy) x 64 co x 16 ci bf16
+constexpr int kWinoXPlane = 2 * 64 * 32;                  // shortcut stage: 2 taps (points 1, 2)
+constexpr int kWinoStage = 2 * kWinoVPlane + 2 * kWinoWPlane;
+constexpr int kWinoWImg = kWinoWPlane;                    // uint16 per main-stage weight image (hi + lo)
+constexpr int kWinoXImg = kWinoXPlane;                    // uint16 per shortcut-stage image (hi + lo)
+// raw input of halo rows 16, 17 (fp32 [2][34][16] = 4352 B), one buffer per chunk parity; each LDS-DMA
+// wave-instruction writes a whole 1 KiB, so a buffer spans the 5 pieces (5 KiB) -- the last piece's
+// surplus lanes must not land in the other chunk's rows
+constexpr int kWinoRawRows = 5 * 1024;
+static_assert(kWinoWImg == kWinoMainImg && kWinoXImg == kWinoShortImg, "host packing (sesa_tapgemm.hpp)");
+
+// FRDB: fragment registers double-buffered across k-steps (the next k-step's LDS reads issued before
+// this one's MFMAs); else read just before use (24 registers fewer).
+// ABL (ablation knob for tools/conv_bench.hip; the product uses 0): 1 = no V split / LDS writes,
+// 2 = no weight DMA, 3 = no staging at all (MFMAs, fragment reads and barriers only), 4 = no halo rows
+// 16, 17 (wave 0's second items).
+// SLC: the staging of the next stage sliced between the k-steps (else all of it after k-step 1).
+template <bool X3, bool XTRA, int EPI = 0, bool FRDB = false, int ABL = 0, bool SLC = false>
+__global__ void __launch_bounds__(512, 1) conv3x3_wino_kernel(ConvArgs a) {
+  constexpr int NT = 512, TM = 16, BN = 64, NI = 2;
+  // two stages, then the raw input of halo rows 16, 17 for two chunks ([2 rows][34 positions][16 ch] fp32)
+  __shared__ __attribute__((aligned(16))) char smem[2 * kWinoStage + 2 * kWinoRawRows];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wm = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+
+  // XCD-aware block order, as conv3x3_db_kernel: the NB channel blocks of a tile run together
+  const int tiles_f = a.F_out / kTF;
+  const int NB = (a.n_cols + BN - 1) / BN;
+  const int n_tiles = ((a.T_out + TM - 1) / TM) * tiles_f;
+  int tile, nb;
+  {
+    const int id = blockIdx.x;
+    const int full = (n_tiles / 8) * 8 * NB;
+    if (id < full) {
+      const int g = id / (8 * NB), r = id - g * 8 * NB;
+      tile = g * 8 + (r & 7);
+      nb = r >> 3;
+    } else {
+      const int r = id - full;
+      tile = (n_tiles / 8) * 8 + r / NB;
+      nb = r % NB;
+    }
+  }
+  const int t0 = (tile / tiles_f) * TM;
+  const int f0 = (tile % tiles_f) * kTF;
+  const int b = blockIdx.z;
+  const int n_main = a.n_chunks;
+  const int n_x = XTRA ? a.x_chunks : 0;
+  const int n_stage = 2 * n_main + n_x;
+  const uint16_t* wblk = a.w + (int64_t)nb * ((int64_t)n_main * 2 * kWinoWImg + (int64_t)n_x * kWinoXImg);
+  const float* X = a.in.src[0].ptr;
+  const int C = a.in.C_in;
+  // shortcut sources as plain values (a select between fields of the kernel-argument struct can become a
+  // select of their addresses, which puts the whole struct in scratch and every derived load on flat)
+  const float* const xs_p0 = a.xin.src[0].ptr;
+  const float* const xs_p1 = a.xin.src[1].ptr;
+  const int xs_c0 = a.xin.src[0].C, xs_c1 = a.xin.src[1].C, xs_split = a.xin.C_split;
+
+  f32x16 acc[4][NI];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[p][j][r] = 0.f;
+
+  // ---- staging: registers hold the next stage's inputs (3 positions x 8 channels per item, halo rows
+  // 0..15); the 64 items of halo rows 16, 17 are wave 0's second items, staged from a raw copy of those
+  // two rows that wave 0 brings into LDS by DMA one chunk ahead (registers for a second item would
+  // spill; spreading those items over all waves as one channel per lane measured slower) ----
+  f32x4 areg[1][6];
+  uint32_t aval = 0;  // bit 3 * item + position: inside the input image (else zero)
+  // weight images go global -> LDS by LDS-DMA (buffer resource over this block's images, 32-bit offsets;
+  // the packed image is the LDS image, 1 KiB per wave-instruction: 3 pieces per wave for a main stage,
+  // 1 for a shortcut stage)
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(wblk), (short)0, (int)(((int64_t)n_main * 2 * kWinoWImg + (int64_t)n_x * kWinoXImg) * 2),
+      0x00020000);
+  auto dma_w = [&](char* stg, int s) __attribute__((always_inline)) {
+    char* wdst = stg + 2 * kWinoVPlane;
+    if (!XTRA || s < 2 * n_main) {
+      const uint32_t base = (uint32_t)(s * kWinoWImg * 2);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int pc = wm + 8 * i;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(wdst + pc * 1024), 16,
+                                                 base + pc * 1024 + lane * 16, 0, 0, 0);
+      }
+    } else {
+      const uint32_t base = (uint32_t)((2 * n_main * kWinoWImg + (s - 2 * n_main) * kWinoXImg) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(wdst + wm * 1024), 16,
+                                               base + wm * 1024 + lane * 16, 0, 0, 0);
+    }
+  };
+  auto item_geom = [&](int it, int& hr, int& pair, int& hh) __attribute__((always_inline)) {
+    const int e = it ? NT + (tid & 63) : tid;
+    hr = e >> 5;
+    pair = (e >> 1) & 15;
+    hh = e & 1;
+  };
+  auto load_stage = [&](int s) __attribute__((always_inline)) {
+    if (!XTRA || s < 2 * n_main) {
+      const int kc = s >> 1, pp = s & 1;
+      aval = 0;
+      Unroll<0, 1>::run([&](auto IT) {
+        constexpr int it = decltype(IT)::value;
+        int hr, pair, hh;
+        item_geom(it, hr, pair, hh);
+        const int ti = t0 - 1 + hr;
+        const int tc = min(max(ti, 0), a.T_in - 1);
+        Unroll<0, 3>::run([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          const int fi = f0 + 2 * pair - 1 + pp + q;
+          const bool ok = ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in;
+          const int fc = min(max(fi, 0), a.F_in - 1);
+          const f32x4* xp =
+              reinterpret_cast<const f32x4*>(X + (((int64_t)b * a.T_in + tc) * a.F_in + fc) * C + kc * kConvBK + 8 * hh);
+          areg[it][2 * q] = xp[0];
+          areg[it][2 * q + 1] = xp[1];
+          aval |= (uint32_t)ok << (3 * it + q);
+        });
+      });
+    } else {
+      const int kx = s - 2 * n_main;
+      const int k0 = kx * kConvBK;
+      const bool s1 = k0 >= xs_split;
+      const float* xp0 = s1 ? xs_p1 : xs_p0;
+      const int xc = s1 ? xs_c1 : xs_c0;
+      const int cl0 = k0 - (s1 ? xs_split : 0);
+      const int r = tid >> 5, pair = (tid >> 1) & 15, hh = tid & 1;
+      const int ti = t0 + r;
+      const int tc = min(ti, a.T_in - 1);
+      aval = 0;
+      Unroll<0, 2>::run([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const int fi = f0 + 2 * pair + q;
+        const f32x4* xp = reinterpret_cast<const f32x4*>(xp0 + (((int64_t)b * a.T_in + tc) * a.F_in + fi) * xc + cl0 + 8 * hh);
+        areg[0][2 * q] = xp[0];
+        areg[0][2 * q + 1] = xp[1];
+        aval |= (uint32_t)(ti < a.T_in) << q;
+      });
+    }
+  };
+  // V byte offset of (point slot pl, halo row hr, pair, channel half hh) within a plane
+  auto v_off = [](int pl, int hr, int pair, int hh) __attribute__((always_inline)) {
+    return ((pl * kWinoRows + hr) * 16 + pair) * 32 + ((hh ^ ((pair >> 3) & 1)) << 4);
+  };
+  auto put8 = [&](char* stg, int off, const float (&v)[8]) __attribute__((always_inline)) {
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __bf16 h0, l0, h1, l1;
+      split_bf16(v[2 * q], h0, l0);
+      split_bf16(v[2 * q + 1], h1, l1);
+      hw[q] = pack2(h0, h1);
+      lw[q] = pack2(l0, l1);
+    }
+    *reinterpret_cast<u32x4*>(stg + off) = u32x4{hw[0], hw[1], hw[2], hw[3]};
+    if (X3) *reinterpret_cast<u32x4*>(stg + kWinoVPlane + off) = u32x4{lw[0], lw[1], lw[2], lw[3]};
+  };
+  // V values of one staging item of stage s: it 0 = this thread's item (registers), it 1 = wave 0's item
+  // of halo rows 16, 17 (the LDS raw rows); returns the two V slots' LDS offsets
+  auto v_item = [&](auto IT, int s, float (&va)[8], float (&vb)[8], int& o0, int& o1) __attribute__((always_inline)) {
+    constexpr int it = decltype(IT)::value;
+    if (XTRA && s >= 2 * n_main) {  // shortcut stage: V1 = x(2j) + x(2j + 1), V2 = x(2j + 1) - x(2j)
+      const int r = tid >> 5, pair = (tid >> 1) & 15, hh = tid & 1;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float e0 = (aval & 1u) ? areg[0][c >> 2][c & 3] : 0.f;
+        const float e1 = ((aval >> 1) & 1u) ? areg[0][2 + (c >> 2)][c & 3] : 0.f;
+        va[c] = e0 + e1;
+        vb[c] = e1 - e0;
+      }
+      o0 = v_off(0, r + 1, pair, hh);
+      o1 = v_off(1, r + 1, pair, hh);
+      return;
+    }
+    const int pp = s & 1;
+    int hr, pair, hh;
+    item_geom(it, hr, pair, hh);
+    f32x4 xq[6];
+    uint32_t okb;
+    if constexpr (it == 0) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) xq[i] = areg[0][i];
+      okb = aval;
+    } else {
+      // halo rows 16, 17 from the raw rows wave 0 copied for this chunk
+      const char* raw = smem + 2 * kWinoStage + ((s >> 1) & 1) * kWinoRawRows;
+      const int ti = t0 - 1 + hr;
+      okb = 0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int pos = 2 * pair + pp + q;  // relative to f0 - 1
+        const int fi = f0 - 1 + pos;
+        const f32x4* rp = reinterpret_cast<const f32x4*>(raw + (((hr - 16) * 34 + pos) * 16 + 8 * hh) * 4);
+        xq[2 * q] = rp[0];
+        xq[2 * q + 1] = rp[1];
+        okb |= (uint32_t)(ti < a.T_in && fi >= 0 && fi < a.F_in) << q;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float q0 = (okb >> 0) & 1u ? xq[c >> 2][c & 3] : 0.f;
+      const float q1 = (okb >> 1) & 1u ? xq[2 + (c >> 2)][c & 3] : 0.f;
+      const float q2 = (okb >> 2) & 1u ? xq[4 + (c >> 2)][c & 3] : 0.f;
+      // pp 0: (q0, q1, q2) = (d0, d1, d2) -> V0 = d0 - d2, V1 = d1 + d2
+      // pp 1: (q0, q1, q2) = (d1, d2, d3) -> V2 = d2 - d1, V3 = d1 - d3
+      va[c] = pp ? q1 - q0 : q0 - q2;
+      vb[c] = pp ? q0 - q2 : q1 + q2;
+    }
+    o0 = v_off(0, hr, pair, hh);
+    o1 = v_off(1, hr, pair, hh);
+  };
+  auto store_stage = [&](char* stg, int s) __attribute__((always_inline)) {
+    float va[8], vb[8];
+    int o0, o1;
+    v_item(std::integral_constant<int, 0>{}, s, va, vb, o0, o1);
+    put8(stg, o0, va);
+    put8(stg, o1, vb);
+    if (wm == 0 && (!XTRA || s < 2 * n_main)) {
+      v_item(std::integral_constant<int, 1>{}, s, va, vb, o0, o1);
+      put8(stg, o0, va);
+      put8(stg, o1, vb);
+    }
+  };
+
+  struct Frags {
+    bf16x8 ah, al, bh[NI], bl[NI];
+  };
+  // k-step (point slot pl, dy) of a stage: A = V_pl at halo row 2 wm + (m >> 4) + dy, B = weight tap
+  auto read_frags = [&](Frags& fr, const char* stg, int pl, int dy, int tap, int wplane) __attribute__((always_inline)) {
+    const int pair = l32 & 15;
+    const int off = v_off(pl, 2 * wm + (l32 >> 4) + dy, pair, h);
+    fr.ah = *reinterpret_cast<const bf16x8*>(stg + off);
+    if (X3) fr.al = *reinterpret_cast<const bf16x8*>(stg + kWinoVPlane + off);
+    const char* W = stg + 2 * kWinoVPlane;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int p = tap * BN + j * 32 + l32;
+      const int o = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+      fr.bh[j] = *reinterpret_cast<const bf16x8*>(W + o);
+      if (X3) fr.bl[j] = *reinterpret_cast<const bf16x8*>(W + wplane + o);
+    }
+  };
+  auto mfmas = [&](const Frags& fr, auto P) __attribute__((always_inline)) {
+    constexpr int p = decltype(P)::value;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      if (X3) {
+        acc[p][j] = mfma32(fr.al, fr.bh[j], acc[p][j]);
+        acc[p][j] = mfma32(fr.ah, fr.bl[j], acc[p][j]);
+      }
+      acc[p][j] = mfma32(fr.ah, fr.bh[j], acc[p][j]);
+    }
+  };
+
+  // wave 0: the raw input of halo rows 16, 17 (t0 + 15, t0 + 16) of chunk kc into its LDS copy
+  // ([row][34 positions from f0 - 1][16 ch], lane-linear 16-B pieces; clamped addresses, the
+  // out-of-image positions are masked when staged)
+  auto dma_rows = [&](int kc) __attribute__((always_inline)) {
+    char* raw = smem + 2 * kWinoStage + (kc & 1) * kWinoRawRows;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(X) + (int64_t)b * a.T_in * a.F_in * C, (short)0,
+        (int)((int64_t)a.T_in * a.F_in * C * 4), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int e = min(lane + 64 * i, 2 * 34 * 4 - 1);
+      const int r = e / 136, rem = e - r * 136, pos = rem >> 2, c4 = rem & 3;
+      const int tc = min(t0 + 15 + r, a.T_in - 1);
+      const int fc = min(max(f0 - 1 + pos, 0), a.F_in - 1);
+      const uint32_t voff = (uint32_t)((((int64_t)tc * a.F_in + fc) * C + kc * kConvBK + 4 * c4) * 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(raw + i * 1024), 16,
+                                               voff, 0, 0, 0);
+    }
+  };
+  // Wait for this wave's DMAs (weights of the next stage, wave 0's raw rows) while the raw loads issued
+  // after them (for the stage after that) stay in flight: vmcnt counts in issue order, and the memory
+  // clobbers keep the DMAs ahead of those loads.  Raw loads per stage: 6 (main), 4 (shortcut).
+  auto wait_dma = [&](int s_loaded) __attribute__((always_inline)) {
+    if (XTRA && s_loaded >= 2 * n_main) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  };
+  // Producing stage s + 1 into `nxt` while stage s's MFMAs run, in slices pinned between the k-steps
+  // (sched_barrier) so the two waves of a SIMD do not both stall their MFMA stream on one clump of VALU:
+  //   k 0: weight DMA (+ wave 0's raw rows of a new chunk)   k 1: V of this thread's item, then the raw
+  //   loads of stage s + 2 (registers free again: the longest lead)   k 2 / k 3: split + LDS writes of
+  //   the two V slots   k 4: wave 0's item of halo rows 16, 17.
+  struct Prod {
+    int s1, s2;
+    float va[8], vb[8];
+    int o0, o1;
+  };
+  auto slice = [&](auto K, Prod& pr, char* nxt, int s) __attribute__((always_inline)) {
+    constexpr int k = decltype(K)::value;
+    if constexpr (ABL == 3) {
+      if constexpr (k == 0) pr.s1 = pr.s2 = 2 * n_main + n_x;  // (wait_dma: vmcnt(6) / (4) still harmless)
+      return;
+    }
+    if constexpr (ABL == 1 && k >= 2) return;
+    if constexpr (ABL == 4 && k == 4) return;
+    if constexpr (ABL == 2 && k == 0) {
+      pr.s1 = min(s + 1, n_stage - 1);
+      pr.s2 = min(s + 2, n_stage - 1);
+      return;
+    }
+    if constexpr (k == 0) {
+      pr.s1 = min(s + 1, n_stage - 1);
+      pr.s2 = min(s + 2, n_stage - 1);
+      // a new chunk's first stage: its rows 16, 17 (read from the next iteration on; that copy last
+      // served chunk kc - 2)
+      if (wm == 0 && pr.s2 < 2 * n_main && (pr.s2 & 1) == 0 && pr.s2 > s) dma_rows(pr.s2 >> 1);
+      dma_w(nxt, pr.s1);
+      asm volatile("" ::: "memory");
+    } else if constexpr (k == 1) {
+      v_item(std::integral_constant<int, 0>{}, pr.s1, pr.va, pr.vb, pr.o0, pr.o1);
+      load_stage(pr.s2);
+    } else if constexpr (k == 2) {
+      put8(nxt, pr.o0, pr.va);
+    } else if constexpr (k == 3) {
+      put8(nxt, pr.o1, pr.vb);
+    } else if constexpr (k == 4) {
+      if (wm == 0 && (!XTRA || pr.s1 < 2 * n_main)) {
+        float va[8], vb[8];
+        int o0, o1;
+        v_item(std::integral_constant<int, 1>{}, pr.s1, va, vb, o0, o1);
+        put8(nxt, o0, va);
+        put8(nxt, o1, vb);
+      }
+    }
+  };
+
+  if (wm == 0) {
+    dma_rows(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  load_stage(0);
+  store_stage(smem, 0);
+  dma_w(smem, 0);
+  asm volatile("" ::: "memory");
+  load_stage(min(1, n_stage - 1));
+  wait_dma(min(1, n_stage - 1));
+  __syncthreads();
+  for (int kc = 0; kc < n_main; ++kc) {
+    Unroll<0, 2>::run([&](auto PP) {
+      constexpr int pp = decltype(PP)::value;
+      const int s = 2 * kc + pp;
+      char* cur = smem + pp * kWinoStage;
+      char* nxt = smem + (1 - pp) * kWinoStage;
+      Prod pr;
+      Frags fr[FRDB ? 2 : 1];
+      if constexpr (FRDB) read_frags(fr[0], cur, 0, 0, 0, kWinoWPlane);
+      Unroll<0, 6>::run([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        if constexpr (FRDB) {
+          if constexpr (k + 1 < 6)
+            read_frags(fr[(k + 1) & 1], cur, (k + 1) / 3, (k + 1) % 3, k + 1, kWinoWPlane);
+          mfmas(fr[k & 1], std::integral_constant<int, 2 * pp + k / 3>{});
+        } else {
+          read_frags(fr[0], cur, k / 3, k % 3, k, kWinoWPlane);
+          mfmas(fr[0], std::integral_constant<int, 2 * pp + k / 3>{});
+        }
+        if constexpr (SLC) {
+          __builtin_amdgcn_sched_barrier(0);
+          slice(K, pr, nxt, s);
+          __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (k == 1) {
+          Unroll<0, 5>::run([&](auto J) { slice(J, pr, nxt, s); });
+        }
+      });
+      wait_dma(pr.s2);
+      __syncthreads();
+    });
+  }
+  if constexpr (XTRA) {
+    for (int kx = 0; kx < n_x; ++kx) {
+      const int s = 2 * n_main + kx;
+      char* cur = smem + (kx & 1) * kWinoStage;
+      char* nxt = smem + ((kx + 1) & 1) * kWinoStage;
+      Prod pr;
+      Frags fr[2];
+      read_frags(fr[0], cur, 0, 1, 0, kWinoXPlane);
+      read_frags(fr[1], cur, 1, 1, 1, kWinoXPlane);
+      mfmas(fr[0], std::integral_constant<int, 1>{});
+      slice(std::integral_constant<int, 0>{}, pr, nxt, s);
+      slice(std::integral_constant<int, 1>{}, pr, nxt, s);
+      mfmas(fr[1], std::integral_constant<int, 2>{});
+      slice(std::integral_constant<int, 2>{}, pr, nxt, s);
+      slice(std::integral_constant<int, 3>{}, pr, nxt, s);
+      wait_dma(pr.s2);
+      __syncthreads();
+    }
+  }
+
+  if constexpr (EPI == 2) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[p][j]));
+    return;
+  }
+  // ---- epilogue: output transform, fp32 stores, per-channel statistics ----
+  double ssum[NI], ssq[NI];
+  const int C_out = a.out.C_out;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    ssum[j] = 0.0;
+    ssq[j] = 0.0;
+    const int co = nb * BN + j * 32 + l32;
+    if (co >= C_out) continue;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {  // r in [8 hb, 8 hb + 8): output row 2 wm + hb
+      const int t = t0 + 2 * wm + hb;
+      if (t >= a.T_out) continue;
+      float ps = 0.f, pq = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int r = 8 * hb + rr;
+        const int pair = ((r & 3) + 8 * (r >> 2) + 4 * h) & 15;
+        const float m0 = acc[0][j][r], m1 = acc[1][j][r], m2 = acc[2][j][r], m3 = acc[3][j][r];
+        const float ye = m0 + m1 + m2;
+        const float yo = m1 - m2 - m3;
+        const int64_t idx = (((int64_t)b * a.T_out + t) * a.F_out + f0 + 2 * pair) * C_out + co;
+        __builtin_nontemporal_store(ye, a.out.ptr + idx);
+        __builtin_nontemporal_store(yo, a.out.ptr + idx + C_out);
+        ps += ye + yo;
+        pq = fmaf(ye, ye, fmaf(yo, yo, pq));
+      }
+      ssum[j] += (double)ps;
+      ssq[j] += (double)pq;
+    }
+  }
+  if (EPI == 0 && a.out.stats) {
+    double* red = reinterpret_cast<double*>(smem);  // [8 waves][BN][2] (the last barrier retired all LDS reads)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      ssum[j] += __shfl_xor(ssum[j], 32);
+      ssq[j] += __shfl_xor(ssq[j], 32);
+      if (h == 0) {
+        const int n = j * 32 + l32;
+        red[(wm * BN + n) * 2 + 0] = ssum[j];
+        red[(wm * BN + n) * 2 + 1] = ssq[j];
+      }
+    }
+    __syncthreads();
+    for (int n = tid; n < BN; n += NT) {
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        s0 += red[(w * BN + n) * 2 + 0];
+        s1 += red[(w * BN + n) * 2 + 1];
+      }
+      const int co = nb * BN + n;
+      if (co < C_out) {
+        double* st = a.out.stats + ((int64_t)b * C_out + co) * 2;
+        atomicAdd(st + 0, s0);
+        atomicAdd(st + 1, s1);
+      }
+    }
+  }
+}
+
 // Sum of a double over the 16 lanes of each DPP row (every lane of the row gets the sum): xor 1 and
 // xor 2 by quad_perm, then row_half_mirror (i <-> 7 - i) and row_mirror (i <-> 15 - i), each applied to
 // both 32-bit halves.
@@ -1924,6 +2416,9 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
 constexpr int kActUnroll = 4;
 // rhi / rlo (nullable): the raw (untransformed) input split to bf16 planes as well -- the fused 1x1
 // shortcut operand of conv3x3_m16_kernel, written while the input is in registers anyway.
+// F32OUT: the activation itself as fp32 (hi = the fp32 output, lo / rhi / rlo unused) -- the SRC_ACT32 input of
+// conv3x3_wino_kernel, whose Winograd input transform needs the unsplit value.
+template <bool F32OUT>
 __global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t n_pos, int pos_per_block,
                                                              uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
                                                              uint16_t* __restrict__ rhi, uint16_t* __restrict__ rlo) {
@@ -1972,6 +2467,15 @@ __global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t 
                     f32x2{x[u][1][2], x[u][1][3]}};
       uint32_t hw[4], lw[4];
       const int64_t o = obase + p * C;
+      if constexpr (F32OUT) {
+        f32x2 y[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] = act ? gelu_erf2(__builtin_elementwise_fma(v[q], sc[q], sh[q])) : v[q];
+        f32x4* op = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(hi) + o);
+        __builtin_nontemporal_store(f32x4{y[0][0], y[0][1], y[1][0], y[1][1]}, op);
+        __builtin_nontemporal_store(f32x4{y[2][0], y[2][1], y[3][0], y[3][1]}, op + 1);
+        continue;
+      }
       if (rhi) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -2072,6 +2576,35 @@ bool conv3x3_fused_act_ok(int T_out, int C_in, int C_out) {
          (mode == 2 || C_out <= 128);
 }
 
+// Winograd F(2, 3) TFC convs (conv3x3_wino_kernel), opt-in: measured on MI355X at parity with the direct
+// kernel end to end (profiles/r03_wino_*): its main loop alone runs 1.6x the direct
+// kernel's effective rate, but staging V (bf16 split + LDS writes, 2 V values per input element) and the
+// shortcut stages give it back.  SESA_CONV_WINO / sesa_mdx23c_set_wino: 0 (default) never; 1 = T_out in
+// [32, 128] (levels 1-3, whose inputs pass through act_split anyway); all / 2 = every T >= 32 level (level
+// 0 then trades its fused activation for an act_split fp32 pass).  Read when a model is finalized.
+std::atomic<int> g_wino_mode{-1};
+int wino_mode() {
+  int v = g_wino_mode.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("SESA_CONV_WINO");
+    v = !e ? 0 : std::string(e) == "all" || std::string(e) == "2" ? 2 : std::string(e) == "1" ? 1 : 0;
+    int expect = -1;
+    g_wino_mode.compare_exchange_strong(expect, v);
+    v = g_wino_mode.load(std::memory_order_relaxed);
+  }
+  return v;
+}
+int set_conv3x3_wino(int mode) {
+  const int prev = wino_mode();
+  g_wino_mode.store(mode >= 0 && mode <= 2 ? mode : 0);
+  return prev;
+}
+bool conv3x3_wino_selected(int T_out, int C_in, int C_out) {
+  const int mode = wino_mode();
+  return mode > 0 && conv_variant() == 0 && T_out >= 32 && (mode == 2 || T_out <= 128) && C_in % kConvBK == 0 &&
+         C_in <= kMaxCin && C_out % 16 == 0;
+}
+
 bool conv3x3_m16_selected(int T_out, int C_in, int C_out, int C_shortcut) {
   return conv_variant() == 1 && T_out >= 32 && C_in % 32 == 0 && C_out % 16 == 0 && C_shortcut % 32 == 0;
 }
@@ -2084,6 +2617,30 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
                kMaxCin);
   switch (kind) {
     case CONV3X3:
+      if (a.in.src[0].mode == SRC_ACT32) {
+        SESA_REQUIRE(a.in.src[0].ptr && a.in.C_split == a.in.C_in && a.in.src[0].C == a.in.C_in &&
+                         a.out.residual == nullptr && a.out.gelu == 0 && a.T_in == a.T_out && a.F_in == a.F_out &&
+                         a.n_chunks * kConvBK == a.in.C_in && a.out.C_out % 16 == 0,
+                     SESA_ERR_INVALID, "conv3x3 (Winograd): needs one pre-activated fp32 input, same-size conv");
+        if (a.x_chunks > 0)
+          SESA_REQUIRE(a.xin.C_in % kConvBK == 0 && a.xin.C_split % kConvBK == 0 && a.x_chunks * kConvBK == a.xin.C_in &&
+                           a.xin.src[0].mode == SRC_RAW && a.xin.src[1].mode == SRC_RAW && a.xin.src[0].C % 8 == 0 &&
+                           a.xin.src[1].C % 8 == 0,
+                       SESA_ERR_INVALID, "conv3x3 (Winograd): fused shortcut must be a raw input, C_in multiple of %d",
+                       kConvBK);
+        const int64_t nblk = (int64_t)((a.T_out + 15) / 16) * (a.F_out / kTF) * ((a.n_cols + 63) / 64);
+        SESA_REQUIRE(nblk < (1ll << 31) && batch < 65536, SESA_ERR_INVALID, "conv3x3 (Winograd): grid too large");
+        dim3 grid((unsigned)nblk, 1u, (unsigned)batch);
+        if (a.x_chunks > 0) {
+          if (x3) hipLaunchKernelGGL((conv3x3_wino_kernel<true, true>), grid, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv3x3_wino_kernel<false, true>), grid, dim3(512), 0, st, a);
+        } else {
+          if (x3) hipLaunchKernelGGL((conv3x3_wino_kernel<true, false>), grid, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv3x3_wino_kernel<false, false>), grid, dim3(512), 0, st, a);
+        }
+        SESA_CHECK_LAUNCH();
+        return SESA_OK;
+      }
       if (a.out.residual == nullptr && a.out.gelu == 0 &&
           conv3x3_m16_selected(a.T_out, a.in.C_in, a.out.C_out, a.x_chunks > 0 ? a.xin.C_in : 0)) {
         SESA_REQUIRE(a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && a.in.src[0].lo && a.in.C_split == a.in.C_in,
@@ -2201,8 +2758,21 @@ int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, u
   const int lanes_pos = groups >= kThreads ? 1 : kThreads / groups;
   const int ppb = lanes_pos * 32;
   dim3 grid((unsigned)((n_pos + ppb - 1) / ppb), (unsigned)batch);
-  hipLaunchKernelGGL(act_split_kernel, grid, dim3((unsigned)(groups * lanes_pos)), 0, st, in, n_pos, ppb, hi, lo,
-                     raw_hi, raw_lo);
+  hipLaunchKernelGGL(act_split_kernel<false>, grid, dim3((unsigned)(groups * lanes_pos)), 0, st, in, n_pos, ppb, hi,
+                     lo, raw_hi, raw_lo);
+  SESA_CHECK_LAUNCH();
+  return SESA_OK;
+}
+
+int launch_act_f32(const GemmIn& in, int64_t n_pos, int batch, float* out, hipStream_t st) {
+  SESA_REQUIRE(in.C_in % 16 == 0 && in.C_split % 8 == 0 && in.C_in <= kMaxCin, SESA_ERR_INVALID,
+               "act_f32: C %d must be a multiple of 16 (<= %d)", in.C_in, kMaxCin);
+  const int groups = in.C_in / 8;
+  const int lanes_pos = groups >= kThreads ? 1 : kThreads / groups;
+  const int ppb = lanes_pos * 32;
+  dim3 grid((unsigned)((n_pos + ppb - 1) / ppb), (unsigned)batch);
+  hipLaunchKernelGGL(act_split_kernel<true>, grid, dim3((unsigned)(groups * lanes_pos)), 0, st, in, n_pos, ppb,
+                     reinterpret_cast<uint16_t*>(out), nullptr, nullptr, nullptr);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }

@@ -10,6 +10,7 @@ enum SrcMode : int {
   SRC_NORM_GELU = 1,  // GELU(InstanceNorm_affine(x))   (get_norm + get_act, mdx23c_tfc_tdf_v3.py:47-71)
   SRC_MUL = 2,        // x * mul                         (x * first_conv_out, :230)
   SRC_PRE = 3,        // pre-activated: bf16 hi/lo planes written by act_split (GELU(IN(x)) already applied)
+  SRC_ACT32 = 4,      // pre-activated fp32 (launch_act_f32): the input of the Winograd 3x3 kernel
 };
 
 // One input source of a (possibly channel-concatenated) NHWC fp32 activation
@@ -71,6 +72,16 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
 // channel-concatenated) input `in` of n_pos positions per batch item.
 int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, uint16_t* lo, hipStream_t st,
                      uint16_t* raw_hi = nullptr, uint16_t* raw_lo = nullptr);
+// act_f32: out[b][pos][c] = GELU(IN_affine(x)) as fp32 (the SRC_ACT32 input of the Winograd conv).
+int launch_act_f32(const GemmIn& in, int64_t n_pos, int batch, float* out, hipStream_t st);
+// True when a same-size TFC 3x3 conv at T_out runs as Winograd F(2, 3) (conv3x3_wino_kernel): its weights
+// are then packed by pack_conv_wino (sesa_mdx23c.hip) and its input is given as SRC_ACT32.
+bool conv3x3_wino_selected(int T_out, int C_in, int C_out);
+int set_conv3x3_wino(int mode);  // 0 off, 1 levels 1-3, 2 every T >= 32 level; returns the previous
+// Winograd weight images (uint16 per stage): main stage = 2 points x 3 dy x 64 co x 16 ci, hi + lo;
+// shortcut stage = 2 points x 64 x 16, hi + lo.
+constexpr int kWinoMainImg = 2 * 6 * 64 * 16;
+constexpr int kWinoShortImg = 2 * 2 * 64 * 16;
 // True when launch_conv runs a 3x3 same-size conv on conv3x3_m16_kernel, whose fused 1x1 shortcut
 // (C_shortcut > 0) must then be given as act_split raw planes (SRC_PRE) instead of a raw fp32 input.
 bool conv3x3_m16_selected(int T_out, int C_in, int C_out, int C_shortcut);

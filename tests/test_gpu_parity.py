@@ -255,6 +255,32 @@ def test_instancenorm_stress_large_offsets(dev, golden):
     assert err <= RMS_GATE
 
 
+@pytest.mark.parametrize("fixture,cfg_name,affine,mode", [
+    ("mdx23c_small.npz", "config_mdx23c_small.yaml", None, 2),
+    ("mdx23c_small_stress.npz", "config_mdx23c_small.yaml", "stress", 2),
+    ("mdx23c_full_chunk.npz", "config_vocals_mdx23c.yaml", "unit", 1),
+    ("mdx23c_full_chunk.npz", "config_vocals_mdx23c.yaml", "unit", 2)])
+def test_conv3x3_wino_matches_reference(golden, dev, fixture, cfg_name, affine, mode):
+    """The opt-in Winograd F(2, 3) TFC convs (conv3x3_wino_kernel; sesa_mdx23c_set_wino(mode), 1 = levels
+    with 32 <= T <= 128, 2 = every T >= 32 level incl. the fused 1x1 shortcut stages) against the same
+    reference goldens as the direct kernel.  The mode is read when the model is finalized, so the model
+    is created under it."""
+    from sesa import _native
+    g = golden(fixture)
+    prev = _native.lib().sesa_mdx23c_set_wino(mode)
+    try:
+        m, _ = _model(cfg_name, affine or str(g["affine"]))
+        y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    finally:
+        _native.lib().sesa_mdx23c_set_wino(prev)
+    err = rms(y, g["y"])
+    print(f"{fixture} (Winograd mode {mode}): rms={err:.3e}")
+    assert err <= RMS_GATE
+    m0, _ = _model(cfg_name, affine or str(g["affine"]))             # direct kernels, same weights
+    y0 = m0(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    assert rms(y0, y) <= 1e-5                                         # fp32 rounding / summation order only
+
+
 @pytest.mark.parametrize("fixture,cfg_name,affine", [("mdx23c_small.npz", "config_mdx23c_small.yaml", None),
                                                      ("mdx23c_small_stress.npz", "config_mdx23c_small.yaml", "stress"),
                                                      ("mdx23c_full_chunk.npz", "config_vocals_mdx23c.yaml", "unit")])

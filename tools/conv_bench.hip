@@ -79,6 +79,84 @@ int main(int argc, char** argv) {
   printf("batch %d\n%-5s %-26s %9s %9s\n", B, "level", "variant", "ms", "TF/s(alg)");
   const bool only_tdf = argc > 2 && strcmp(argv[2], "tdf") == 0;  // ./tools/conv_bench 57 tdf
   const bool only_act = argc > 2 && strcmp(argv[2], "act") == 0;  // ./tools/conv_bench 57 act
+  const bool only_wino = argc > 2 && strcmp(argv[2], "wino") == 0;  // ./tools/conv_bench 57 wino
+  if (only_wino) {
+    // Winograd F(2, 3) conv3x3_wino_kernel (SRC_ACT32 input) vs the direct conv3x3_db_kernel (act_split
+    // planes) on the level shapes; random operands (timing only -- parity is tests/test_gpu_parity.py)
+    for (int lvl = 0; lvl < 4; ++lvl) {
+      const int C = 128 * (lvl + 1), T = 256 >> lvl, F = 1024 >> lvl;
+      const int64_t n_act = (int64_t)B * T * F * C;
+      float *x, *out;
+      uint16_t *hi, *lo, *w, *ww;
+      double* stats;
+      const int nblk = C / 64, nch = C / kConvBK;
+      const int64_t w_elems = (int64_t)nblk * nch * 2 * 9 * 64 * 16;
+      const int64_t ww_elems = (int64_t)nblk * (nch * 2 * kWinoMainImg + nch * kWinoShortImg);
+      CK(hipMalloc(&x, n_act * 4));
+      CK(hipMalloc(&hi, n_act * 2));
+      CK(hipMalloc(&lo, n_act * 2));
+      CK(hipMalloc(&w, w_elems * 2));
+      CK(hipMalloc(&ww, ww_elems * 2));
+      CK(hipMalloc(&out, n_act * 4));
+      CK(hipMalloc(&stats, (size_t)B * C * 2 * 8));
+      hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint16_t*>(x), n_act * 2, 4u, 1.f);
+      hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, hi, n_act, 1u, 1.f);
+      hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, lo, n_act, 2u, 1.f / 256);
+      hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, w, w_elems, 3u, 0.03f);
+      hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, ww, ww_elems, 5u, 0.03f);
+      CK(hipDeviceSynchronize());
+      ConvArgs a{};
+      a.in.src[0] = Src{nullptr, nullptr, nullptr, C, SRC_PRE, hi, lo};
+      a.in.src[1] = a.in.src[0];
+      a.in.C_split = a.in.C_in = C;
+      a.out.ptr = out;
+      a.out.stats = stats;
+      a.out.C_out = C;
+      a.w = w;
+      a.T_in = a.T_out = T;
+      a.F_in = a.F_out = F;
+      a.n_cols = C;
+      a.n_chunks = nch;
+      ConvArgs aw = a;
+      aw.in.src[0] = Src{x, nullptr, nullptr, C, SRC_ACT32, nullptr, nullptr};
+      aw.in.src[1] = aw.in.src[0];
+      aw.w = ww;
+      ConvArgs ax = aw;  // + fused 1x1 shortcut over a raw C-channel input
+      ax.xin.src[0] = Src{x, nullptr, nullptr, C, SRC_RAW, nullptr, nullptr};
+      ax.xin.src[1] = ax.xin.src[0];
+      ax.xin.C_split = ax.xin.C_in = C;
+      ax.x_chunks = nch;
+      ConvArgs adx = a;
+      adx.xin = ax.xin;
+      adx.x_chunks = nch;
+      const double flop = 2.0 * B * T * F * (double)C * C * 9;
+      const dim3 grid((unsigned)(((T + 15) / 16) * (F / kTF) * ((C + 63) / 64)), 1u, (unsigned)B);
+      auto rep = [&](const char* v, float ms) { printf("L%-4d %-26s %9.3f %9.1f\n", lvl, v, ms, flop / ms * 1e-9); };
+      rep("db", time_ms([&] { hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0>), grid, dim3(512), 0, 0, a); }));
+      rep("wino", time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, false, 0>), grid, dim3(512), 0, 0, aw); }));
+      rep("wino sliced staging", time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, false, 0, false, 0, true>), grid, dim3(512), 0, 0, aw); }));
+      rep("wino frdb", time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, false, 0, true>), grid, dim3(512), 0, 0, aw); }));
+      rep("wino abl1 no V writes", time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, false, 0, false, 1>), grid, dim3(512), 0, 0, aw); }));
+      rep("wino abl4 no rows 16/17", time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, false, 0, false, 4>), grid, dim3(512), 0, 0, aw); }));
+      rep("wino abl2 no W DMA", time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, false, 0, false, 2>), grid, dim3(512), 0, 0, aw); }));
+      rep("wino abl3 no staging", time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, false, 0, false, 3>), grid, dim3(512), 0, 0, aw); }));
+      rep("wino abl3 no stg/epi", time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, false, 2, false, 3>), grid, dim3(512), 0, 0, aw); }));
+      rep("db no epilogue", time_ms([&] { hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 2>), grid, dim3(512), 0, 0, a); }));
+      rep("wino no epilogue",
+          time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, false, 2>), grid, dim3(512), 0, 0, aw); }));
+      rep("db + shortcut", time_ms([&] { hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0>), grid, dim3(512), 0, 0, adx); }));
+      rep("wino + shortcut",
+          time_ms([&] { hipLaunchKernelGGL((conv3x3_wino_kernel<true, true, 0>), grid, dim3(512), 0, 0, ax); }));
+      CK(hipFree(x));
+      CK(hipFree(hi));
+      CK(hipFree(lo));
+      CK(hipFree(w));
+      CK(hipFree(ww));
+      CK(hipFree(out));
+      CK(hipFree(stats));
+    }
+    return 0;
+  }
   if (only_act) {
     // act_split + pre-activated conv3x3_db_kernel vs conv3x3_db_kernel<ACT> (norm + GELU + split fused
     // into the staging) on the level shapes; cat: two channel-concatenated sources (decoder tfc1)
