@@ -740,10 +740,11 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
     a.a_ld = ld;
     a.row_scale = RSC;
   };
-  // q / k / v / gate logits as bf16 planes written by the QKV epilogue (the attention then stages K / V
-  // by plain copies); SESA_BSR_QKV_PLANES=0 keeps the fp32 QKV buffer (A/B)
-  static const bool qkv_planes =
-      !(getenv("SESA_BSR_QKV_PLANES") && std::string(getenv("SESA_BSR_QKV_PLANES")) == "0");
+  // SESA_BSR_QKV_PLANES=1: q / k / v / gate logits as bf16 planes written by the QKV epilogue (the attention
+  // then stages K / V by plain copies).  Off by default: measured same-box on the vocals 4-min track, the
+  // fp32 QKV buffer is faster -- 115.3x vs 110.5x real-time, attention 356 vs 410 ms and token GEMMs 1597
+  // vs 1634 ms per step, twice each (profiles/r03_bsr_qkv_planes_ab_*.json).
+  static const bool qkv_planes = getenv("SESA_BSR_QKV_PLANES") && std::string(getenv("SESA_BSR_QKV_PLANES")) == "1";
   const bool qp = qkv_planes && m->qkv_ld % 8 == 0 && c.dim_head % 8 == 0;
   uint16_t* QKVhi = reinterpret_cast<uint16_t*>(QKV);
   uint16_t* QKVlo = x3 ? QKVhi + (int64_t)M * m->qkv_ld : nullptr;
