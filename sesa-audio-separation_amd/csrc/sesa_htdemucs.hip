@@ -49,6 +49,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <string>
@@ -1267,6 +1268,21 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     a.act = act;
     a.glu = glu;
     a.conv = 1;
+    {
+      // narrow convs on 64-column tiles: N <= 64 (a 128-column tile computes and runs the epilogue on 19-50 %
+      // useful columns) and N = 64 mod 128 (192, 320, ...: 75 % -> 100 %).  Same box, configs[3]:
+      // hconv 1240 -> 1123 ms per step (N <= 64 only) -> 1071 ms (both), 633x -> 660x -> 672x real-time,
+      // twice each (profiles/r03_htd_bn64_*.json).  SESA_HCONV_BN64=0: 128-column tiles; =1: N <= 64 only.
+      static const int bn64_mode = [] {
+        const char* e = getenv("SESA_HCONV_BN64");
+        return !e ? 2 : std::string(e) == "0" ? 0 : std::string(e) == "1" ? 1 : 2;
+      }();
+      const int N = gm.groups[0].N;
+      if (bn64_mode > 0 && (N <= 64 || (bn64_mode == 2 && N % 128 == 64))) {
+        a.bn64 = 1;
+        a.n_tiles_n = (N + 63) / 64;
+      }
+    }
     ConvGeo& g = a.geo;
     g.P1 = P1; g.P2 = P2; g.Q1 = Q1; g.Q2 = Q2; g.s1 = s1; g.s2 = 1;
     g.Cin = Cin;
@@ -1279,6 +1295,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     g.phases = phases;
     g.O1 = O1;
     g.opad = opad;
+    // SESA_HTD_TRACE=1: one stderr line per implicit-GEMM conv launch (shape survey for tuning)
+    static const bool trace = getenv("SESA_HTD_TRACE") && std::string(getenv("SESA_HTD_TRACE")) == "1";
+    if (trace)
+      fprintf(stderr, "[htd conv] M %d N %d K %d taps %d Cin %d phases %d glu %d act %d x2 %d\n", a.M,
+              gm.groups[0].N, gm.groups[0].K, g.n_taps, Cin, phases, glu, act, x2 != nullptr);
     void* t0 = profile_begin(st);
     rc = launch_tok_gemm(a, x3, st);
     profile_end(t0, st, SESA_KCLASS_HCONV, gemm_flops(gm, a.M));

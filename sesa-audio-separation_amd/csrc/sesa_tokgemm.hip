@@ -70,9 +70,12 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 // the next chunk's global loads in flight under the MFMAs.  DB = true (512 threads, 1 WG / CU):
 // two stages, one barrier per chunk.  The body is straight-line (clamped addresses, validity
 // applied at store time).
-template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB, bool CONV, bool PRE>
+// BN: output columns per tile, 128 (the packed weight row block) or 64 (one half of it, for the narrow
+// implicit-GEMM convs of HTDemucs: N = 24 / 32 / 48 / 64 fill a 128-column tile to 19-50 %).
+template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB, bool CONV, bool PRE, int BN = kTokBN>
 __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a) {
-  constexpr int BN = kTokBN, BK = kTokBK;
+  constexpr int BK = kTokBK;
+  static_assert(BN == kTokBN || BN == kTokBN / 2, "tile width");
   static_assert((NT / 64) == (BM / (32 * MI)) * WN && BN == WN * NI * 32, "tile");
   static_assert(!(PRE && CONV), "pre-split A is for token rows");
   constexpr int ROWB = BK * 2;                 // 64 B per image row (32 bf16)
@@ -85,8 +88,9 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
 
   const TokGroup g = a.groups[blockIdx.y];
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int n_tile = tile % a.n_tiles_n;
-  const int m_tile = tile / a.n_tiles_n;
+  const int n_tiles = a.n_tiles_n;             // BN-column tiles (the caller counts them for this BN)
+  const int n_tile = tile % n_tiles;
+  const int m_tile = tile / n_tiles;
   const int n0 = n_tile * BN;
   if (n0 >= g.N) return;                       // this group has fewer column tiles
   const int m0 = m_tile * BM;
@@ -140,13 +144,19 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
   constexpr int W16 = (X3 ? 2 : 1) * W_BYTES / 16;
   constexpr int W_ITEMS = (W16 + NT - 1) / NT;
   u32x4 wreg[W_ITEMS];
-  const uint16_t* wblk = a.w + g.w_off + (int64_t)n_tile * n_chunks * (2 * W_BYTES / 2);
+  // packed per 128-column block: [block][chunk][hi 128 x 32][lo 128 x 32]; a 64-column tile takes rows
+  // 64 half .. 64 half + 63 of both planes (the row swizzle depends on row & 15 only, so it carries over)
+  constexpr int IMG128 = kTokBN * BK;                       // uint16 per plane of a packed chunk image
+  const uint16_t* wblk = a.w + g.w_off + (int64_t)(BN == kTokBN ? n_tile : n_tile >> 1) * n_chunks * (2 * IMG128) +
+                         (BN == kTokBN ? 0 : (n_tile & 1) * (BN * BK));
 
   auto load_chunk = [&](int kc) {
-    const u32x4* s4 = reinterpret_cast<const u32x4*>(wblk + (int64_t)kc * (2 * W_BYTES / 2));
+    const uint16_t* wc = wblk + (int64_t)kc * (2 * IMG128);
     Unroll<0, W_ITEMS>::run([&](auto I) {
-      const int e = tid + I * NT;
-      wreg[I] = s4[e < W16 ? e : W16 - 1];
+      const int e = min(tid + I * NT, W16 - 1);
+      constexpr int PL16 = W_BYTES / 16;                    // u32x4 per plane of this tile
+      const int pl = e >= PL16 ? 1 : 0, ee = e - pl * PL16;
+      wreg[I] = reinterpret_cast<const u32x4*>(wc + pl * IMG128)[ee];
     });
     const int k = kc * BK + akq;
     kok = k < g.K;  // K % 4 == 0 (host check): a quad is wholly in or out
@@ -1034,7 +1044,11 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
     SESA_REQUIRE(!a.a_hi, SESA_ERR_INVALID, "tok_gemm conv: pre-split A is for token rows");
     // SESA_HCONV_VARIANT=1: the double-buffered 512-thread 256 x 128 tile for the implicit-GEMM convs (A/B)
     static const int hv = getenv("SESA_HCONV_VARIANT") ? atoi(getenv("SESA_HCONV_VARIANT")) : 0;
-    if (hv == 1) {
+    if (a.bn64) {
+      // 64-column tiles (the caller asked for them and counted n_tiles_n in 64-column units)
+      if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 1, false, true, false, 64>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 1, false, true, false, 64>), grid, dim3(256), 0, st, a);
+    } else if (hv == 1) {
       const dim3 g2((unsigned)(((a.M + 255) / 256) * a.n_tiles_n));
       if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 512, 256, 2, 2, 2, true, true, false>), g2, dim3(512), 0, st, a);
       else hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 2, true, true, false>), g2, dim3(512), 0, st, a);

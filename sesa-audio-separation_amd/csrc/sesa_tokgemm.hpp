@@ -76,6 +76,8 @@ struct TokGemmArgs {
   // only feeds another tok_gemm; no residual).  out_lo may be null (bf16).
   uint16_t* out_hi;
   uint16_t* out_lo;
+  // conv mode: 64-column tiles (n_tiles_n then counts ceil(N / 64)) for narrow convolutions
+  int bn64;
 };
 
 // Split fp32 rows into bf16 planes for tok_gemm's pre-split A: hi = bf16(x), lo = bf16(x - hi),
