@@ -20,9 +20,10 @@
 //                           stats, normalise-on-load, conv1d k3 (weights in LDS), GLU
 //   scn_cm_out_kernel       ConvolutionModule tail per row: depthwise k3, GroupNorm(1, h), Swish,
 //                           1x1 conv, residual (+ the SD block's GELU after the last layer)
-//   scn_conv3x3_kernel      3x3 conv over (F, T), 4 x 32 positions x 64 output columns per
-//                           workgroup, 16-channel K chunks staged in LDS; FusionLayer: skip add on
-//                           load, repeated input folded into the weights, GLU in the epilogue
+//   tok_gemm (conv mode)    3x3 conv over (F, T) as an implicit GEMM, K = 9 taps x C (MFMA, bf16x3):
+//                           globalconv, and FusionLayer with the skip added on load, the repeated
+//                           input folded into the weights, GLU over interleaved column pairs
+//   scn_conv3x3_kernel      the same convs in exact fp32 on the VALU (SESA_SCN_CONV3_VALU=1, A/B)
 //   scn_convtr_kernel       SU layer transposed band conv with the symmetric trim
 //   scn_gn_*                DualPathRNN GroupNorm(1, d) (fp64 statistics)
 //   tok_gemm (MFMA)         LSTM input projections (both directions, b_ih + b_hh) and the
@@ -1126,6 +1127,7 @@ struct Level {
   bool cm_gen;                        // ConvolutionModule on the wide-level kernels (scn_cm_*_gen_kernel)
   BandConv sd[3], su[3];
   int64_t sd_w[3], sd_b[3], gc_w, gc_b, fu_w, fu_b, su_w[3], su_b[3];
+  Gemm gc_gm, fu_gm;                  // globalconv / FusionLayer as implicit-GEMM convs (MFMA, bf16x3)
   std::vector<CmLayer> cm[3];
 };
 
@@ -1188,6 +1190,13 @@ size_t al(size_t floats) { return (floats * 4 + 255) / 256 * 256; }
 // Recurrence kernel choice (measured on MI355X, musdb18 config, 4-min track): bf16x3 MFMA for every
 // H (325.7x real-time) beats MFMA for H <= 128 only (307.6x) and the fp32-FMA kernel (280.8x).
 // SESA_LSTM_MFMA=0: fp32 everywhere; =1: MFMA for H <= 128 only (A/B comparisons).
+// globalconv / FusionLayer 3x3 convs on the token GEMM's conv mode (MFMA, bf16x3); SESA_SCN_CONV3_VALU=1
+// keeps the exact-fp32 VALU kernel (scn_conv3x3_kernel) for A/B.
+bool scn_conv3_mfma() {
+  static const bool v = !(getenv("SESA_SCN_CONV3_VALU") && std::string(getenv("SESA_SCN_CONV3_VALU")) == "1");
+  return v;
+}
+
 // (The fp32 kernel needs 256 % H == 0; wider or odd widths always take the MFMA recurrence.)
 bool lstm_mfma_on(int H) {
   static const int mode = getenv("SESA_LSTM_MFMA") ? atoi(getenv("SESA_LSTM_MFMA")) : 2;
@@ -1511,6 +1520,32 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
   }
   std::vector<uint16_t> blob;
   std::vector<float> bias;
+  // globalconv / FusionLayer 3x3 convs for the token GEMM's conv mode: K = 9 taps x C (tap = 3 df + dt,
+  // channel-minor); FusionLayer: repeat(1, 2) folded, GLU pairs interleaved (column 2j = a_j, 2j + 1 = gate_j)
+  for (int i = 0; i < m->nl; ++i) {
+    Level& L = m->lv[i];
+    const int C = L.Cout;
+    const auto& Wg = P(m, "encoder." + S(i) + ".globalconv.weight");  // [C][C][3][3]
+    const auto& Bg = P(m, "encoder." + S(i) + ".globalconv.bias");
+    TokGroup g = pack_group(
+        C, 9 * C, [&](int n, int k) { const int tap = k / C, ci = k - tap * C; return Wg[((size_t)n * C + ci) * 9 + tap]; },
+        true, [&](int n) { return Bg[n]; }, blob, bias);
+    g.x_off = g.o_off = 0;
+    L.gc_gm.groups = {g};
+    const std::string dpfx = "decoder." + S(m->nl - 1 - i);
+    const auto& Wf = P(m, dpfx + ".0.conv.weight");  // [2C][2C][3][3]
+    const auto& Bf = P(m, dpfx + ".0.conv.bias");
+    const int C2 = 2 * C;
+    g = pack_group(
+        C2, 9 * C,
+        [&](int n, int k) {
+          const int co = (n & 1) ? C + (n >> 1) : (n >> 1), tap = k / C, ci = k - tap * C;
+          return Wf[((size_t)co * C2 + ci) * 9 + tap] + Wf[((size_t)co * C2 + ci + C) * 9 + tap];
+        },
+        true, [&](int n) { return Bf[(n & 1) ? C + (n >> 1) : (n >> 1)]; }, blob, bias);
+    g.x_off = g.o_off = 0;
+    L.fu_gm.groups = {g};
+  }
   for (int i = 0; i < (int)m->dp.size(); ++i) {
     DpLayer& L = m->dp[i];
     const std::string p = "separation_net.dp_modules." + S(i);
@@ -1597,6 +1632,11 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
     const int rc = lstm_mfma_prepare(L.H);
     if (rc) return rc;
   }
+  for (auto& L : m->lv) {
+    int rc = upload_groups(L.gc_gm);
+    if (!rc) rc = upload_groups(L.fu_gm);
+    if (rc) return rc;
+  }
   for (auto& L : m->dp)
     for (int l = 0; l < 2; ++l) {
       int rc = upload_groups(L.ih[l]);
@@ -1639,6 +1679,39 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
   int rc = get_tables(&tb);
   if (rc) return rc;
   auto blocks = [](int64_t n) { return dim3((unsigned)((n + kST - 1) / kST)); };
+  // 3x3 conv over (F, T), padding 1, as an implicit GEMM (K = 9 taps x C): A = x (+ S on load), bias,
+  // optional GLU over interleaved column pairs (FusionLayer)
+  auto conv3_gemm = [&](const Gemm& gm, const float* xin, const float* S, int F, int C, float* o, int o_ld, int glu) {
+    TokGemmArgs a{};
+    a.x = xin;
+    a.x_ld = C;
+    a.out = o;
+    a.o_ld = o_ld;
+    a.w = m->d_w;
+    a.bias = m->d_bias;
+    a.groups = gm.d_groups;
+    a.n_groups = 1;
+    a.n_tiles_n = gm.n_tiles_n;
+    a.M = B * F * T;
+    a.act = TOK_ACT_NONE;
+    a.glu = glu;
+    a.conv = 1;
+    ConvGeo& g = a.geo;
+    g.P1 = F; g.P2 = T; g.Q1 = F; g.Q2 = T; g.s1 = 1; g.s2 = 1;
+    g.Cin = C;
+    g.n_taps = 9;
+    for (int t = 0; t < 9; ++t) {
+      g.d1[t] = t / 3 - 1;
+      g.d2[t] = t % 3 - 1;
+    }
+    g.x2 = S;
+    g.phases = 1;
+    if (gm.groups[0].N % 128 == 64) {  // 64-column tiles where a 128-column tile would be 75 % full
+      a.bn64 = 1;
+      a.n_tiles_n = (gm.groups[0].N + 63) / 64;
+    }
+    return launch_tok_gemm(a, x3, st);
+  };
 
   // 1. STFT (scnet.py:335-348)
   float* spec = F32(pl.spec);
@@ -1712,6 +1785,15 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         }
         fl += 2.0 * rows * T * (6.0 * L.h * L.Cout + 3.0 * L.h + (double)L.h * L.Cout);
       }
+    }
+    if (scn_conv3_mfma()) {  // globalconv (3x3) -> bufA on the token GEMM's conv mode
+      profile_end(tok, st, SESA_KCLASS_SIMT, fl);
+      tok = profile_begin(st);
+      rc = conv3_gemm(L.gc_gm, skip, nullptr, L.Fout, L.Cout, bufA, L.Cout, 0);
+      if (rc) return rc;
+      profile_end(tok, st, SESA_KCLASS_TOKGEMM, 2.0 * B * L.Fout * T * L.Cout * L.Cout * 9);
+      cur = bufA;
+      continue;
     }
     {  // globalconv (3x3) -> bufA
       C3Args a{};
@@ -1847,6 +1929,13 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
   for (int j = 0; j < m->nl; ++j) {
     const Level& L = m->lv[m->nl - 1 - j];
     void* tok = profile_begin(st);
+    double fl = 0;
+    if (scn_conv3_mfma()) {  // FusionLayer: x + skip on load, 3x3 C -> 2C, GLU
+      rc = conv3_gemm(L.fu_gm, X, F32(pl.skip[m->nl - 1 - j]), L.Fout, L.Cout, Y, L.Cout, 1);
+      if (rc) return rc;
+      profile_end(tok, st, SESA_KCLASS_TOKGEMM, 2.0 * B * L.Fout * T * 2.0 * L.Cout * L.Cout * 9);
+      tok = profile_begin(st);
+    } else {
     C3Args a{};
     a.A = X;
     a.S = F32(pl.skip[m->nl - 1 - j]);
@@ -1863,7 +1952,8 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
               (unsigned)B);
     hipLaunchKernelGGL(scn_conv3x3_kernel, grid, dim3(kST), 0, st, a);
     SESA_CHECK_LAUNCH();
-    double fl = 2.0 * B * L.Fout * T * 2.0 * L.Cout * 2.0 * L.Cout * 9;
+    fl = 2.0 * B * L.Fout * T * 2.0 * L.Cout * 2.0 * L.Cout * 9;
+    }
     for (int b = 0; b < 3; ++b) {
       const BandConv& bc = L.su[b];
       const int64_t total = (int64_t)B * bc.n_out * T * (L.Cdec / 4);
@@ -1898,6 +1988,9 @@ extern "C" int sesa_scnet_destroy(sesa_scnet* m) {
       if (L.ih[l].d_groups) (void)hipFree(L.ih[l].d_groups);
       if (L.lin[l].d_groups) (void)hipFree(L.lin[l].d_groups);
     }
+  for (auto& L : m->lv)
+    for (Gemm* g : {&L.gc_gm, &L.fu_gm})
+      if (g->d_groups) (void)hipFree(g->d_groups);
   delete m;
   return SESA_OK;
 }
