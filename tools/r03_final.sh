@@ -25,6 +25,7 @@ timeout -k 10 700 bash tools/pmc_refresh.sh bs_roformer "tokgemm=tok_gemm" > $O/
 mkdir -p $O/pmc
 cp gpurun_out/pmc_*.json $O/pmc/ 2>/dev/null || true
 cp $O/pmc/pmc_*.json profiles/          # bench.py below reads the fresh, sha-matched summaries
+rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step mdx23c
 timeout -k 10 400 python bench.py > $O/bench_mdx23c.json 2> $O/bench_mdx23c.err
 step mdx23c bf16
@@ -45,4 +46,13 @@ step rocprof htdemucs
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_htdemucs -o run -- python3 bench.py --model htdemucs --steps 1 --warmup 1 --no-cpu-baseline --no-parity > $O/prof_htdemucs.json 2> $O/prof_htdemucs.err
 step rocprof bs_roformer
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_bsr -o run -- python3 bench.py --model bs_roformer --steps 1 --warmup 1 --no-cpu-baseline --no-parity > $O/prof_bsr.json 2> $O/prof_bsr.err
+step summarize
+# the raw rocpd databases are tens of MiB each: keep the per-kernel summaries, drop the raw dirs so the
+# gpurun_out merge-back stays under its size cap
+for r in mdx23c htdemucs bsr; do
+  python3 tools/rocprof_summary.py $O/prof_$r $O/kernel_stats_$r.txt > /dev/null
+  rm -rf $O/prof_$r
+done
+rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
+du -sh gpurun_out
 step done
