@@ -295,7 +295,7 @@ def main():
     ap.add_argument("--model", default="mdx23c", choices=sorted(MODELS))
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"])
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp16w2", "fp16"])
     ap.add_argument("--exec-batch", type=int, default=0, help="chunks per forward (0: per-model default)")
     ap.add_argument("--track-seconds", type=float, default=0.0, help="0: 240 (1800 for htdemucs)")
     ap.add_argument("--cpu-sample-chunks", type=int, default=8)
@@ -409,10 +409,15 @@ def main():
     if kclass is None:
         kclass = max(("conv3x3", "tokgemm", "lstm", "hconv", "attn"), key=lambda k: _native.profile_read(k)[0])
     ms, launches, work = _native.profile_read(kclass)
-    passes = 3 if args.precision == "bf16x3" else 1
+    # MFMA passes per algorithmic FLOP of the dominant class (fp16 has the same dense peak as bf16); in the
+    # fp16 modes the conv3x3 class is the fp16 direct convs (the T < 32 tap_gemm 3x3s, ~2 % of its FLOPs,
+    # stay bf16x3)
+    passes = {"bf16x3": 3, "bf16": 1, "fp16w2": 2, "fp16": 1}[args.precision]
+    if args.precision.startswith("fp16") and kclass != "conv3x3":
+        passes = 3
     achieved = work / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     peak = BF16_DENSE_TFLOPS / passes
-    note = f"2.5 PF/s dense bf16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
+    note = f"2.5 PF/s dense bf16/fp16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
     if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
         peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
     traffic, traffic_src = pmc_traffic(kclass)

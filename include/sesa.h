@@ -14,6 +14,10 @@
  *   SESA_PREC_BF16X3 -- hi/lo bf16 split, 3 MFMA passes, fp32 accumulate (parity mode:
  *                       ~1.4e-6 RMS vs the fp32 reference on the vocals config)
  *   SESA_PREC_BF16   -- single bf16 pass (throughput mode; ~6e-4 RMS, outside the 1e-4 gate)
+ *   SESA_PREC_F16W2 / SESA_PREC_F16 -- the TFC 3x3 convolutions of the T >= 32 levels (~70 % of the
+ *                       MDX23C FLOPs) on fp16 MFMA: the activation rounded once to fp16 (2^-11) against
+ *                       the fp16 hi + lo weights (2 passes) or the fp16 weights (1 pass); every other
+ *                       contraction bf16x3 (MDX23C only; the other models accept BF16X3 / BF16)
  */
 #ifndef SESA_H_
 #define SESA_H_
@@ -33,6 +37,8 @@ extern "C" {
 
 #define SESA_PREC_BF16X3 0
 #define SESA_PREC_BF16 1
+#define SESA_PREC_F16W2 2 /* MDX23C: TFC 3x3 convs (T >= 32) fp16 activations x fp16 hi/lo weights, 2 passes */
+#define SESA_PREC_F16 3   /* MDX23C: TFC 3x3 convs (T >= 32) single fp16 pass; the rest bf16x3 in both    */
 
 int sesa_version(void);
 const char* sesa_last_error(void);

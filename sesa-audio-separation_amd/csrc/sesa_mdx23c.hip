@@ -52,6 +52,7 @@ struct ConvW {
   int kind = 0, C_in = 0, C_out = 0, n_cols = 0, bn = 64, param = -1;
   int64_t w_off = 0;  // uint16 offset into the packed weight blob
   bool wino = false;  // packed for conv3x3_wino_kernel (decided at finalize, conv3x3_wino_selected)
+  bool f16 = false;   // main chunks packed fp16 hi / lo (SESA_PREC_F16 / F16W2 direct 3x3 convs, finalize)
 };
 struct TdfW {
   int M = 0, K = 0, param = -1;
@@ -166,6 +167,8 @@ Stack add_stack(sesa_mdx23c* m, const std::string& prefix, int in_c, int c, int 
 // ---- weight packing (layouts consumed by sesa_tapgemm.hip) ----
 // Packs one conv (and, for a 3x3 with a fused 1x1 shortcut `xs`, the shortcut's one-tap chunks
 // after each output block's main chunks: [nb][main kc][hi,lo][tap][BN][16] then [xs kc][hi,lo][BN][16]).
+// w.f16: the main chunks as fp16 hi = fp16(v), lo = fp16(v - hi) (round to nearest even; the shortcut chunks
+// stay bf16 hi / lo).
 void pack_conv(const Param& P, ConvW& w, std::vector<uint16_t>& blob, const Param* xs = nullptr, int xs_cin = 0) {
   const bool tr = w.kind == DECONV2X2S2;
   const int KH = (int)P.shape[2], KW = (int)P.shape[3];
@@ -188,6 +191,12 @@ void pack_conv(const Param& P, ConvW& w, std::vector<uint16_t>& blob, const Para
     hi[o] = h;
     lo[o] = f2bf(v - bf2f(h));
   };
+  auto put_h = [&](uint16_t* hi, uint16_t* lo, int p, int kk, float v) {
+    const int64_t o = (int64_t)p * 16 + ((((kk >> 3) ^ ((p >> 3) & 1))) << 3) + (kk & 7);
+    const _Float16 h = (_Float16)v;
+    hi[o] = __builtin_bit_cast(uint16_t, h);
+    lo[o] = __builtin_bit_cast(uint16_t, (_Float16)(v - (float)h));
+  };
   for (int nb = 0; nb < nblk; ++nb) {
     for (int kc = 0; kc < nch; ++kc) {
       uint16_t* hi = base + nb * per_nb + (int64_t)kc * 2 * img;
@@ -206,7 +215,8 @@ void pack_conv(const Param& P, ConvW& w, std::vector<uint16_t>& blob, const Para
                 v = W[(((int64_t)ci * w.C_out + co) * 2 + (t2 >> 1)) * 2 + (t2 & 1)];
               }
             }
-            put(hi, lo, tap * BN + n, kk, v);
+            if (w.f16) put_h(hi, lo, tap * BN + n, kk, v);
+            else put(hi, lo, tap * BN + n, kk, v);
           }
     }
     for (int kc = 0; kc < xch; ++kc) {
@@ -333,6 +343,7 @@ struct Fwd {
   int B;
   int x3;
   char* ws;
+  int f16c = 0;          // launch_conv mode of the w.f16 convs (2 = SESA_PREC_F16W2, 3 = SESA_PREC_F16)
   size_t off = 0;        // float region bump offset (bytes)
   size_t peak = 0;       // high-water mark of `off` (block temporaries are released, see stack())
   size_t stats_off = 0;  // stats region bump offset (bytes), relative to stats_base
@@ -397,7 +408,7 @@ struct Fwd {
                        : w.kind == CONV1X1 ? SESA_KCLASS_CONV1X1
                        : w.kind == CONV2X2S2 ? SESA_KCLASS_DOWN : SESA_KCLASS_UP;
     void* tok = profile_begin(st);
-    rc = launch_conv(w.kind, w.bn, x3, a, B, st);
+    rc = launch_conv(w.kind, w.bn, w.f16 ? f16c : x3, a, B, st);
     profile_end(tok, st, kclass,
                 2.0 * B * T_out * F_out * (double)w.n_cols * (w.C_in * taps + (xin ? xin->C_in : 0)));
   }
@@ -454,6 +465,26 @@ struct Fwd {
     return in;
   }
 
+  // GELU(InstanceNorm(a [++ b])) rounded to fp16, one plane -- the input of an fp16 TFC conv (w.f16)
+  GemmIn act16(Tensor a, Tensor b, const Norm* nrm, int T, int F) {
+    const int C = a.C + (b.C > 0 ? b.C : 0);
+    const int64_t n = (int64_t)B * T * F * C;
+    uint16_t* hi = reinterpret_cast<uint16_t*>(buf((n + 1) / 2));
+    const GemmIn src = input(a, b, SRC_NORM_GELU, SRC_NORM_GELU, nrm, T, F);
+    if (!dry && !rc) {
+      void* tok = profile_begin(st);
+      rc = launch_act_f16(src, (int64_t)T * F, B, hi, st);
+      profile_end(tok, st, SESA_KCLASS_ACT, 6.0 * n);
+    }
+    GemmIn in{};
+    in.src[0] = Src{nullptr, nullptr, nullptr, C, SRC_PRE, hi, nullptr};
+    in.src[1] = in.src[0];
+    in.C_split = C;
+    in.C_in = C;
+    in.inv_count = src.inv_count;
+    return in;
+  }
+
   // GELU(InstanceNorm(a [++ b])) as fp32 -- the input of a Winograd conv (SRC_ACT32)
   GemmIn act32(Tensor a, Tensor b, const Norm* nrm, int T, int F) {
     const int C = a.C + (b.C > 0 ? b.C : 0);
@@ -476,10 +507,10 @@ struct Fwd {
 
   // Input of a TFC 3x3 conv (norm + GELU of `a` [++ `b`]): the raw normalised sources when the conv
   // kernel fuses the activation into its staging (T >= 32 levels), else one act_split pass.
-  GemmIn conv3_input(Tensor a, Tensor b, const Norm* nrm, int T, int F, int C_out) {
-    if (conv3x3_fused_act_ok(T, a.C + (b.C > 0 ? b.C : 0), C_out))
+  GemmIn conv3_input(Tensor a, Tensor b, const Norm* nrm, int T, int F, const ConvW& w) {
+    if (conv3x3_fused_act_ok(T, a.C + (b.C > 0 ? b.C : 0), w.C_out))
       return input(a, b, SRC_NORM_GELU, SRC_NORM_GELU, nrm, T, F);
-    return act(a, b, nrm, T, F);
+    return w.f16 ? act16(a, b, nrm, T, F) : act(a, b, nrm, T, F);
   }
 
   // TFC_TDF.forward (mdx23c_tfc_tdf_v3.py:131-138)
@@ -503,7 +534,7 @@ struct Fwd {
       conv(bk.conv1,
            bk.conv1.wino ? act32(x0, x1, &bk.tfc1, L.T, L.F)
            : pre_sc      ? act(x0, x1, &bk.tfc1, L.T, L.F, &xs)
-                         : conv3_input(x0, x1, &bk.tfc1, L.T, L.F, c),
+                         : conv3_input(x0, x1, &bk.tfc1, L.T, L.F, bk.conv1),
            L.T, L.F, L.T, L.F, H, nullptr, st_h1, 0);
       // x = x + tdf(x)
       tdf(bk.lin1, input(Tensor{H, st_h1, c}, Tensor{}, SRC_NORM_GELU, 0, &bk.tdf0, L.T, L.F), L.T, U, nullptr, st_u,
@@ -516,7 +547,7 @@ struct Fwd {
       if (!pre_sc) xs = input(x0, x1, SRC_RAW, SRC_RAW, nullptr, L.T, L.F);
       conv(bk.conv2,
            bk.conv2.wino ? act32(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F)
-                         : conv3_input(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F, c),
+                         : conv3_input(Tensor{H, st_h2, c}, Tensor{}, &bk.tfc2, L.T, L.F, bk.conv2),
            L.T, L.F, L.T, L.F, S, nullptr, st_out, 0, &xs);
       x0 = Tensor{S, st_out, c};
       x1 = Tensor{};
@@ -601,8 +632,9 @@ extern "C" int sesa_mdx23c_create(const sesa_mdx23c_config* cfg, sesa_mdx23c** o
                c.dim_t - 1);
   SESA_REQUIRE(c.num_subbands > 0 && c.dim_f % c.num_subbands == 0 && c.dim_f <= c.n_fft / 2, SESA_ERR_INVALID,
                "mdx23c: bad dim_f / num_subbands");
-  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16, SESA_ERR_INVALID,
-               "mdx23c: bad precision %d", c.precision);
+  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16 || c.precision == SESA_PREC_F16W2 ||
+                   c.precision == SESA_PREC_F16,
+               SESA_ERR_INVALID, "mdx23c: bad precision %d", c.precision);
   const int F0 = c.dim_f / c.num_subbands;
   const int n = c.num_scales;
   SESA_REQUIRE(n >= 1 && c.num_blocks_per_scale >= 1 && c.bottleneck_factor >= 1, SESA_ERR_INVALID,
@@ -683,9 +715,15 @@ extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
   std::vector<uint16_t> blob;
   std::vector<float> aff;
   auto pc = [&](ConvW& w) { pack_conv(m->params[w.param], w, blob); };
+  // the fp16 precisions: the direct (T >= 32) TFC 3x3 convs only; everything else stays bf16x3
+  const bool f16p = m->cfg.precision == SESA_PREC_F16W2 || m->cfg.precision == SESA_PREC_F16;
   auto pstack = [&](Stack& s) {
     for (auto& b : s.blocks) {
       b.conv1.wino = b.conv2.wino = false;
+      b.conv1.f16 = f16p && b.T >= 32 && !conv3x3_wino_selected(b.T, b.in_c, b.c) &&
+                    !conv3x3_m16_selected(b.T, b.c, b.c, b.in_c);
+      b.conv2.f16 = f16p && b.T >= 32 && !conv3x3_wino_selected(b.T, b.c, b.c) &&
+                    !conv3x3_m16_selected(b.T, b.c, b.c, b.in_c);
       if (conv3x3_wino_selected(b.T, b.in_c, b.c)) pack_conv_wino(m->params[b.conv1.param], b.conv1, blob);
       else pc(b.conv1);
       if (conv3x3_wino_selected(b.T, b.c, b.c))
@@ -733,7 +771,8 @@ extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
 
 namespace {
 void plan_sizes(sesa_mdx23c* m, int batch, size_t* float_bytes, size_t* stats_bytes) {
-  Fwd f{m, nullptr, true, batch, m->cfg.precision == SESA_PREC_BF16X3 ? 1 : 0, nullptr};
+  Fwd f{m, nullptr, true, batch, m->cfg.precision == SESA_PREC_BF16 ? 0 : 1, nullptr};
+  f.f16c = m->cfg.precision == SESA_PREC_F16 ? 3 : 2;
   f.run(nullptr, nullptr);
   *float_bytes = f.peak;
   *stats_bytes = f.stats_off;
@@ -759,7 +798,8 @@ extern "C" int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, fl
   hipStream_t st = as_stream(stream);
   char* ws = reinterpret_cast<char*>(workspace);
   SESA_CHECK_HIP(hipMemsetAsync(ws + fb, 0, sb, st));  // norm statistics accumulate atomically
-  Fwd f{m, st, false, batch, m->cfg.precision == SESA_PREC_BF16X3 ? 1 : 0, ws};
+  Fwd f{m, st, false, batch, m->cfg.precision == SESA_PREC_BF16 ? 0 : 1, ws};
+  f.f16c = m->cfg.precision == SESA_PREC_F16 ? 3 : 2;
   f.stats_base = ws + fb;
   f.stats_cap = sb;
   f.float_cap = fb;

@@ -60,6 +60,16 @@ __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// fp16 operands (SESA_PREC_F16 / F16W2 TFC convs): the same 8 x 16-bit fragment registers, read as fp16
+__device__ __forceinline__ f32x16 mfma32h(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+__device__ __forceinline__ uint32_t pack2h(float a, float b) {  // round-to-nearest-even fp16 pair
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
+}
+
 __device__ __forceinline__ uint32_t pack2(__bf16 a, __bf16 b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
 }
@@ -459,9 +469,16 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 // separate act_split pass over HBM (8 B per element).  The per-channel affine of this batch item is
 // built once per workgroup into LDS (kActMaxC channels).  Each thread stages a fixed 8-channel half of
 // every chunk (tid & 1), so its 8 (scale, shift) pairs are two ds_read_b128 per chunk.
+// F16 (SESA_PREC_F16 / SESA_PREC_F16W2, X3 = true): the main chunks run on v_mfma_f32_32x32x16_f16 with
+// the activation rounded once to fp16 (one A image: act_split's fp16 plane, or the fused staging's fp16
+// pack) against the fp16 weight image (F16 = 1, one pass) or its fp16 hi + lo pair (F16 = 2, two
+// passes: the weights to ~2^-22); the fused 1x1 shortcut chunks stay bf16x3.
 constexpr int kActMaxC = 1024;
-template <bool X3, bool XTRA, int EPI = 0, bool ACT = false>
+template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0>
 __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
+  static_assert(F16 == 0 || X3, "the fp16 modes keep the shortcut chunks bf16x3");
+  constexpr bool ALO = X3 && F16 == 0;  // main chunks read an A lo image
+  constexpr bool WLO = X3 && F16 != 1;  // main chunks read a W lo image
   constexpr int NT = 512;
   constexpr int TM = 16, WM = 8, MI = 2, NI = 2, BN = 64;
   constexpr int HT = TM + 2, HW = kTF + 2, NPOS = HT * HW;
@@ -516,7 +533,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   constexpr int P_ITEMS = (NPOS * 2 + NT - 1) / NT;           // (position, 8-ch half): 16 B hi + 16 B lo
-  constexpr int W16 = (X3 ? 2 : 1) * W_BYTES / 16;
+  constexpr int W16 = (WLO ? 2 : 1) * W_BYTES / 16;
   constexpr int W_ITEMS = (W16 + NT - 1) / NT;
   constexpr int X_ITEMS = TM * kTF * 4 / NT;                 // ext: (inner position, 4-ch group) fp32
   constexpr int W1_16 = (X3 ? 2 : 1) * W1_BYTES / 16;
@@ -565,7 +582,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     } else {
       const int64_t idx = (((int64_t)b * a.T_in + tc) * a.F_in + fc) * C + cl0 + 8 * hf;
       areg[2 * i] = *reinterpret_cast<const f32x4*>(src.hi + idx);
-      areg[2 * i + 1] = *reinterpret_cast<const f32x4*>(src.lo + idx);
+      if constexpr (ALO) areg[2 * i + 1] = *reinterpret_cast<const f32x4*>(src.lo + idx);
     }
     avalid = (avalid & ~(1u << i)) | ((uint32_t)ok << i);
   };
@@ -598,11 +615,15 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     const float h0_ = aff[2 + (q >> 1)][(q & 1) * 2], h1_ = aff[2 + (q >> 1)][(q & 1) * 2 + 1];
     const float y0 = gelu_erf(fmaf(x0, s0, h0_));
     const float y1 = gelu_erf(fmaf(x1, s1, h1_));
-    __bf16 h0, l0, h1, l1;
-    split_bf16(y0, h0, l0);
-    split_bf16(y1, h1, l1);
-    hw[i][q] = pack2(h0, h1) & keep;
-    lw[i][q] = pack2(l0, l1) & keep;
+    if constexpr (F16 != 0) {
+      hw[i][q] = pack2h(y0, y1) & keep;
+    } else {
+      __bf16 h0, l0, h1, l1;
+      split_bf16(y0, h0, l0);
+      split_bf16(y1, h1, l1);
+      hw[i][q] = pack2(h0, h1) & keep;
+      lw[i][q] = pack2(l0, l1) & keep;
+    }
   };
   auto item_off = [&](int i) {
     const int e = min(tid + i * NT, NPOS * 2 - 1);
@@ -613,7 +634,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     constexpr int i = decltype(I)::value;
     const int off = item_off(i);
     *reinterpret_cast<u32x4*>(stg + off) = u32x4{hw[i][0], hw[i][1], hw[i][2], hw[i][3]};
-    if (X3) *reinterpret_cast<u32x4*>(stg + A_BYTES + off) = u32x4{lw[i][0], lw[i][1], lw[i][2], lw[i][3]};
+    if (ALO) *reinterpret_cast<u32x4*>(stg + A_BYTES + off) = u32x4{lw[i][0], lw[i][1], lw[i][2], lw[i][3]};
   };
   auto store_main = [&](char* stg, int kc) {
     store_w(stg);
@@ -630,7 +651,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
         const bool ok = (avalid >> i) & 1u;
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
         *reinterpret_cast<f32x4*>(stg + off) = ok ? areg[2 * i] : z;
-        if (X3) *reinterpret_cast<f32x4*>(stg + A_BYTES + off) = ok ? areg[2 * i + 1] : z;
+        if (ALO) *reinterpret_cast<f32x4*>(stg + A_BYTES + off) = ok ? areg[2 * i + 1] : z;
       });
     }
   };
@@ -681,7 +702,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   struct Frags {
     bf16x8 ah[MI], al[MI], bh[NI], bl[NI];
   };
-  auto read_frags = [&](Frags& fr, const char* stg, int dy, int dx, int wt, int wimg) {
+  // EXT: a shortcut chunk (bf16x3 in every mode); else a main chunk (ALO / WLO)
+  auto read_frags = [&](Frags& fr, const char* stg, int dy, int dx, int wt, int wimg, auto EXT) {
+    constexpr bool rd_al = decltype(EXT)::value ? X3 : ALO;
+    constexpr bool rd_bl = decltype(EXT)::value ? X3 : WLO;
     const char* A_hi = stg;
     const char* A_lo = stg + A_BYTES;
     const char* W_hi = stg + 2 * A_BYTES;
@@ -691,35 +715,36 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       const int p = (row + dy) * HW + l32 + dx;
       const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
       fr.ah[i] = *reinterpret_cast<const bf16x8*>(A_hi + off);
-      if (X3) fr.al[i] = *reinterpret_cast<const bf16x8*>(A_lo + off);
+      if (rd_al) fr.al[i] = *reinterpret_cast<const bf16x8*>(A_lo + off);
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int p = wt * BN + j * 32 + l32;
       const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
       fr.bh[j] = *reinterpret_cast<const bf16x8*>(W_hi + off);
-      if (X3) fr.bl[j] = *reinterpret_cast<const bf16x8*>(W_hi + wimg + off);
+      if (rd_bl) fr.bl[j] = *reinterpret_cast<const bf16x8*>(W_hi + wimg + off);
     }
   };
-  auto mfma_group = [&](const Frags& fr, int i, int j) {
-    if (X3) {
-      acc[i][j] = mfma32(fr.al[i], fr.bh[j], acc[i][j]);
-      acc[i][j] = mfma32(fr.ah[i], fr.bl[j], acc[i][j]);
+  auto mfma_group = [&](const Frags& fr, int i, int j, auto EXT) {
+    if constexpr (F16 != 0 && !decltype(EXT)::value) {
+      if constexpr (F16 == 2) acc[i][j] = mfma32h(fr.ah[i], fr.bl[j], acc[i][j]);
+      acc[i][j] = mfma32h(fr.ah[i], fr.bh[j], acc[i][j]);
+    } else {
+      if (X3) {
+        acc[i][j] = mfma32(fr.al[i], fr.bh[j], acc[i][j]);
+        acc[i][j] = mfma32(fr.ah[i], fr.bl[j], acc[i][j]);
+      }
+      acc[i][j] = mfma32(fr.ah[i], fr.bh[j], acc[i][j]);
     }
-    acc[i][j] = mfma32(fr.ah[i], fr.bh[j], acc[i][j]);
   };
-  auto mfmas = [&](const Frags& fr) {
+  auto mfmas = [&](const Frags& fr, auto EXT) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        if (X3) {
-          acc[i][j] = mfma32(fr.al[i], fr.bh[j], acc[i][j]);
-          acc[i][j] = mfma32(fr.ah[i], fr.bl[j], acc[i][j]);
-        }
-        acc[i][j] = mfma32(fr.ah[i], fr.bh[j], acc[i][j]);
-      }
+      for (int j = 0; j < NI; ++j) mfma_group(fr, i, j, EXT);
   };
+  constexpr std::false_type kMain{};
+  constexpr std::true_type kExt{};
 
   // ---- main chunks: straight-line pipelined body, clamped (redundant) prefetch at the tail ----
   load_main(0);
@@ -731,12 +756,12 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     char* cur = smem + (kc & 1) * STAGE;
     char* nxt = smem + ((kc + 1) & 1) * STAGE;
     Frags fr[2];
-    read_frags(fr[0], cur, 0, 0, 0, W_BYTES);
+    read_frags(fr[0], cur, 0, 0, 0, W_BYTES, kMain);
     if constexpr (!ACT) {
       Unroll<0, 9>::run([&](auto T) {
         constexpr int tap = decltype(T)::value;
-        if (tap + 1 < 9) read_frags(fr[(tap + 1) & 1], cur, (tap + 1) / 3, (tap + 1) % 3, tap + 1, W_BYTES);
-        mfmas(fr[tap & 1]);
+        if (tap + 1 < 9) read_frags(fr[(tap + 1) & 1], cur, (tap + 1) / 3, (tap + 1) % 3, tap + 1, W_BYTES, kMain);
+        mfmas(fr[tap & 1], kMain);
         if (tap == 1) {
           // stage chunk kc+1 (in registers since the previous iteration) under the MFMAs, then start
           // loading chunk kc+2; past the end both are harmless repeats of the last chunk
@@ -754,10 +779,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       load_aff(ks);
       Unroll<0, 9>::run([&](auto T) {
         constexpr int tap = decltype(T)::value;
-        if (tap + 1 < 9) read_frags(fr[(tap + 1) & 1], cur, (tap + 1) / 3, (tap + 1) % 3, tap + 1, W_BYTES);
+        if (tap + 1 < 9) read_frags(fr[(tap + 1) & 1], cur, (tap + 1) / 3, (tap + 1) % 3, tap + 1, W_BYTES, kMain);
         Unroll<0, MI * NI>::run([&](auto G) {
           constexpr int g = decltype(G)::value, gi = 4 * tap + g;
-          mfma_group(fr[tap & 1], g / NI, g % NI);
+          mfma_group(fr[tap & 1], g / NI, g % NI, kMain);
           __builtin_amdgcn_sched_barrier(0);
           if constexpr (gi == 0) {
             store_w(nxt);
@@ -788,8 +813,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       char* cur = smem + (kx & 1) * STAGE;
       char* nxt = smem + ((kx + 1) & 1) * STAGE;
       Frags fr;
-      read_frags(fr, cur, 1, 1, 0, W1_BYTES);
-      mfmas(fr);
+      read_frags(fr, cur, 1, 1, 0, W1_BYTES, kExt);
+      mfmas(fr, kExt);
       store_ext(nxt);
       load_ext(min(kx + 2, nx - 1));
       __syncthreads();
@@ -2418,7 +2443,8 @@ constexpr int kActUnroll = 4;
 // shortcut operand of conv3x3_m16_kernel, written while the input is in registers anyway.
 // F32OUT: the activation itself as fp32 (hi = the fp32 output, lo / rhi / rlo unused) -- the SRC_ACT32 input of
 // conv3x3_wino_kernel, whose Winograd input transform needs the unsplit value.
-template <bool F32OUT>
+// F16OUT (lo == nullptr): the activation rounded once to fp16 into `hi` -- the A plane of the fp16 TFC convs.
+template <bool F32OUT, bool F16OUT = false>
 __global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t n_pos, int pos_per_block,
                                                              uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
                                                              uint16_t* __restrict__ rhi, uint16_t* __restrict__ rlo) {
@@ -2474,6 +2500,15 @@ __global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t 
         f32x4* op = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(hi) + o);
         __builtin_nontemporal_store(f32x4{y[0][0], y[0][1], y[1][0], y[1][1]}, op);
         __builtin_nontemporal_store(f32x4{y[2][0], y[2][1], y[3][0], y[3][1]}, op + 1);
+        continue;
+      }
+      if constexpr (F16OUT) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 y = act ? gelu_erf2(__builtin_elementwise_fma(v[q], sc[q], sh[q])) : v[q];
+          hw[q] = pack2h(y[0], y[1]);
+        }
+        *reinterpret_cast<uint4*>(hi + o) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
         continue;
       }
       if (rhi) {
@@ -2610,8 +2645,16 @@ bool conv3x3_m16_selected(int T_out, int C_in, int C_out, int C_shortcut) {
 }
 
 // Tile choices per kind (BN = 64 unless the GEMM N is <= 32).
+// x3: 0 = bf16, 1 = bf16x3; 2 / 3 = the fp16 TFC-conv modes (SESA_PREC_F16W2 / SESA_PREC_F16), accepted only
+// for the direct double-buffered 3x3 kernel (the host packs those convs' main chunks as fp16 hi / lo).
 int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStream_t st) {
   SESA_REQUIRE(a.F_out % kTF == 0, SESA_ERR_INVALID, "conv: F_out %d not a multiple of %d", a.F_out, kTF);
+  const int xmode = x3;
+  x3 = x3 != 0 ? 1 : 0;
+  const bool db3 = kind == CONV3X3 && a.in.src[0].mode != SRC_ACT32 && a.T_out >= 32 && a.out.residual == nullptr &&
+                   a.out.gelu == 0 && !conv3x3_m16_selected(a.T_out, a.in.C_in, a.out.C_out, a.x_chunks > 0 ? a.xin.C_in : 0);
+  SESA_REQUIRE(xmode >= 0 && xmode <= 3 && (xmode < 2 || db3), SESA_ERR_INVALID,
+               "conv: fp16 mode %d only for the direct 3x3 kernel", xmode);
   SESA_REQUIRE(a.in.C_in % kConvBK == 0 && a.in.C_split % kConvBK == 0 && a.in.C_in <= kMaxCin, SESA_ERR_INVALID,
                "conv: C_in %d / split %d must be multiples of %d (<= %d)", a.in.C_in, a.in.C_split, kConvBK,
                kMaxCin);
@@ -2675,7 +2718,8 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
                        SESA_ERR_INVALID, "conv3x3: fused-activation input must be normalised fp32 sources, C <= %d",
                        kActMaxC);
         } else {
-          SESA_REQUIRE(a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && a.in.src[0].lo && a.in.C_split == a.in.C_in,
+          SESA_REQUIRE(a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && (xmode >= 2 || a.in.src[0].lo) &&
+                           a.in.C_split == a.in.C_in,
                        SESA_ERR_INVALID, "conv3x3: needs a single pre-activated (act_split) input");
         }
         dim3 grid((unsigned)(((a.T_out + 15) / 16) * (a.F_out / kTF) * ((a.n_cols + 63) / 64)), 1u, (unsigned)batch);
@@ -2683,17 +2727,22 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
           SESA_REQUIRE(a.xin.C_in % kConvBK == 0 && a.xin.C_split % kConvBK == 0 && a.xin.src[0].mode == SRC_RAW &&
                            a.xin.src[1].mode == SRC_RAW,
                        SESA_ERR_INVALID, "conv3x3: fused shortcut must be a raw input, C_in multiple of %d", kConvBK);
-#define SESA_DB(X3V, XTRAV)                                                                              \
-  do {                                                                                                  \
-    if (act) hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, true>), grid, dim3(512), 0, st, a);    \
-    else hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, false>), grid, dim3(512), 0, st, a);       \
+#define SESA_DB(X3V, XTRAV, F16V)                                                                            \
+  do {                                                                                                      \
+    if (act) hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, true, F16V>), grid, dim3(512), 0, st, a);  \
+    else hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, false, F16V>), grid, dim3(512), 0, st, a);     \
   } while (0)
+        // xmode 2 = fp16 x fp16 hi/lo weights (F16 = 2), 3 = fp16 single pass (F16 = 1)
         if (a.x_chunks > 0) {
-          if (x3) SESA_DB(true, true);
-          else SESA_DB(false, true);
+          if (xmode == 3) SESA_DB(true, true, 1);
+          else if (xmode == 2) SESA_DB(true, true, 2);
+          else if (x3) SESA_DB(true, true, 0);
+          else SESA_DB(false, true, 0);
         } else {
-          if (x3) SESA_DB(true, false);
-          else SESA_DB(false, false);
+          if (xmode == 3) SESA_DB(true, false, 1);
+          else if (xmode == 2) SESA_DB(true, false, 2);
+          else if (x3) SESA_DB(true, false, 0);
+          else SESA_DB(false, false, 0);
         }
 #undef SESA_DB
         SESA_CHECK_LAUNCH();
@@ -2760,6 +2809,19 @@ int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, u
   dim3 grid((unsigned)((n_pos + ppb - 1) / ppb), (unsigned)batch);
   hipLaunchKernelGGL(act_split_kernel<false>, grid, dim3((unsigned)(groups * lanes_pos)), 0, st, in, n_pos, ppb, hi,
                      lo, raw_hi, raw_lo);
+  SESA_CHECK_LAUNCH();
+  return SESA_OK;
+}
+
+int launch_act_f16(const GemmIn& in, int64_t n_pos, int batch, uint16_t* out, hipStream_t st) {
+  SESA_REQUIRE(in.C_in % 16 == 0 && in.C_split % 8 == 0 && in.C_in <= kMaxCin, SESA_ERR_INVALID,
+               "act_f16: C %d must be a multiple of 16 (<= %d)", in.C_in, kMaxCin);
+  const int groups = in.C_in / 8;
+  const int lanes_pos = groups >= kThreads ? 1 : kThreads / groups;
+  const int ppb = lanes_pos * 32;
+  dim3 grid((unsigned)((n_pos + ppb - 1) / ppb), (unsigned)batch);
+  hipLaunchKernelGGL((act_split_kernel<false, true>), grid, dim3((unsigned)(groups * lanes_pos)), 0, st, in, n_pos,
+                     ppb, out, nullptr, nullptr, nullptr);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }

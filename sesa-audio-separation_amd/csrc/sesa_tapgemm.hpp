@@ -74,6 +74,8 @@ int launch_act_split(const GemmIn& in, int64_t n_pos, int batch, uint16_t* hi, u
                      uint16_t* raw_hi = nullptr, uint16_t* raw_lo = nullptr);
 // act_f32: out[b][pos][c] = GELU(IN_affine(x)) as fp32 (the SRC_ACT32 input of the Winograd conv).
 int launch_act_f32(const GemmIn& in, int64_t n_pos, int batch, float* out, hipStream_t st);
+// GELU(InstanceNorm(x)) rounded to fp16 (one plane, NHWC): the A operand of the fp16 TFC 3x3 convs
+int launch_act_f16(const GemmIn& in, int64_t n_pos, int batch, uint16_t* out, hipStream_t st);
 // True when a same-size TFC 3x3 conv at T_out runs as Winograd F(2, 3) (conv3x3_wino_kernel): its weights
 // are then packed by pack_conv_wino (sesa_mdx23c.hip) and its input is given as SRC_ACT32.
 bool conv3x3_wino_selected(int T_out, int C_in, int C_out);

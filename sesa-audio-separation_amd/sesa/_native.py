@@ -12,6 +12,8 @@ P_i64 = ctypes.POINTER(ctypes.c_int64)
 
 SESA_PREC_BF16X3 = 0
 SESA_PREC_BF16 = 1
+SESA_PREC_F16W2 = 2
+SESA_PREC_F16 = 3
 
 
 class SesaMdx23cConfig(ctypes.Structure):

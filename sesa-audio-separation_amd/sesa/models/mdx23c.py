@@ -28,6 +28,10 @@ class TFC_TDF_net(NativeModule):
     """Reference-compatible MDX23C module (torch.nn.Module) backed by the native HIP forward."""
 
     _prefix = "mdx23c"
+    # fp16 / fp16w2: the TFC 3x3 convs of the T >= 32 levels on fp16 MFMA (include/sesa.h SESA_PREC_F16*)
+    _precisions = ("bf16x3", "bf16", "fp16w2", "fp16")
+    _prec_codes = {"bf16x3": N.SESA_PREC_BF16X3, "bf16": N.SESA_PREC_BF16, "fp16w2": N.SESA_PREC_F16W2,
+                   "fp16": N.SESA_PREC_F16}
 
     def __init__(self, config, precision="bf16x3"):
         super().__init__(precision)
@@ -56,7 +60,7 @@ class TFC_TDF_net(NativeModule):
 
     def _config(self, chunk):
         return N.SesaMdx23cConfig(**self._ccfg,
-                                  precision=N.SESA_PREC_BF16 if self.precision == "bf16" else N.SESA_PREC_BF16X3)
+                                  precision=self._prec_codes[self.precision])
 
     def workspace_bytes(self, batch, chunk=None):
         # not cached: the size depends on the precision (bf16x3 adds lo planes) and on the process-wide

@@ -37,6 +37,7 @@ class NativeModule(torch.nn.Module):
     points) and implement ``_config(chunk)`` (the ctypes config struct) and ``_out_shape``."""
 
     _prefix = None
+    _precisions = ("bf16x3", "bf16")
 
     def __init__(self, precision="bf16x3"):
         super().__init__()
@@ -110,8 +111,8 @@ class NativeModule(torch.nn.Module):
         return self._handles[idx]
 
     def set_precision(self, precision):
-        if precision not in ("bf16x3", "bf16"):
-            raise ValueError(precision)
+        if precision not in self._precisions:
+            raise ValueError(f"{type(self).__name__}: precision {precision!r} not in {self._precisions}")
         self.precision = precision
         return self
 

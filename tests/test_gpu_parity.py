@@ -300,3 +300,27 @@ def test_conv3x3_m16_variant_matches_reference(golden, dev, fixture, cfg_name, a
     assert err <= RMS_GATE
     y0 = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()           # default kernel, same model
     assert rms(y0, y) <= 1e-5                                         # fp32 summation order only
+
+
+@pytest.mark.parametrize("precision", ["fp16w2", "fp16"])
+@pytest.mark.parametrize("fixture,cfg_name,affine", [("mdx23c_small.npz", "config_mdx23c_small.yaml", None),
+                                                     ("mdx23c_small_stress.npz", "config_mdx23c_small.yaml", "stress"),
+                                                     ("mdx23c_full_chunk.npz", "config_vocals_mdx23c.yaml", "unit")])
+def test_forward_fp16_conv_matches_reference(golden, dev, fixture, cfg_name, affine, precision, record_property):
+    """SESA_PREC_F16W2 / SESA_PREC_F16: the direct TFC 3x3 convs (T >= 32 levels) on fp16 MFMA -- the
+    activation rounded once to fp16 against fp16 hi + lo weights (fp16w2) or fp16 weights (fp16); every other
+    contraction bf16x3.  Same 1e-4 per-sample RMS gate against the reference's fp32 goldens as the parity
+    mode.  (CPU emulation of the same rounding on the full chunk, oracle/mdx23c.py with the 3x3 inputs
+    rounded: 3.8e-5 for fp16w2, 5.2e-5 for fp16.)"""
+    g = golden(fixture)
+    m, _ = _model(cfg_name, affine or str(g["affine"]), precision=precision)
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, g["y"])
+    print(f"{fixture} ({precision} TFC convs): rms={err:.3e}")
+    record_property(f"{fixture}_{precision}_rms", err)
+    out_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(out_dir):
+        import json
+        with open(os.path.join(out_dir, f"parity_{precision}_{fixture.replace('.npz', '')}.json"), "w") as f:
+            json.dump({"fixture": fixture, "precision": precision, "rms_vs_reference": err, "gate": RMS_GATE}, f)
+    assert np.isfinite(y).all() and err <= RMS_GATE
