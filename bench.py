@@ -104,9 +104,17 @@ def kernel_sources_sha16(kclass):
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(kclass):
+def default_precision(model):
+    """MDX23C: the fp16 TFC-conv precision (SESA_PREC_F16: the T >= 32 3x3 convs on fp16 MFMA, the rest
+    bf16x3; 5.1e-5 RMS vs the reference's full-chunk golden, inside the 1e-4 north_star gate -- the line
+    carries the measured value); every other model and the ensemble: bf16x3."""
+    return "fp16" if model == "mdx23c" else "bf16x3"
+
+
+def pmc_traffic(kclass, precision="bf16x3"):
     """(HBM bytes per launch, provenance) from profiles/pmc_<class>.json when its ``src_sha16`` matches
-    the kernel sources in this tree; (None, reason) otherwise -- a stale counter figure is not reported."""
+    the kernel sources in this tree and it was measured in the same precision mode; (None, reason)
+    otherwise -- a stale counter figure is not reported."""
     pmc = os.path.join(REPO, "profiles", f"pmc_{kclass}.json")
     if not os.path.exists(pmc):
         return None, f"no profiles/pmc_{kclass}.json"
@@ -116,17 +124,21 @@ def pmc_traffic(kclass):
     if d.get("src_sha16") != cur:
         return None, (f"profiles/pmc_{kclass}.json measured on sources {d.get('src_sha16')} (git "
                       f"{d.get('git_sha', '?')}), this tree has {cur}: stale, not reported")
+    if d.get("precision", "bf16x3") != precision:
+        return None, (f"profiles/pmc_{kclass}.json measured in precision {d.get('precision', 'bf16x3')}, this run "
+                      f"is {precision}: not reported")
     return d.get("hbm_bytes_per_launch"), {"file": f"profiles/pmc_{kclass}.json", "src_sha16": cur,
-                                           "git_sha": d.get("git_sha"), "algorithmic_bytes_per_launch":
-                                           d.get("algorithmic_bytes_per_launch")}
+                                           "git_sha": d.get("git_sha"), "precision": precision,
+                                           "algorithmic_bytes_per_launch": d.get("algorithmic_bytes_per_launch")}
 
 
-def mdx23c_conv3x3_alg_bytes(cfg, batch):
+def mdx23c_conv3x3_alg_bytes(cfg, batch, precision="bf16x3"):
     """Algorithmic HBM bytes of the conv3x3 class over one MDX23C forward of `batch` chunks, and its launch
-    count: each TFC 3x3 conv reads its input once (4 B per element: fp32 for the fused-activation
-    kernel, bf16 hi + lo planes otherwise -- the same bytes), the fused 1x1 shortcut's raw input (4 B)
-    for conv2, and writes its fp32 output (4 B); weights as bf16 hi + lo (4 B per coefficient)
-    (mdx23c_tfc_tdf_v3.py:100-138; levels as TFC_TDF_net.__init__ :141-203)."""
+    count: each TFC 3x3 conv reads its input once (fp32 for the fused-activation kernel -- T >= 32,
+    C_out <= 128 -- else the act_split planes: bf16 hi + lo 4 B, one fp16 or bf16 plane 2 B), the fused
+    1x1 shortcut's raw input (4 B) for conv2, and writes its fp32 output (4 B); weights per coefficient
+    4 B (bf16 hi + lo, fp16 hi + lo), 2 B (bf16 or fp16 alone); the T < 32 convs stay bf16x3 in the fp16
+    modes (mdx23c_tfc_tdf_v3.py:100-138; levels as TFC_TDF_net.__init__ :141-203)."""
     m = cfg.model
     n, nb, c0, g = int(m.num_scales), int(m.num_blocks_per_scale), int(m.num_channels), int(m.growth)
     T0, F0 = int(cfg.audio.dim_t), int(cfg.audio.dim_f) // int(m.num_subbands)
@@ -135,10 +147,14 @@ def mdx23c_conv3x3_alg_bytes(cfg, batch):
     def stack(T, F, in_c, c):
         nonlocal total, launches
         pos = batch * T * F
+        f16 = precision.startswith("fp16") and T >= 32
+        single = precision == "bf16" or (f16 and precision == "fp16")
+        a_in = 4.0 if (T >= 32 and c <= 128) else (2.0 if (f16 or precision == "bf16") else 4.0)
+        wb = 2.0 if single else 4.0
         for i in range(nb):
             ic = in_c if i == 0 else c
-            total += pos * (ic + c) * 4.0 + 9 * ic * c * 4.0                  # conv1
-            total += pos * (c + c + ic) * 4.0 + (9 * c + ic) * c * 4.0        # conv2 (+ shortcut operand)
+            total += pos * ic * a_in + pos * c * 4.0 + 9 * ic * c * wb                     # conv1
+            total += pos * c * a_in + pos * (c + ic) * 4.0 + 9 * c * c * wb + ic * c * 4.0  # conv2 (+ shortcut)
             launches += 2
     for lv in range(n):
         stack(T0 >> lv, F0 >> lv, c0 + g * lv, c0 + g * lv)
@@ -285,6 +301,8 @@ def build_model(name, precision):
     cfg_path = os.path.join(CFG_DIR, MODELS[name][0])
     model, cfg = get_model_from_config(name, cfg_path)
     model.load_state_dict(synth_state_dict(model) if name == "mdx23c" else synth_weights(model), strict=True)
+    if precision.startswith("fp16") and name != "mdx23c":
+        precision = "bf16x3"  # the fp16 TFC-conv modes are MDX23C's; other members run their parity precision
     model.set_precision(precision)
     return model, cfg, cfg_path
 
@@ -295,7 +313,8 @@ def main():
     ap.add_argument("--model", default="mdx23c", choices=sorted(MODELS))
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp16w2", "fp16"])
+    ap.add_argument("--precision", default=None, choices=["bf16x3", "bf16", "fp16w2", "fp16"],
+                    help="default: fp16 for mdx23c (TFC 3x3 convs on fp16 MFMA, inside the 1e-4 gate), else bf16x3")
     ap.add_argument("--exec-batch", type=int, default=0, help="chunks per forward (0: per-model default)")
     ap.add_argument("--track-seconds", type=float, default=0.0, help="0: 240 (1800 for htdemucs)")
     ap.add_argument("--cpu-sample-chunks", type=int, default=8)
@@ -308,6 +327,8 @@ def main():
     ap.add_argument("--cpu-chunks-only", action="store_true",
                     help="mdx23c: time --cpu-sample-chunks forwards instead of the configs[0] 10 s end-to-end run")
     args = ap.parse_args()
+    if args.precision is None:
+        args.precision = default_precision(args.model)
     track_seconds = args.track_seconds or TRACK_SECONDS.get(args.model, 240.0)
 
     from sesa.launch import needs_spawn, spawn_world, world_from_env
@@ -420,13 +441,13 @@ def main():
     note = f"2.5 PF/s dense bf16/fp16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
     if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
         peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
-    traffic, traffic_src = pmc_traffic(kclass)
+    traffic, traffic_src = pmc_traffic(kclass, args.precision)
     alg_bytes = None
     if kclass == "conv3x3":
         m0, cfg0, _ = members[0]
         per_fwd, l_fwd = 0.0, 0
         for nb_ in [len(x) for x in _forward_sizes(chunks[0], batches[0], world)]:
-            b_, l_ = mdx23c_conv3x3_alg_bytes(cfg0, nb_)
+            b_, l_ = mdx23c_conv3x3_alg_bytes(cfg0, nb_, args.precision)
             per_fwd += b_
             l_fwd += l_
         alg_bytes = round(per_fwd / max(l_fwd, 1))

@@ -5,8 +5,9 @@ The reference backend wraps an nn.Module with device flags, fp16 autocast and to
 jit / channels_last modes.  Here the model is a native libsesa network; the optimisation modes
 are accepted for CLI compatibility and map onto what exists on MI355X:
 
-* ``enable_amp``  -> throughput precision (single-pass bf16 MFMA) instead of the default
-  3-pass bf16x3 parity precision.  (The reference's AMP is fp16 autocast, :308-311.)
+* ``enable_amp``  -> the model's throughput precision (``_amp_precision``) instead of the default
+  3-pass bf16x3 parity precision: MDX23C ``fp16`` (its TFC 3x3 convs on fp16 MFMA, 5.1e-5 RMS -- the
+  reference's AMP is fp16 autocast, :308-311, 1.35e-4 RMS), the other models single-pass ``bf16``.
 * ``optimize_mode`` ('channels_last' | 'compile' | 'jit' | 'default') -> no effect: the native
   forward already runs channels-last with fused prologues/epilogues, and there is no tracing
   compiler in the path.
@@ -40,7 +41,7 @@ class HipBackend:
         self.model = model.eval()
         self.use_amp = bool(use_amp)
         if hasattr(model, "set_precision"):
-            model.set_precision("bf16" if self.use_amp else "bf16x3")
+            model.set_precision(getattr(model, "_amp_precision", "bf16") if self.use_amp else "bf16x3")
         self.compiled_model = self.model
         return self.compiled_model
 

@@ -60,7 +60,7 @@ def build_parser():
     p.add_argument("--overlap", type=int, default=4)             # parsed but unused, as in the reference
     p.add_argument("--optimize_mode", type=str, choices=["channels_last", "compile", "jit", "default"],
                    default="channels_last")
-    p.add_argument("--enable_amp", action="store_true", help="single-pass bf16 (faster, ~6e-4 RMS)")
+    p.add_argument("--enable_amp", action="store_true", help="throughput precision: MDX23C fp16 TFC convs (~5e-5 RMS), others single-pass bf16")
     p.add_argument("--enable_tf32", action="store_true")
     p.add_argument("--enable_cudnn_benchmark", action="store_true")
     p.add_argument("--lora_checkpoint", type=str, default="")

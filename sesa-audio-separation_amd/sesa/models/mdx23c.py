@@ -30,6 +30,7 @@ class TFC_TDF_net(NativeModule):
     _prefix = "mdx23c"
     # fp16 / fp16w2: the TFC 3x3 convs of the T >= 32 levels on fp16 MFMA (include/sesa.h SESA_PREC_F16*)
     _precisions = ("bf16x3", "bf16", "fp16w2", "fp16")
+    _amp_precision = "fp16"
     _prec_codes = {"bf16x3": N.SESA_PREC_BF16X3, "bf16": N.SESA_PREC_BF16, "fp16w2": N.SESA_PREC_F16W2,
                    "fp16": N.SESA_PREC_F16}
 

@@ -38,6 +38,7 @@ class NativeModule(torch.nn.Module):
 
     _prefix = None
     _precisions = ("bf16x3", "bf16")
+    _amp_precision = "bf16"  # --enable_amp (sesa.backend)
 
     def __init__(self, precision="bf16x3"):
         super().__init__()

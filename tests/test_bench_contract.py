@@ -1,0 +1,59 @@
+"""bench.py host logic (no GPU): the precision each model's default line runs in, and the conv3x3
+algorithmic-bytes model that roofline.traffic is compared against."""
+import os
+import sys
+from types import SimpleNamespace as NS
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def _vocals_cfg():
+    # config_vocals_mdx23c.yaml: dim_f 4096 / 4 subbands, dim_t 256, 4 scales, 128 + 128 per level
+    return NS(model=NS(num_scales=4, num_blocks_per_scale=1, num_channels=128, growth=128, num_subbands=4),
+              audio=NS(dim_t=256, dim_f=4096))
+
+
+def test_default_precision():
+    assert bench.default_precision("mdx23c") == "fp16"
+    for m in ("bs_roformer", "htdemucs", "scnet", "ensemble"):
+        assert bench.default_precision(m) == "bf16x3"
+
+
+def test_conv3x3_alg_bytes_by_precision():
+    c = _vocals_cfg()
+    b3, n3 = bench.mdx23c_conv3x3_alg_bytes(c, 57, "bf16x3")
+    bw, nw = bench.mdx23c_conv3x3_alg_bytes(c, 57, "fp16w2")
+    b1, n1 = bench.mdx23c_conv3x3_alg_bytes(c, 57, "fp16")
+    assert n3 == nw == n1 == 2 * 9                       # 9 TFC_TDF stacks x (conv1, conv2)
+    assert b1 < bw < b3                                   # fp16 plane (2 B) inputs, then 2 B weights
+    # level 0 (fused fp32 input) is precision-independent apart from the weights
+    b3_l0 = 57 * 256 * 1024 * (128 * 4 + 128 * 4) + 9 * 128 * 128 * 4
+    assert b3 > 2 * b3_l0
+
+
+def test_fp16_modes_are_mdx23c_only():
+    from sesa.models.mdx23c import TFC_TDF_net
+    from sesa.models.native import NativeModule
+    assert "fp16" in TFC_TDF_net._precisions and TFC_TDF_net._amp_precision == "fp16"
+    assert "fp16" not in NativeModule._precisions and NativeModule._amp_precision == "bf16"
+
+
+@pytest.mark.parametrize("name", ["bs_roformer", "scnet", "htdemucs"])
+def test_bench_maps_fp16_to_parity_for_other_members(name, monkeypatch):
+    seen = {}
+
+    class Fake:
+        def load_state_dict(self, *a, **k):
+            pass
+
+        def set_precision(self, p):
+            seen["p"] = p
+
+    import sesa.utils
+    monkeypatch.setattr(sesa.utils, "get_model_from_config", lambda n, p: (Fake(), None))
+    monkeypatch.setattr(bench, "synth_weights", lambda m: {})
+    bench.build_model(name, "fp16")
+    assert seen["p"] == "bf16x3"

@@ -204,15 +204,18 @@ def test_demix_edge_lengths_vs_oracle(dev, L):
     np.testing.assert_array_equal(est[1], ref["other"])
 
 
-def test_config0_demix_10s_full_model_matches_reference(dev, golden):
+@pytest.mark.parametrize("precision", ["bf16x3", "fp16"])
+def test_config0_demix_10s_full_model_matches_reference(dev, golden, precision):
     """BASELINE configs[0] end to end: the REAL reference demix_pytorch_optimized (full MDX23C vocals
     config, 10 s seed-0 mix, 13 chunks, batch_size 1; tests/golden/make_golden.py --only demix_full)
-    against sesa.demix.demix_pytorch_optimized on the device: RMS <= 1e-4, identical progress lines."""
+    against sesa.demix.demix_pytorch_optimized on the device: RMS <= 1e-4, identical progress lines --
+    in the parity precision and in the fp16 TFC-conv precision the headline bench runs."""
     from sesa.backend import create_inference_session
     from sesa.demix import demix_pytorch_optimized
     g = golden("demix_full_10s.npz")
-    m, c = _model("config_vocals_mdx23c.yaml", "unit")
+    m, c = _model("config_vocals_mdx23c.yaml", "unit", precision=precision)
     be = create_inference_session(m, device="cuda:0")
+    m.set_precision(precision)
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
         out = demix_pytorch_optimized(c, be, g["mix"], "cuda:0")
@@ -220,17 +223,18 @@ def test_config0_demix_10s_full_model_matches_reference(dev, golden):
     assert prog == list(g["progress"])
     for k in ("vocals", "other"):
         err = rms(out[k], g[k])
-        print(f"configs[0] 10 s {k}: rms {err:.3e} (ref rms {rms(g[k], 0):.3e})")
+        print(f"configs[0] 10 s {k} ({precision}): rms {err:.3e} (ref rms {rms(g[k], 0):.3e})")
         assert out[k].shape == g[k].shape == (2, 441000) and err <= RMS_GATE
 
 
-def test_full_size_4min_properties(dev):
+@pytest.mark.parametrize("precision", ["bf16x3", "fp16"])
+def test_full_size_4min_properties(dev, precision):
     """configs[1] at full size (4-min track, full vocals config, 169 chunks): the sharded path at world 1
     equals demix_device bit-for-bit, the stems are finite and shaped [2, 2, L], and the two stems
     are not degenerate (size-independent properties; the oracle would need ~17 min of CPU)."""
     from sesa.demix import demix_device
     from sesa.parallel import demix_sharded
-    m, c = _model("config_vocals_mdx23c.yaml", "unit")
+    m, c = _model("config_vocals_mdx23c.yaml", "unit", precision=precision)
     L = 240 * 44100
     rng = np.random.default_rng(0)
     mix = torch.from_numpy((0.1 * rng.standard_normal((2, L))).astype(np.float32)).to(dev)

@@ -74,6 +74,7 @@ def main(fetch_dir, write_dir, substr, out=None, kclass=None):
         res["kernel_class"] = kclass
         res["src_sha16"] = bench.kernel_sources_sha16(kclass)
         res["git_sha"] = os.environ.get("GIT_SHA", "unknown")
+        res["precision"] = os.environ.get("SESA_PMC_PRECISION", "bf16x3")
     print(json.dumps(res, indent=1))
     if out:
         with open(out, "w") as fo:
