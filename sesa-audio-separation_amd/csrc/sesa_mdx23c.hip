@@ -508,7 +508,9 @@ struct Fwd {
   // Input of a TFC 3x3 conv (norm + GELU of `a` [++ `b`]): the raw normalised sources when the conv
   // kernel fuses the activation into its staging (T >= 32 levels), else one act_split pass.
   GemmIn conv3_input(Tensor a, Tensor b, const Norm* nrm, int T, int F, const ConvW& w) {
-    if (conv3x3_fused_act_ok(T, a.C + (b.C > 0 ? b.C : 0), w.C_out))
+    // (the fp16 convs take act_split's fp16 plane: fusing the GELU into their staging measured 2.4 %
+    // slower end to end -- profiles/r03_f16ab_*.json -- with a third of the MFMA work left to hide it under)
+    if (!w.f16 && conv3x3_fused_act_ok(T, a.C + (b.C > 0 ? b.C : 0), w.C_out))
       return input(a, b, SRC_NORM_GELU, SRC_NORM_GELU, nrm, T, F);
     return w.f16 ? act16(a, b, nrm, T, F) : act(a, b, nrm, T, F);
   }

@@ -473,19 +473,31 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 // the activation rounded once to fp16 (one A image: act_split's fp16 plane, or the fused staging's fp16
 // pack) against the fp16 weight image (F16 = 1, one pass) or its fp16 hi + lo pair (F16 = 2, two
 // passes: the weights to ~2^-22); the fused 1x1 shortcut chunks stay bf16x3.
+// MI4 (F16 = 1, pre-activated input): 32-row tiles, each wave 4 output rows x 64 channels (128
+// accumulators), main loop dx-major -- per dx the MI + 2 = 6 halo-row A fragments are read once and serve
+// the 3 dy taps (4 x 2 MFMAs each) -- so 0.5 LDS fragment reads per MFMA instead of 1.  A stage then
+// holds only the images the mode reads (one A, one W: 55 KB); the shortcut stages keep their bf16 hi / lo
+// layout (78 KB), so a stage is the larger of the two.
 constexpr int kActMaxC = 1024;
-template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0>
+template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0, bool MI4 = false>
 __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   static_assert(F16 == 0 || X3, "the fp16 modes keep the shortcut chunks bf16x3");
+  static_assert(!MI4 || (F16 == 1 && !ACT), "MI4: fp16 single pass on pre-activated planes");
   constexpr bool ALO = X3 && F16 == 0;  // main chunks read an A lo image
   constexpr bool WLO = X3 && F16 != 1;  // main chunks read a W lo image
   constexpr int NT = 512;
-  constexpr int TM = 16, WM = 8, MI = 2, NI = 2, BN = 64;
+  constexpr int MI = MI4 ? 4 : 2;
+  constexpr int TM = 8 * MI, WM = 8, NI = 2, BN = 64;
   constexpr int HT = TM + 2, HW = kTF + 2, NPOS = HT * HW;
   constexpr int A_BYTES = NPOS * 32;           // one (hi or lo) image
   constexpr int W_BYTES = 9 * BN * 32;
   constexpr int W1_BYTES = BN * 32;
-  constexpr int STAGE = 2 * A_BYTES + 2 * W_BYTES;
+  // main stage: [A hi][A lo if ALO][W hi][W lo if WLO]; shortcut stage: [A hi][A lo][W1 hi][W1 lo]
+  constexpr int WOFF_M = (ALO ? 2 : 1) * A_BYTES;
+  constexpr int WOFF_X = 2 * A_BYTES;
+  constexpr int STAGE_M = WOFF_M + (WLO ? 2 : 1) * W_BYTES;
+  constexpr int STAGE_X = XTRA ? WOFF_X + 2 * W1_BYTES : 0;
+  constexpr int STAGE = MI4 ? (STAGE_M > STAGE_X ? STAGE_M : STAGE_X) : 2 * A_BYTES + 2 * W_BYTES;
   // (one LDS array: the ACT affine table sits past the two stages)
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (ACT ? 2 * kActMaxC * 4 : 0)];
   float* act_sc = reinterpret_cast<float*>(smem + 2 * STAGE);
@@ -550,7 +562,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     });
   };
   auto store_w = [&](char* stg) {
-    u32x4* wdst = reinterpret_cast<u32x4*>(stg + 2 * A_BYTES);
+    u32x4* wdst = reinterpret_cast<u32x4*>(stg + (MI4 ? WOFF_M : 2 * A_BYTES));
     Unroll<0, W_ITEMS>::run([&](auto I) {
       const int e = min(tid + I * NT, W16 - 1);  // duplicates write identical values
       wdst[e] = wreg[I];
@@ -680,7 +692,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   auto store_ext = [&](char* stg) {
     char* A_hi = stg;
     char* A_lo = stg + A_BYTES;
-    u32x4* wdst = reinterpret_cast<u32x4*>(stg + 2 * A_BYTES);
+    u32x4* wdst = reinterpret_cast<u32x4*>(stg + WOFF_X);
     wdst[min(tid, W1_16 - 1)] = wreg[0];
     Unroll<0, X_ITEMS>::run([&](auto I) {
       constexpr int i = decltype(I)::value;
@@ -708,7 +720,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     constexpr bool rd_bl = decltype(EXT)::value ? X3 : WLO;
     const char* A_hi = stg;
     const char* A_lo = stg + A_BYTES;
-    const char* W_hi = stg + 2 * A_BYTES;
+    const char* W_hi = stg + (decltype(EXT)::value || !MI4 ? 2 * A_BYTES : WOFF_M);
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int row = wm * MI + i;
@@ -756,6 +768,43 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     char* cur = smem + (kc & 1) * STAGE;
     char* nxt = smem + ((kc + 1) & 1) * STAGE;
     Frags fr[2];
+    if constexpr (MI4) {
+      // dx-major: the 6 halo-row A fragments of column shift dx, then the 3 dy taps (B double-buffered)
+      const char* Wm = cur + WOFF_M;
+      auto read_b = [&](bf16x8* bq, int tap) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int p = tap * BN + j * 32 + l32;
+          bq[j] = *reinterpret_cast<const bf16x8*>(Wm + p * 32 + ((h ^ ((p >> 3) & 1)) << 4));
+        }
+      };
+      bf16x8 bq[2][NI];
+      read_b(bq[0], 0);
+      Unroll<0, 3>::run([&](auto DX) {
+        constexpr int dx = decltype(DX)::value;
+        bf16x8 ar[MI + 2];
+#pragma unroll
+        for (int r = 0; r < MI + 2; ++r) {
+          const int p = (wm * MI + r) * HW + l32 + dx;
+          ar[r] = *reinterpret_cast<const bf16x8*>(cur + p * 32 + ((h ^ ((p >> 3) & 1)) << 4));
+        }
+        Unroll<0, 3>::run([&](auto DY) {
+          constexpr int dy = decltype(DY)::value, q = dx * 3 + dy;  // q: order of this tap
+          constexpr int nq = q + 1, ntap = (nq % 3) * 3 + nq / 3;   // the next tap in dx-major order
+          if (nq < 9) read_b(bq[nq & 1], ntap);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) acc[i][j] = mfma32h(ar[i + dy], bq[q & 1][j], acc[i][j]);
+          if (q == 1) {
+            store_main(nxt, min(kc + 1, n_main - 1));
+            load_main(min(kc + 2, n_main - 1));
+          }
+        });
+      });
+      __syncthreads();
+      continue;
+    }
     read_frags(fr[0], cur, 0, 0, 0, W_BYTES, kMain);
     if constexpr (!ACT) {
       Unroll<0, 9>::run([&](auto T) {
@@ -2590,6 +2639,12 @@ int set_conv3x3_variant(int v) {
   return prev;
 }
 
+// SESA_CONV_MI4=0: the fp16 single-pass TFC convs on the 16-row tile (A/B of conv3x3_db_kernel<MI4>)
+bool conv3x3_mi4_enabled() {
+  static const bool v = !(getenv("SESA_CONV_MI4") && std::string(getenv("SESA_CONV_MI4")) == "0");
+  return v;
+}
+
 bool tap_bn128_enabled() {
   static const bool v = !(getenv("SESA_TAP_BN128") && std::string(getenv("SESA_TAP_BN128")) == "0");
   return v;
@@ -2732,8 +2787,14 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
     if (act) hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, true, F16V>), grid, dim3(512), 0, st, a);  \
     else hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, false, F16V>), grid, dim3(512), 0, st, a);     \
   } while (0)
-        // xmode 2 = fp16 x fp16 hi/lo weights (F16 = 2), 3 = fp16 single pass (F16 = 1)
-        if (a.x_chunks > 0) {
+        // xmode 2 = fp16 x fp16 hi/lo weights (F16 = 2), 3 = fp16 single pass (F16 = 1; on pre-activated
+        // planes the 32-row MI4 tile unless SESA_CONV_MI4=0)
+        if (xmode == 3 && !act && conv3x3_mi4_enabled()) {
+          const dim3 g32((unsigned)(((a.T_out + 31) / 32) * (a.F_out / kTF) * ((a.n_cols + 63) / 64)), 1u,
+                         (unsigned)batch);
+          if (a.x_chunks > 0) hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true>), g32, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0, false, 1, true>), g32, dim3(512), 0, st, a);
+        } else if (a.x_chunks > 0) {
           if (xmode == 3) SESA_DB(true, true, 1);
           else if (xmode == 2) SESA_DB(true, true, 2);
           else if (x3) SESA_DB(true, true, 0);
