@@ -22,12 +22,22 @@ timeout -k 10 700 bash tools/pmc_refresh.sh htdemucs \
   > $O/pmc_htdemucs.log 2>&1
 step pmc bs_roformer
 timeout -k 10 700 bash tools/pmc_refresh.sh bs_roformer "tokgemm=tok_gemm" > $O/pmc_bsr.log 2>&1
+step pmc scnet
+timeout -k 10 700 bash tools/pmc_refresh.sh scnet "lstm=scn_lstm_mfma" > $O/pmc_scnet.log 2>&1
 mkdir -p $O/pmc
 cp gpurun_out/pmc_*.json $O/pmc/ 2>/dev/null || true
 cp $O/pmc/pmc_*.json profiles/          # bench.py below reads the fresh, sha-matched summaries
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step mdx23c
 timeout -k 10 400 python bench.py > $O/bench_mdx23c.json 2> $O/bench_mdx23c.err
+step mdx23c bf16x3
+timeout -k 10 300 python bench.py --precision bf16x3 --no-cpu-baseline > $O/bench_mdx23c_bf16x3.json 2> $O/bench_mdx23c_bf16x3.err
+step mdx23c fp16w2
+timeout -k 10 300 python bench.py --precision fp16w2 --no-cpu-baseline > $O/bench_mdx23c_fp16w2.json 2> $O/bench_mdx23c_fp16w2.err
+step mdx23c fp16 16-row tile
+timeout -k 10 300 env SESA_CONV_MI4=0 python bench.py --no-cpu-baseline > $O/bench_mdx23c_fp16_mi2.json 2> $O/bench_mdx23c_fp16_mi2.err
+step mdx23c fp16 again
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_mdx23c_fp16_again.json 2> $O/bench_mdx23c_fp16_again.err
 step mdx23c bf16
 timeout -k 10 300 python bench.py --precision bf16 --no-cpu-baseline > $O/bench_mdx23c_bf16.json 2> $O/bench_mdx23c_bf16.err
 step bs_roformer
