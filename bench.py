@@ -107,8 +107,17 @@ def kernel_sources_sha16(kclass):
 def default_precision(model):
     """MDX23C: the fp16 TFC-conv precision (SESA_PREC_F16: the T >= 32 3x3 convs on fp16 MFMA, the rest
     bf16x3; 5.1e-5 RMS vs the reference's full-chunk golden, inside the 1e-4 north_star gate -- the line
-    carries the measured value); every other model and the ensemble: bf16x3."""
-    return "fp16" if model == "mdx23c" else "bf16x3"
+    carries the measured value) -- also for the MDX23C member of the ensemble; every other model (and the
+    other ensemble members, build_model) bf16x3."""
+    return "fp16" if model in ("mdx23c", "ensemble") else "bf16x3"
+
+
+# kernel classes whose kernels run in the MDX23C precision mode; every other class is bf16x3 in the fp16 modes
+MDX_CLASSES = ("conv3x3", "conv1x1", "down", "up", "tdf", "act")
+
+
+def class_precision(kclass, precision):
+    return precision if (kclass in MDX_CLASSES or not precision.startswith("fp16")) else "bf16x3"
 
 
 def pmc_traffic(kclass, precision="bf16x3"):
@@ -441,7 +450,7 @@ def main():
     note = f"2.5 PF/s dense bf16/fp16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
     if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
         peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
-    traffic, traffic_src = pmc_traffic(kclass, args.precision)
+    traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision))
     alg_bytes = None
     if kclass == "conv3x3":
         m0, cfg0, _ = members[0]

@@ -17,9 +17,13 @@ def _vocals_cfg():
 
 
 def test_default_precision():
-    assert bench.default_precision("mdx23c") == "fp16"
-    for m in ("bs_roformer", "htdemucs", "scnet", "ensemble"):
+    assert bench.default_precision("mdx23c") == bench.default_precision("ensemble") == "fp16"
+    for m in ("bs_roformer", "htdemucs", "scnet"):
         assert bench.default_precision(m) == "bf16x3"
+    # PMC stamps: only the MDX23C classes run in the fp16 mode
+    assert bench.class_precision("conv3x3", "fp16") == "fp16"
+    assert bench.class_precision("tokgemm", "fp16") == "bf16x3"
+    assert bench.class_precision("tokgemm", "bf16") == "bf16"
 
 
 def test_conv3x3_alg_bytes_by_precision():

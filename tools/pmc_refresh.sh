@@ -10,12 +10,14 @@ M=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 # the precision the default bench line of this model runs in (bench.py default_precision), stamped into the
 # summaries (bench.py reports traffic only for a run in the same mode)
-export SESA_PMC_PRECISION=$(python3 -c "import bench; print(bench.default_precision('$M'))")
-B="python3 bench.py --model $M --steps 1 --warmup 0 --no-cpu-baseline --no-parity --precision $SESA_PMC_PRECISION"
+P=$(python3 -c "import bench; print(bench.default_precision('$M'))")
+B="python3 bench.py --model $M --steps 1 --warmup 0 --no-cpu-baseline --no-parity --precision $P"
 O=gpurun_out
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_${M}_f -o run -- $B > $O/pmc_${M}_f.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_${M}_w -o run -- $B > $O/pmc_${M}_w.log 2>&1
 for spec in "$@"; do
   K=${spec%%=*}; S=${spec#*=}
-  python3 tools/pmc_traffic.py $O/pmc_${M}_f $O/pmc_${M}_w "$S" $O/pmc_${K}.json $K
+  # stamped with the precision that class's kernels ran in (bench.py class_precision)
+  SESA_PMC_PRECISION=$(python3 -c "import bench; print(bench.class_precision('$K', '$P'))") \
+    python3 tools/pmc_traffic.py $O/pmc_${M}_f $O/pmc_${M}_w "$S" $O/pmc_${K}.json $K
 done
