@@ -43,8 +43,10 @@ def _oracle_member(kind, cfg_name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("method", ["avg_wave", "median_fft"])
-def test_ensemble_separate_matches_oracle_composition(method):
+@pytest.mark.parametrize("method,mdx_precision", [("avg_wave", "bf16x3"), ("median_fft", "bf16x3"),
+                                                  ("avg_wave", "fp16")])
+def test_ensemble_separate_matches_oracle_composition(method, mdx_precision):
+    """mdx_precision: the MDX23C member's precision (fp16 TFC convs as in the configs[4] bench line)."""
     from oracle import demix as odm
     from oracle import ensemble as oen
     from sesa.ensemble import ensemble_separate
@@ -58,6 +60,8 @@ def test_ensemble_separate_matches_oracle_composition(method):
             ref_stems.append(odm.demix(cfg, fwd, mix)["vocals"])
         m, c = get_model_from_config(kind, os.path.join(CONFIGS, cfg_name))
         m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in raw.items()}, strict=True)
+        if kind == "mdx23c":
+            m.set_precision(mdx_precision)
         members.append((c, m))
     out, stems = ensemble_separate(members, torch.from_numpy(mix).to(dev), "vocals", method, rank=0, world=1,
                                    exec_batch=4)
