@@ -310,8 +310,8 @@ def build_model(name, precision):
     cfg_path = os.path.join(CFG_DIR, MODELS[name][0])
     model, cfg = get_model_from_config(name, cfg_path)
     model.load_state_dict(synth_state_dict(model) if name == "mdx23c" else synth_weights(model), strict=True)
-    if precision.startswith("fp16") and name != "mdx23c":
-        precision = "bf16x3"  # the fp16 TFC-conv modes are MDX23C's; other members run their parity precision
+    if precision not in getattr(model, "_precisions", ()):
+        precision = "bf16x3"  # (e.g. fp16w2 is MDX23C's only; SCNet / HTDemucs have no fp16 mode)
     model.set_precision(precision)
     return model, cfg, cfg_path
 

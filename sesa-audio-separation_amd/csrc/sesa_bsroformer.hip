@@ -328,7 +328,8 @@ extern "C" int sesa_bsr_create(const sesa_bsr_config* cfg, sesa_bsr** out) {
                "bsr: mask_estimator_depth 1..4");
   SESA_REQUIRE(!c.mel || (c.freq_indices && c.n_freq_indices > 0), SESA_ERR_INVALID, "bsr: mel needs freq_indices");
   SESA_REQUIRE(c.mel || c.mask_estimator_depth >= 2, SESA_ERR_INVALID, "bsr: BS-Roformer mask MLP needs depth >= 2");
-  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16, SESA_ERR_INVALID, "bsr: precision");
+  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16 || c.precision == SESA_PREC_F16,
+               SESA_ERR_INVALID, "bsr: precision");
   sesa_bsr* m = new sesa_bsr();
   m->cfg = c;
   m->fpb.assign(c.freqs_per_bands, c.freqs_per_bands + c.n_bands);
@@ -442,6 +443,7 @@ extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
   const int dim = c.dim, inner = m->inner;
   std::vector<uint16_t> blob;
   std::vector<float> bias;
+  const bool f16p = c.precision == SESA_PREC_F16;  // QKV / FF1 / FF2 weight images in fp16 (one-pass Linears)
   std::vector<float2> rope;
   // band split: W' = W diag(gamma) (RMSNorm folded)
   m->band.groups.clear();
@@ -469,7 +471,7 @@ extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
         [&](int n, int k) {
           return (n < 3 * inner ? Wqkv[(int64_t)n * dim + k] : Wg[(int64_t)(n - 3 * inner) * dim + k]) * ga[k];
         },
-        true, [&](int n) { return n < 3 * inner ? 0.f : bg[n - 3 * inner]; }, blob, bias);
+        true, [&](int n) { return n < 3 * inner ? 0.f : bg[n - 3 * inner]; }, blob, bias, f16p);
     g.x_off = 0;
     g.o_off = 0;
     L.qkv.groups = {g};
@@ -482,14 +484,14 @@ extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
     const auto& b1 = P(m, p + ".1.net.1.bias");
     const auto& gf = P(m, p + ".1.net.0.gamma");
     g = pack_group(m->ff, dim, [&](int n, int k) { return W1[(int64_t)n * dim + k] * gf[k]; }, true,
-                   [&](int n) { return b1[n]; }, blob, bias);
+                   [&](int n) { return b1[n]; }, blob, bias, f16p);
     g.x_off = g.o_off = 0;
     L.ff1.groups = {g};
     const auto& W2 = P(m, p + ".1.net.4.weight");
     const auto& b2 = P(m, p + ".1.net.4.bias");
     const int ffd = m->ff;
     g = pack_group(dim, ffd, [&](int n, int k) { return W2[(int64_t)n * ffd + k]; }, true, [&](int n) { return b2[n]; },
-                   blob, bias);
+                   blob, bias, f16p);
     g.x_off = g.o_off = 0;
     L.ff2.groups = {g};
     // rotary table from this layer's freqs: angle = fp32(pos * freq) (the library's fp32 einsum)
@@ -682,7 +684,10 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
   float* XG = reinterpret_cast<float*>(ws + pl.xg);
   float* H2 = reinterpret_cast<float*>(ws + pl.h2);
   float* MASKG = reinterpret_cast<float*>(ws + pl.maskg);
-  const int x3 = c.precision == SESA_PREC_BF16X3 ? 1 : 0;
+  // SESA_PREC_F16: the QKV / FF1 / FF2 Linears one fp16 pass (fp16 A planes, fp16 weight images; tok_gemm
+  // x3 = 2); band split, attention, out-projection and mask MLPs bf16x3
+  const bool f16 = c.precision == SESA_PREC_F16;
+  const int x3 = c.precision == SESA_PREC_BF16 ? 0 : 1;
   const int ch = c.audio_channels, dim = c.dim;
   const int T = m->T, nb = m->nb;
   const int64_t Mtok = (int64_t)B * T * nb;
@@ -697,10 +702,10 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
   SESA_CHECK_LAUNCH();
   profile_end(tok, st, SESA_KCLASS_STFT, 4.0 * B * ch * ((double)c.chunk_size + (double)T * m->F * 2));
 
-  auto gemm = [&](const TokGemmArgs& a, const Gemm& gm, int64_t rows) {
+  auto gemm = [&](const TokGemmArgs& a, const Gemm& gm, int64_t rows, bool h16 = false) {
     if (rc) return;
     void* t0 = profile_begin(st);
-    rc = launch_tok_gemm(a, x3, st);
+    rc = launch_tok_gemm(a, h16 ? 2 : x3, st);
     profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(gm, rows));
   };
   const int64_t rowsBT = (int64_t)B * T;
@@ -730,8 +735,9 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
   auto split_x = [&]() {
     if (rc) return;
     void* t0 = profile_begin(st);
-    rc = launch_tok_split(X, dim, Mtok, dim, XPhi, XPlo, dim, RSC, st);
-    profile_end(t0, st, SESA_KCLASS_ACT, (double)Mtok * dim * (x3 ? 8.0 : 6.0) + 4.0 * Mtok);
+    rc = f16 ? launch_tok_split_f16(X, dim, Mtok, dim, XPhi, dim, RSC, st)
+             : launch_tok_split(X, dim, Mtok, dim, XPhi, XPlo, dim, RSC, st);
+    profile_end(t0, st, SESA_KCLASS_ACT, (double)Mtok * dim * (x3 && !f16 ? 8.0 : 6.0) + 4.0 * Mtok);
   };
   auto pre = [&](TokGemmArgs& a, const uint16_t* hi, const uint16_t* lo, int64_t ld) {
     a.x = nullptr;
@@ -745,7 +751,7 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
   // fp32 QKV buffer is faster -- 115.3x vs 110.5x real-time, attention 356 vs 410 ms and token GEMMs 1597
   // vs 1634 ms per step, twice each (profiles/r03_bsr_qkv_planes_ab_*.json).
   static const bool qkv_planes = getenv("SESA_BSR_QKV_PLANES") && std::string(getenv("SESA_BSR_QKV_PLANES")) == "1";
-  const bool qp = qkv_planes && m->qkv_ld % 8 == 0 && c.dim_head % 8 == 0;
+  const bool qp = qkv_planes && !f16 && m->qkv_ld % 8 == 0 && c.dim_head % 8 == 0;
   uint16_t* QKVhi = reinterpret_cast<uint16_t*>(QKV);
   uint16_t* QKVlo = x3 ? QKVhi + (int64_t)M * m->qkv_ld : nullptr;
   for (size_t li = 0; li < m->layers.size(); ++li) {
@@ -754,7 +760,7 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
     split_x();
     {
       TokGemmArgs a = gemm_args(m, L.qkv, X, dim, QKV, m->qkv_ld, M);
-      pre(a, XPhi, XPlo, dim);
+      pre(a, XPhi, f16 ? XPhi : XPlo, dim);  // (fp16: the kernel stages a second copy it does not read)
       a.rownorm = 1;
       a.rope = m->d_rope + L.rope_off;
       a.rope_cols = 2 * m->inner;
@@ -765,7 +771,7 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
         a.out_hi = QKVhi;
         a.out_lo = QKVlo;
       }
-      gemm(a, L.qkv, M);
+      gemm(a, L.qkv, M, f16);
     }
     if (rc) return rc;
     {
@@ -812,18 +818,18 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
     split_x();
     {
       TokGemmArgs a = gemm_args(m, L.ff1, X, dim, H, m->ff, M);
-      pre(a, XPhi, XPlo, dim);
+      pre(a, XPhi, f16 ? XPhi : XPlo, dim);
       a.rownorm = 1;
       a.act = TOK_ACT_GELU;
       a.out_hi = Hhi;
-      a.out_lo = Hlo;
-      gemm(a, L.ff1, M);
+      a.out_lo = f16 ? nullptr : Hlo;  // fp16: one plane
+      gemm(a, L.ff1, M, f16);
     }
     {
       TokGemmArgs a = gemm_args(m, L.ff2, H, m->ff, X, dim, M);
-      pre(a, Hhi, Hlo, m->ff);
+      pre(a, Hhi, f16 ? Hhi : Hlo, m->ff);
       a.residual = X;
-      gemm(a, L.ff2, M);
+      gemm(a, L.ff2, M, f16);
     }
     if (rc) return rc;
     // Mel: Transformer.norm after the last layer of each (time / freq) transformer (:218, :226)

@@ -410,7 +410,8 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
 // cost more than the main loop.  Operands a 32x32 block would gather with a load -> wait round trip
 // each are staged once into the freed LDS by LDS-DMA: the rotary (cos, sin) rows of the tile's tokens
 // (64 KiB), the residual in two 128-row halves (128 KiB each).
-enum : int { EP_RS = 1, EP_ROPE = 2, EP_GELU = 4, EP_RES = 8, EP_SPLIT = 16, EP_RAW = 32, EP_NONE = 64 };
+enum : int { EP_RS = 1, EP_ROPE = 2, EP_GELU = 4, EP_RES = 8, EP_SPLIT = 16, EP_RAW = 32, EP_NONE = 64, EP_F16 = 128 };
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float dpp_xor1(float x) {  // lane ^ 1 (quad_perm [1, 0, 3, 2])
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
@@ -533,17 +534,27 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
       f.bl[j] = *reinterpret_cast<const bf16x8*>(stg + off + W_PLANE);
     }
   };
+  // EP_F16: fp16 A planes x fp16 weight images, one pass (the lo images are staged but not read)
+  constexpr bool F16 = (EP & EP_F16) != 0;
   auto mma = [&](const bf16x8& x, const bf16x8& y, Acc& c) {
-    if constexpr (M16) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, c, 0, 0, 0);
-    else c = mfma32(x, y, c);
+    if constexpr (F16) {
+      const f16x8 xh = __builtin_bit_cast(f16x8, x), yh = __builtin_bit_cast(f16x8, y);
+      if constexpr (M16) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, yh, c, 0, 0, 0);
+      else c = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yh, c, 0, 0, 0);
+    } else {
+      if constexpr (M16) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, c, 0, 0, 0);
+      else c = mfma32(x, y, c);
+    }
   };
   auto mfmas = [&](const Frags& f) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        mma(f.al[i], f.bh[j], acc[i][j]);
-        mma(f.ah[i], f.bl[j], acc[i][j]);
+        if constexpr (!F16) {
+          mma(f.al[i], f.bh[j], acc[i][j]);
+          mma(f.ah[i], f.bl[j], acc[i][j]);
+        }
         mma(f.ah[i], f.bh[j], acc[i][j]);
       }
   };
@@ -651,7 +662,21 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
         v[r] = x;
       }
     }
-    if constexpr ((EP & EP_SPLIT) != 0) {
+    if constexpr ((EP & EP_SPLIT) != 0 && F16) {
+      // one fp16 plane, two columns per 4-byte store by the even lanes
+#pragma unroll
+      for (int r = 0; r < RPB; ++r) {
+        const int m = m0 + row_of(i, r);
+        const uint32_t hb = __builtin_bit_cast(uint16_t, (_Float16)v[r]);
+        const int64_t o = (int64_t)m * a.o_ld + g.o_off + n;
+        const uint32_t hn = dpp_xor1u(hb);  // uniform control flow
+        if (FULL) {
+          if (!(l32 & 1)) *reinterpret_cast<uint32_t*>(a.out_hi + o) = hb | (hn << 16);
+        } else if (m < a.M && n < g.N) {
+          a.out_hi[o] = (uint16_t)hb;
+        }
+      }
+    } else if constexpr ((EP & EP_SPLIT) != 0) {
       // bf16 planes, two columns per 4-byte store: even lanes write the hi pair (n, n + 1), odd
       // lanes the lo pair (n - 1, n)
 #pragma unroll
@@ -996,6 +1021,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // fp32 rows -> bf16 hi / lo planes (+ RMSNorm row scale): one wave per row, f32x4 per lane-step.
+// F16: one fp16 plane (round to nearest even) -- the A operand of the fp16 single-pass Linears.
+template <bool F16>
 __global__ void __launch_bounds__(256) tok_split_kernel(const float* __restrict__ x, int64_t x_ld, int64_t M, int K,
                                                         uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
                                                         int64_t p_ld, float* __restrict__ row_scale) {
@@ -1006,6 +1033,18 @@ __global__ void __launch_bounds__(256) tok_split_kernel(const float* __restrict_
   float ss = 0.f;
   for (int k = lane * 4; k < K; k += 256) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(xr + k);
+    if constexpr (F16) {
+      uint32_t w[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ss = fmaf(v[2 * q], v[2 * q], ss);
+        ss = fmaf(v[2 * q + 1], v[2 * q + 1], ss);
+        w[q] = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v[2 * q]) |
+               ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v[2 * q + 1]) << 16);
+      }
+      *reinterpret_cast<uint2*>(hi + m * p_ld + k) = make_uint2(w[0], w[1]);
+      continue;
+    }
     __bf16 h[4], l[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1026,6 +1065,7 @@ __global__ void __launch_bounds__(256) tok_split_kernel(const float* __restrict_
 
 int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
   SESA_REQUIRE(a.n_groups >= 1 && a.n_tiles_n >= 1 && a.M >= 0, SESA_ERR_INVALID, "tok_gemm: bad grid");
+  SESA_REQUIRE(x3 != 2 || (a.a_hi && !a.conv), SESA_ERR_INVALID, "tok_gemm: the fp16 mode takes pre-split fp16 A");
   SESA_REQUIRE(!(a.out_hi && a.residual) && (a.out_hi || a.out), SESA_ERR_INVALID,
                "tok_gemm: split epilogue takes no residual; an output is required");
   if (a.M == 0) return SESA_OK;
@@ -1064,11 +1104,13 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
     // the specialised forms); SESA_TOKGEMM_GLDS=0 selects the register-staged kernel for A/B runs
     static const int glds = getenv("SESA_TOKGEMM_GLDS") ? atoi(getenv("SESA_TOKGEMM_GLDS")) : 1;
     int ep = -1;
-    if (glds && x3 && a.k8 && a.a_ld % 8 == 0 && !a.glu && !a.conv && a.o_ld % 4 == 0 &&
+    // x3 == 2: fp16 A planes x fp16 weight images, one pass (SESA_PREC_F16 Linears; LDS-DMA kernel only)
+    const bool f16 = x3 == 2;
+    if ((glds || f16) && x3 && a.k8 && a.a_ld % 8 == 0 && !a.glu && !a.conv && a.o_ld % 4 == 0 &&
         (a.act == TOK_ACT_NONE || a.act == TOK_ACT_GELU) && (!a.rope || (a.dim_head == 64 && !a.residual)) &&
-        (!a.out_hi || a.out_lo) && (!a.residual || a.n4)) {
+        (!a.out_hi || a.out_lo || f16) && (!a.residual || a.n4)) {
       ep = (a.rownorm ? EP_RS : 0) | (a.rope ? EP_ROPE : 0) | (a.act == TOK_ACT_GELU ? EP_GELU : 0) |
-           (a.residual ? EP_RES : 0) | (a.out_hi ? EP_SPLIT : 0);
+           (a.residual ? EP_RES : 0) | (a.out_hi ? EP_SPLIT : 0) | (f16 ? EP_F16 : 0);
     }
     const dim3 gbig((unsigned)(((a.M + 255) / 256) * ((a.n_tiles_n + 1) / 2)), (unsigned)a.n_groups);
     static const int m16 = getenv("SESA_TOKGEMM_M16") ? atoi(getenv("SESA_TOKGEMM_M16")) : 1;
@@ -1083,8 +1125,12 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
       case EP_GELU | EP_SPLIT: SESA_GLDS(EP_GELU | EP_SPLIT) break;
       case EP_SPLIT: SESA_GLDS(EP_SPLIT) break;                       // q / k / v planes for attention
       case EP_RS | EP_ROPE | EP_SPLIT: SESA_GLDS(EP_RS | EP_ROPE | EP_SPLIT) break;
+      case EP_F16 | EP_RS | EP_GELU | EP_SPLIT: SESA_GLDS(EP_F16 | EP_RS | EP_GELU | EP_SPLIT) break;  // FF1
+      case EP_F16 | EP_RES: SESA_GLDS(EP_F16 | EP_RES) break;                                         // FF2
+      case EP_F16 | EP_RS | EP_ROPE: SESA_GLDS(EP_F16 | EP_RS | EP_ROPE) break;                       // QKV
       default: ep = -1;
     }
+    SESA_REQUIRE(!f16 || ep >= 0, SESA_ERR_INVALID, "tok_gemm: no fp16 kernel for this epilogue / shape");
 #undef SESA_GLDS
     if (ep >= 0) {
       SESA_CHECK_LAUNCH();
@@ -1111,8 +1157,20 @@ int launch_tok_split(const float* x, int64_t x_ld, int64_t M, int K, uint16_t* h
                    (M + 3) / 4 < (1ll << 31),
                SESA_ERR_INVALID, "tok_split: bad shape");
   if (M == 0) return SESA_OK;
-  hipLaunchKernelGGL(tok_split_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, x, x_ld, M, K, hi, lo, p_ld,
-                     row_scale);
+  hipLaunchKernelGGL(tok_split_kernel<false>, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, x, x_ld, M, K, hi, lo,
+                     p_ld, row_scale);
+  SESA_CHECK_LAUNCH();
+  return SESA_OK;
+}
+
+int launch_tok_split_f16(const float* x, int64_t x_ld, int64_t M, int K, uint16_t* hi, int64_t p_ld, float* row_scale,
+                         hipStream_t st) {
+  SESA_REQUIRE(x && hi && M >= 0 && K > 0 && K % 4 == 0 && x_ld % 4 == 0 && p_ld % 4 == 0 && p_ld >= K &&
+                   (M + 3) / 4 < (1ll << 31),
+               SESA_ERR_INVALID, "tok_split_f16: bad shape");
+  if (M == 0) return SESA_OK;
+  hipLaunchKernelGGL(tok_split_kernel<true>, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, x, x_ld, M, K, hi,
+                     nullptr, p_ld, row_scale);
   SESA_CHECK_LAUNCH();
   return SESA_OK;
 }

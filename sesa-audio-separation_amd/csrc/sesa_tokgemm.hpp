@@ -85,6 +85,9 @@ struct TokGemmArgs {
 // gets sqrt(K) / max(||x_m||_2, 1e-12) (the RMSNorm scale of rownorm).  lo null: hi only.
 int launch_tok_split(const float* x, int64_t x_ld, int64_t M, int K, uint16_t* hi, uint16_t* lo, int64_t p_ld,
                      float* row_scale, hipStream_t st);
+// the same rows as ONE fp16 plane (round to nearest even): A of the fp16 single-pass Linears (tok_gemm x3 = 2)
+int launch_tok_split_f16(const float* x, int64_t x_ld, int64_t M, int K, uint16_t* hi, int64_t p_ld, float* row_scale,
+                         hipStream_t st);
 
 // Flash attention over strided sequences of a token-major qkv buffer.
 // token(seq, p) = (seq / sdiv) * smul_a + (seq % sdiv) * smul_b + p * pstride
@@ -140,9 +143,10 @@ struct Gemm {          // one packed (possibly grouped) GEMM
 };
 
 // Pack W[n][k] (row accessor) of an N x K GEMM for one group; returns the TokGroup with w_off/b_off set.
+// f16: the image as fp16 hi = fp16(v), lo = fp16(v - hi) (the fp16 single-pass Linears read hi only).
 template <class RowFn, class BiasFn>
 TokGroup pack_group(int N, int K, RowFn row_val, bool has_bias, BiasFn bias_val, std::vector<uint16_t>& blob,
-                    std::vector<float>& bias) {
+                    std::vector<float>& bias, bool f16 = false) {
   TokGroup g{};
   g.K = K;
   g.N = N;
@@ -161,6 +165,12 @@ TokGroup pack_group(int N, int K, RowFn row_val, bool has_bias, BiasFn bias_val,
           const int k = kc * kTokBK + kk;
           const float v = (n < N && k < K) ? row_val(n, k) : 0.f;
           const int64_t o = (int64_t)r * kTokBK + (((kk >> 3) ^ ((r >> 2) & 3)) << 3) + (kk & 7);
+          if (f16) {
+            const _Float16 hh = (_Float16)v;
+            hi[o] = __builtin_bit_cast(uint16_t, hh);
+            lo[o] = __builtin_bit_cast(uint16_t, (_Float16)(v - (float)hh));
+            continue;
+          }
           const uint16_t h = f2bf(v);
           hi[o] = h;
           lo[o] = f2bf(v - bf2f(h));

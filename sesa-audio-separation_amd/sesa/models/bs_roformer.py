@@ -26,6 +26,10 @@ class BSRoformer(NativeModule):
     """Reference-compatible BS-Roformer module (torch.nn.Module) backed by the native HIP forward."""
 
     _prefix = "bsr"
+    # fp16: the QKV / FF Linears on one fp16 MFMA pass (include/sesa.h SESA_PREC_F16; 7e-6 emulated on the
+    # full vocals chunk); the band split, attention, out-projection and mask MLPs stay bf16x3
+    _precisions = ("bf16x3", "bf16", "fp16")
+    _prec_codes = {"bf16x3": N.SESA_PREC_BF16X3, "bf16": N.SESA_PREC_BF16, "fp16": N.SESA_PREC_F16}
 
     def __init__(self, dim, *, depth, stereo=False, num_stems=1, time_transformer_depth=2, freq_transformer_depth=2,
                  linear_transformer_depth=0, freqs_per_bands=DEFAULT_FREQS_PER_BANDS, dim_head=64, heads=8,
@@ -101,7 +105,7 @@ class BSRoformer(NativeModule):
         fpb = (ctypes.c_int * len(self.freqs_per_bands))(*self.freqs_per_bands)
         fidx = (ctypes.c_int * max(1, len(self._freq_indices)))(*self._freq_indices)
         c = N.SesaBsrConfig(chunk_size=int(chunk), n_bands=len(self.freqs_per_bands), freqs_per_bands=fpb,
-                            precision=N.SESA_PREC_BF16 if self.precision == "bf16" else N.SESA_PREC_BF16X3,
+                            precision=self._prec_codes[self.precision],
                             mel=1 if self._mel else 0, n_freq_indices=len(self._freq_indices), freq_indices=fidx,
                             **self._kw)
         self._keep = (fpb, fidx)   # ctypes arrays must outlive the create call

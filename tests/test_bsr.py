@@ -193,3 +193,21 @@ def test_full_size_4min_properties(dev):
     assert torch.isfinite(a).all().item()
     assert torch.equal(a, b)
     assert float(a[0].std()) > 1e-5 and float((a[0, 0] - a[0, 1]).abs().max()) > 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fixture,cfg_name,mel", [("bsr_small.npz", "config_bs_roformer_small.yaml", False),
+                                                  ("bsr_full_chunk.npz", "config_bs_roformer_vocals.yaml", False),
+                                                  ("mbr_small.npz", "config_mel_band_roformer_small.yaml", True),
+                                                  ("mbr_full_chunk.npz", "config_mel_band_roformer_vocals.yaml", True)])
+def test_forward_fp16_linears_match_reference(golden, dev, fixture, cfg_name, mel):
+    """SESA_PREC_F16: the QKV / FF1 / FF2 Linears on one fp16 MFMA pass (fp16 A planes from the RMSNorm split
+    and the FF1 epilogue, fp16 weight images); same 1e-4 per-sample RMS gate against the reference goldens.
+    (CPU emulation with every Linear in fp16, tests/emulation/emulate_bsr_fp16.py: 7.0e-6 on the full chunk.)"""
+    g = golden(fixture)
+    m, _ = (_mel_model if mel else _model)(cfg_name, str(g["affine"]), precision="fp16")
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    assert y.shape == g["y"].shape
+    err = rms(y, g["y"])
+    print(f"{fixture} (fp16 Linears): rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    assert np.isfinite(y).all() and err <= RMS_GATE
