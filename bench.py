@@ -116,8 +116,15 @@ def default_precision(model):
 MDX_CLASSES = ("conv3x3", "conv1x1", "down", "up", "tdf", "act")
 
 
-def class_precision(kclass, precision):
-    return precision if (kclass in MDX_CLASSES or not precision.startswith("fp16")) else "bf16x3"
+def class_precision(kclass, precision, model="mdx23c"):
+    """The precision a kernel class's launches run in for a bench line of `model` in `precision` (the PMC
+    stamp bench.py compares): the MDX23C classes follow the MDX23C mode; the token GEMMs follow it for
+    BS-Roformer's fp16 Linears (bs_roformer, ensemble); every other class is bf16x3 in the fp16 modes."""
+    if not precision.startswith("fp16") or kclass in MDX_CLASSES:
+        return precision
+    if kclass == "tokgemm" and precision == "fp16" and model in ("bs_roformer", "ensemble"):
+        return "fp16"
+    return "bf16x3"
 
 
 def pmc_traffic(kclass, precision="bf16x3"):
@@ -450,7 +457,7 @@ def main():
     note = f"2.5 PF/s dense bf16/fp16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
     if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
         peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
-    traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision))
+    traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model))
     alg_bytes = None
     if kclass == "conv3x3":
         m0, cfg0, _ = members[0]

@@ -23,6 +23,8 @@ def test_default_precision():
     # PMC stamps: only the MDX23C classes run in the fp16 mode
     assert bench.class_precision("conv3x3", "fp16") == "fp16"
     assert bench.class_precision("tokgemm", "fp16") == "bf16x3"
+    assert bench.class_precision("tokgemm", "fp16", "bs_roformer") == "fp16"
+    assert bench.class_precision("hconv", "fp16", "ensemble") == "bf16x3"
     assert bench.class_precision("tokgemm", "bf16") == "bf16"
 
 
@@ -59,5 +61,5 @@ def test_bench_maps_fp16_to_parity_for_other_members(name, monkeypatch):
     import sesa.utils
     monkeypatch.setattr(sesa.utils, "get_model_from_config", lambda n, p: (Fake(), None))
     monkeypatch.setattr(bench, "synth_weights", lambda m: {})
-    bench.build_model(name, "fp16")
+    bench.build_model(name, "fp16w2")
     assert seen["p"] == "bf16x3"

@@ -18,6 +18,6 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_${M}_w -o run -- $B > $
 for spec in "$@"; do
   K=${spec%%=*}; S=${spec#*=}
   # stamped with the precision that class's kernels ran in (bench.py class_precision)
-  SESA_PMC_PRECISION=$(python3 -c "import bench; print(bench.class_precision('$K', '$P'))") \
+  SESA_PMC_PRECISION=$(python3 -c "import bench; print(bench.class_precision('$K', '$P', '$M'))") \
     python3 tools/pmc_traffic.py $O/pmc_${M}_f $O/pmc_${M}_w "$S" $O/pmc_${K}.json $K
 done
