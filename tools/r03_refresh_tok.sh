@@ -8,9 +8,10 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 step() { echo "[refresh] $(date +%T) $*"; }
 step pmc htdemucs
 timeout -k 10 700 bash tools/pmc_refresh.sh htdemucs \
-  "hconv=tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, true, false>|htd_dc_conv_valu" > $O/pmc_htdemucs.log 2>&1
+  "hconv=tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, true, false>|htd_dc_conv_valu" "attn=attn_kernel" \
+  > $O/pmc_htdemucs.log 2>&1
 step pmc bs_roformer
-timeout -k 10 700 bash tools/pmc_refresh.sh bs_roformer "tokgemm=tok_gemm" "attn=attn_kernel" > $O/pmc_bsr.log 2>&1
+timeout -k 10 700 bash tools/pmc_refresh.sh bs_roformer "tokgemm=tok_gemm" > $O/pmc_bsr.log 2>&1
 step pmc scnet
 timeout -k 10 700 bash tools/pmc_refresh.sh scnet "lstm=scn_lstm_mfma" > $O/pmc_scnet.log 2>&1
 mkdir -p $O/pmc
