@@ -107,9 +107,10 @@ def kernel_sources_sha16(kclass):
 def default_precision(model):
     """MDX23C: the fp16 TFC-conv precision (SESA_PREC_F16: the T >= 32 3x3 convs on fp16 MFMA, the rest
     bf16x3; 5.1e-5 RMS vs the reference's full-chunk golden, inside the 1e-4 north_star gate -- the line
-    carries the measured value) -- also for the MDX23C member of the ensemble; every other model (and the
-    other ensemble members, build_model) bf16x3."""
-    return "fp16" if model in ("mdx23c", "ensemble") else "bf16x3"
+    carries the measured value) -- also for the MDX23C member of the ensemble; BS-Roformer: its QKV / FF
+    Linears on one fp16 pass (SESA_PREC_F16; parity tests at the same gate); SCNet / HTDemucs (and those
+    ensemble members, build_model) bf16x3."""
+    return "fp16" if model in ("mdx23c", "bs_roformer", "ensemble") else "bf16x3"
 
 
 # kernel classes whose kernels run in the MDX23C precision mode; every other class is bf16x3 in the fp16 modes

@@ -18,7 +18,8 @@ def _vocals_cfg():
 
 def test_default_precision():
     assert bench.default_precision("mdx23c") == bench.default_precision("ensemble") == "fp16"
-    for m in ("bs_roformer", "htdemucs", "scnet"):
+    assert bench.default_precision("bs_roformer") == "fp16"
+    for m in ("htdemucs", "scnet"):
         assert bench.default_precision(m) == "bf16x3"
     # PMC stamps: only the MDX23C classes run in the fp16 mode
     assert bench.class_precision("conv3x3", "fp16") == "fp16"

@@ -60,7 +60,7 @@ def test_ensemble_separate_matches_oracle_composition(method, mdx_precision):
             ref_stems.append(odm.demix(cfg, fwd, mix)["vocals"])
         m, c = get_model_from_config(kind, os.path.join(CONFIGS, cfg_name))
         m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in raw.items()}, strict=True)
-        if kind == "mdx23c":
+        if kind in ("mdx23c", "bs_roformer"):  # (both have an fp16 mode; SCNet stays bf16x3)
             m.set_precision(mdx_precision)
         members.append((c, m))
     out, stems = ensemble_separate(members, torch.from_numpy(mix).to(dev), "vocals", method, rank=0, world=1,

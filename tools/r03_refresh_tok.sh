@@ -6,6 +6,9 @@ O=gpurun_out/refresh
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 step() { echo "[refresh] $(date +%T) $*"; }
+step parity values
+timeout -k 10 300 python -u -m pytest tests/test_bsr.py tests/test_ensemble_models.py -m gpu -x -s -q --timeout 150 \
+  --timeout-method thread -k "fp16 or ensemble" > $O/parity_fp16_s.log 2>&1
 step pmc htdemucs
 timeout -k 10 700 bash tools/pmc_refresh.sh htdemucs \
   "hconv=tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, true, false>|htd_dc_conv_valu" "attn=attn_kernel" \
