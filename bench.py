@@ -450,9 +450,10 @@ def main():
     # MFMA passes per algorithmic FLOP of the dominant class (fp16 has the same dense peak as bf16); in the
     # fp16 modes the conv3x3 class is the fp16 direct convs (the T < 32 tap_gemm 3x3s, ~2 % of its FLOPs,
     # stay bf16x3)
-    passes = {"bf16x3": 3, "bf16": 1, "fp16w2": 2, "fp16": 1}[args.precision]
-    if args.precision.startswith("fp16") and kclass != "conv3x3":
-        passes = 3
+    # (by the class's own precision, class_precision; a class that mixes fp16 and bf16x3 launches -- BS-Roformer's
+    # token GEMMs: QKV / FF fp16, band split / out-projection / mask MLPs bf16x3 -- is priced at the fp16 peak,
+    # the conservative choice)
+    passes = {"bf16x3": 3, "bf16": 1, "fp16w2": 2, "fp16": 1}[class_precision(kclass, args.precision, args.model)]
     achieved = work / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     peak = BF16_DENSE_TFLOPS / passes
     note = f"2.5 PF/s dense bf16/fp16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
