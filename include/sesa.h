@@ -38,7 +38,8 @@ extern "C" {
 #define SESA_PREC_BF16X3 0
 #define SESA_PREC_BF16 1
 #define SESA_PREC_F16W2 2 /* MDX23C: TFC 3x3 convs (T >= 32) fp16 activations x fp16 hi/lo weights, 2 passes */
-#define SESA_PREC_F16 3   /* MDX23C: TFC 3x3 convs (T >= 32) single fp16 pass; the rest bf16x3 in both    */
+#define SESA_PREC_F16 3   /* MDX23C: TFC 3x3 convs (T >= 32) single fp16 pass; BS- / Mel-Band-Roformer: the
+                             QKV / FF Linears single fp16 pass; the rest bf16x3                           */
 
 int sesa_version(void);
 const char* sesa_last_error(void);

@@ -7,7 +7,8 @@ are accepted for CLI compatibility and map onto what exists on MI355X:
 
 * ``enable_amp``  -> the model's throughput precision (``_amp_precision``) instead of the default
   3-pass bf16x3 parity precision: MDX23C ``fp16`` (its TFC 3x3 convs on fp16 MFMA, 5.1e-5 RMS -- the
-  reference's AMP is fp16 autocast, :308-311, 1.35e-4 RMS), the other models single-pass ``bf16``.
+  reference's AMP is fp16 autocast, :308-311, 1.35e-4 RMS), BS- / Mel-Band-Roformer ``fp16`` (QKV / FF
+  Linears on fp16 MFMA, 4.7e-6), SCNet / HTDemucs single-pass ``bf16``.
 * ``optimize_mode`` ('channels_last' | 'compile' | 'jit' | 'default') -> no effect: the native
   forward already runs channels-last with fused prologues/epilogues, and there is no tracing
   compiler in the path.

@@ -29,6 +29,7 @@ class BSRoformer(NativeModule):
     # fp16: the QKV / FF Linears on one fp16 MFMA pass (include/sesa.h SESA_PREC_F16; 7e-6 emulated on the
     # full vocals chunk); the band split, attention, out-projection and mask MLPs stay bf16x3
     _precisions = ("bf16x3", "bf16", "fp16")
+    _amp_precision = "fp16"  # --enable_amp (the reference's AMP is fp16 autocast)
     _prec_codes = {"bf16x3": N.SESA_PREC_BF16X3, "bf16": N.SESA_PREC_BF16, "fp16": N.SESA_PREC_F16}
 
     def __init__(self, dim, *, depth, stereo=False, num_stems=1, time_transformer_depth=2, freq_transformer_depth=2,
