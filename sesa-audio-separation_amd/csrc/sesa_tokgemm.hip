@@ -468,6 +468,7 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
 
   // this lane's A pieces: piece p (per plane) covers tile rows 16 p .. 16 p + 15, 4 lanes a row
   constexpr int AP1 = A_BYTES / 1024 / (NT / 64);           // pieces per plane per wave (2)
+  constexpr bool F16 = (EP & EP_F16) != 0;                  // fp16 A planes x fp16 weight images, one pass
   int64_t asrc[AP1];
   int aslot8[AP1];
 #pragma unroll
@@ -484,6 +485,9 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   auto issue = [&](int kc, char* stg) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
+      // EP_F16: the lo planes are never read -- skip their pieces (A plane 1; the odd W pieces of this
+      // wave, q = wave + 8 (i - APW), are the lo halves of the two 128-column images)
+      if (F16 && (i < APW ? i / AP1 == 1 : ((i - APW) & 1) == 1)) continue;
       if (i < APW) {                                        // A: plane i / AP1, piece wave + 8 (i % AP1)
         const int ii = i % AP1, plane = i / AP1;
         const int k = kc * BK + aslot8[ii];
@@ -534,8 +538,7 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
       f.bl[j] = *reinterpret_cast<const bf16x8*>(stg + off + W_PLANE);
     }
   };
-  // EP_F16: fp16 A planes x fp16 weight images, one pass (the lo images are staged but not read)
-  constexpr bool F16 = (EP & EP_F16) != 0;
+  // EP_F16: fp16 A planes x fp16 weight images, one pass
   auto mma = [&](const bf16x8& x, const bf16x8& y, Acc& c) {
     if constexpr (F16) {
       const f16x8 xh = __builtin_bit_cast(f16x8, x), yh = __builtin_bit_cast(f16x8, y);
