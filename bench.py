@@ -78,11 +78,33 @@ TRACK_SECONDS = {"htdemucs": 1800.0}
 # rank's last forward is not a small remainder (169 chunks at N=1 -> 3 forwards of 57; 22 per rank at
 # N=8 -> one forward of 22)
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
-KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, v_mfma_f32_32x32x16_bf16)",
-         "tokgemm": "tok_gemm_glds_kernel + tok_gemm_kernel (token-major Linear layers, v_mfma_f32_32x32x16_bf16)",
+KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, bf16x3 v_mfma_f32_32x32x16_bf16)",
+         "tokgemm": "tok_gemm_glds_kernel + tok_gemm_kernel (token-major Linear layers, bf16x3 "
+                    "v_mfma_f32_32x32x16_bf16 / v_mfma_f32_16x16x32_bf16)",
          "lstm": "scn_lstm_mfma_kernel (bi-LSTM recurrence, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "hconv": "tok_gemm_kernel<conv> (HTDemucs implicit-GEMM convolutions, v_mfma_f32_32x32x16_bf16)",
          "attn": "attn_kernel (flash attention, S^T = K Q^T, bf16x3 v_mfma_f32_32x32x16_bf16)"}
+
+
+def kdesc(kclass, precision, model):
+    """KDESC with the MFMA instruction of the precision the class's launches run in (class_precision)."""
+    cp = class_precision(kclass, precision, model)
+    if kclass == "conv3x3":
+        return {"bf16x3": KDESC["conv3x3"],
+                "bf16": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, single-pass v_mfma_f32_32x32x16_bf16)",
+                "fp16": "conv3x3_db_kernel<F16, MI4> (TFC conv3x3 T >= 32: one v_mfma_f32_32x32x16_f16 pass, "
+                        "fused 1x1 shortcut bf16x3; T < 32: tap_gemm bf16x3)",
+                "fp16w2": "conv3x3_db_kernel<F16 = 2> (TFC conv3x3 T >= 32: v_mfma_f32_32x32x16_f16 against fp16 "
+                          "hi + lo weights, 2 passes; shortcut and T < 32 bf16x3)",
+                "fp16mix": "conv3x3_db_kernel (TFC conv3x3 T >= 32 per level as the fp16mix plan: one "
+                           "v_mfma_f32_32x32x16_f16 pass, or bf16x3 v_mfma_f32_32x32x16_bf16; shortcut and "
+                           "T < 32 bf16x3)"}[cp]
+    if kclass == "tokgemm" and cp == "fp16":
+        return ("tok_gemm_glds_kernel<EP_F16> (QKV / FF Linears, one v_mfma_f32_16x16x32_f16 pass) + bf16x3 "
+                "token GEMMs (out-projection, band split, mask MLPs: v_mfma_f32_32x32x16_bf16 / 16x16x32_bf16)")
+    if cp == "bf16" and kclass in KDESC:
+        return KDESC[kclass].replace("bf16x3 ", "single-pass ")
+    return KDESC[kclass]
 
 
 # Sources that compile each kernel class: a committed PMC summary (profiles/pmc_<class>.json) counts only
@@ -149,36 +171,58 @@ def pmc_traffic(kclass, precision="bf16x3"):
                                            "algorithmic_bytes_per_launch": d.get("algorithmic_bytes_per_launch")}
 
 
-def mdx23c_conv3x3_alg_bytes(cfg, batch, precision="bf16x3"):
+def conv_plan_modes(precision, plan=None):
+    """Per (side, level) mode of the direct (T >= 32) TFC 3x3 convs: '1' one fp16 pass, '2' fp16 x fp16 hi / lo
+    weights, '3' bf16x3, 'b' single bf16 -- the SESA_PREC_F16MIX plan string of libsesa for fp16mix."""
+    if precision == "fp16mix":
+        return plan
+    return {"fp16": "1", "fp16w2": "2", "bf16x3": "3", "bf16": "b"}[precision] * 16
+
+
+def mdx23c_conv3x3_alg_bytes(cfg, batch, precision="bf16x3", plan=None):
     """Algorithmic HBM bytes of the conv3x3 class over one MDX23C forward of `batch` chunks, and its launch
-    count: each TFC 3x3 conv reads its input once (fp32 for the fused-activation kernel -- T >= 32,
-    C_out <= 128 -- else the act_split planes: bf16 hi + lo 4 B, one fp16 or bf16 plane 2 B), the fused
-    1x1 shortcut's raw input (4 B) for conv2, and writes its fp32 output (4 B); weights per coefficient
-    4 B (bf16 hi + lo, fp16 hi + lo), 2 B (bf16 or fp16 alone); the T < 32 convs stay bf16x3 in the fp16
-    modes (mdx23c_tfc_tdf_v3.py:100-138; levels as TFC_TDF_net.__init__ :141-203)."""
+    count: each TFC 3x3 conv reads its input once -- fp32 for the fused-activation kernel (a bf16x3 / bf16
+    conv with T >= 32, C_out <= 128), else the act_split planes: bf16 hi + lo 4 B, one fp16 (the fp16 modes)
+    or bf16 plane 2 B -- the fused 1x1 shortcut's raw input (4 B) for conv2, and writes its fp32 output
+    (4 B); weights per coefficient 4 B (bf16 hi + lo, fp16 hi + lo), 2 B (bf16 or fp16 alone); the T < 32
+    convs run bf16x3 in every fp16 mode (mdx23c_tfc_tdf_v3.py:100-138; levels as TFC_TDF_net.__init__
+    :141-203).  `plan`: the fp16mix plan (16 digits, encoder levels 0..7 then decoder levels 0..7)."""
     m = cfg.model
     n, nb, c0, g = int(m.num_scales), int(m.num_blocks_per_scale), int(m.num_channels), int(m.growth)
     T0, F0 = int(cfg.audio.dim_t), int(cfg.audio.dim_f) // int(m.num_subbands)
+    modes = conv_plan_modes(precision, plan)
     total, launches = 0.0, 0
 
-    def stack(T, F, in_c, c):
+    def stack(T, F, in_c, c, enc, lv):
         nonlocal total, launches
         pos = batch * T * F
-        f16 = precision.startswith("fp16") and T >= 32
-        single = precision == "bf16" or (f16 and precision == "fp16")
-        a_in = 4.0 if (T >= 32 and c <= 128) else (2.0 if (f16 or precision == "bf16") else 4.0)
-        wb = 2.0 if single else 4.0
+        md = modes[(0 if enc else 8) + min(lv, 7)] if T >= 32 else ("b" if precision == "bf16" else "3")
+        if md in "12":
+            a_in, wb = 2.0, (2.0 if md == "1" else 4.0)
+        else:
+            fused = T >= 32 and c <= 128
+            a_in = 4.0 if (fused or md == "3") else 2.0
+            wb = 2.0 if md == "b" else 4.0
         for i in range(nb):
             ic = in_c if i == 0 else c
             total += pos * ic * a_in + pos * c * 4.0 + 9 * ic * c * wb                     # conv1
             total += pos * c * a_in + pos * (c + ic) * 4.0 + 9 * c * c * wb + ic * c * 4.0  # conv2 (+ shortcut)
             launches += 2
     for lv in range(n):
-        stack(T0 >> lv, F0 >> lv, c0 + g * lv, c0 + g * lv)
-    stack(T0 >> n, F0 >> n, c0 + g * n, c0 + g * n)
+        stack(T0 >> lv, F0 >> lv, c0 + g * lv, c0 + g * lv, True, lv)
+    stack(T0 >> n, F0 >> n, c0 + g * n, c0 + g * n, True, n)
     for lv in reversed(range(n)):
-        stack(T0 >> lv, F0 >> lv, 2 * (c0 + g * lv), c0 + g * lv)
+        stack(T0 >> lv, F0 >> lv, 2 * (c0 + g * lv), c0 + g * lv, False, lv)
     return total, launches
+
+
+def f16_plan():
+    """libsesa's current SESA_PREC_F16MIX plan (16 digits; sesa_mdx23c_set_f16_plan query)."""
+    import ctypes
+    from sesa import _native
+    buf = ctypes.create_string_buffer(17)
+    _native.check(_native.lib().sesa_mdx23c_set_f16_plan(None, buf))
+    return buf.value.decode()
 
 
 def log(*a):
@@ -283,6 +327,44 @@ def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chu
                       f"(OLA <1% of CPU time, SURVEY §6)"}
 
 
+# north_star parity, measured by the bench itself after the timed region: every benchmarked member, in the
+# precision it ran, on the reference's own full-width outputs (tests/golden/make_golden*.py: the reference
+# classes run in fp32 on CPU) -- MDX23C on four fixtures (0.1-RMS white noise, the SURVEY §8(d) seed-1 sines +
+# noise signal, 0.3-RMS white noise, a second weight draw), the other models on their full-chunk golden
+PARITY_FIXTURES = {"mdx23c": ["mdx23c_full_chunk.npz", "mdx23c_full_sines.npz", "mdx23c_full_loud.npz",
+                              "mdx23c_full_wseed2.npz"],
+                   "bs_roformer": ["bsr_full_chunk.npz"], "scnet": ["scnet_full_chunk.npz"],
+                   "htdemucs": ["htdemucs_full_segment.npz"]}
+
+
+def parity_leg(names, members, dev):
+    from sesa.utils import get_model_from_config
+    from sesa.weights import synth_model_state, synth_state_dict
+    out, worst = {}, 0.0
+    for nm, (model, _, cfg_path) in zip(names, members):
+        for fx in PARITY_FIXTURES[nm]:
+            g = np.load(os.path.join(REPO, "tests", "golden", fx), allow_pickle=False)
+            affine = str(g["affine"]) if "affine" in g.files else "random"
+            seed = int(g["weight_seed"]) if "weight_seed" in g.files else 0
+            m, _ = get_model_from_config(nm, cfg_path)
+            m.load_state_dict(synth_state_dict(m, affine=affine, seed=seed) if nm == "mdx23c" else
+                              synth_model_state(m, affine=affine, seed=seed), strict=True)
+            m.set_precision(model.precision)
+            with torch.no_grad():
+                y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy().astype(np.float64)
+            ref = g["y"].astype(np.float64)
+            err = float(np.sqrt(np.mean((y - ref) ** 2)))
+            ref_rms = float(np.sqrt(np.mean(ref ** 2)))
+            out[fx] = {"model": nm, "precision": model.precision, "rms": err, "rel_rms": err / ref_rms,
+                       "max_abs": float(np.abs(y - ref).max()), "ref_rms": ref_rms,
+                       "input_rms": float(np.sqrt(np.mean(np.asarray(g["x"], np.float64) ** 2))),
+                       "weight_seed": seed, "affine": affine}
+            worst = max(worst, err)
+            del m
+    return {"gate": 1e-4, "within_gate": worst <= 1e-4, "worst_rms": worst, "fixtures": out,
+            "reference": "tests/golden/<fixture> (reference classes in fp32 on CPU, same name-keyed weights)"}
+
+
 def synth_weights(model):
     """Name-keyed random-init weights with PyTorch's default-init bounds (no checkpoint offline)."""
     import zlib
@@ -330,7 +412,7 @@ def main():
     ap.add_argument("--model", default="mdx23c", choices=sorted(MODELS))
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--precision", default=None, choices=["bf16x3", "bf16", "fp16w2", "fp16"],
+    ap.add_argument("--precision", default=None, choices=["bf16x3", "bf16", "fp16w2", "fp16", "fp16mix"],
                     help="default: fp16 for mdx23c (TFC 3x3 convs on fp16 MFMA, inside the 1e-4 gate), else bf16x3")
     ap.add_argument("--exec-batch", type=int, default=0, help="chunks per forward (0: per-model default)")
     ap.add_argument("--track-seconds", type=float, default=0.0, help="0: 240 (1800 for htdemucs)")
@@ -453,10 +535,14 @@ def main():
     # (by the class's own precision, class_precision; a class that mixes fp16 and bf16x3 launches -- BS-Roformer's
     # token GEMMs: QKV / FF fp16, band split / out-projection / mask MLPs bf16x3 -- is priced at the fp16 peak,
     # the conservative choice)
-    passes = {"bf16x3": 3, "bf16": 1, "fp16w2": 2, "fp16": 1}[class_precision(kclass, args.precision, args.model)]
+    passes = {"bf16x3": 3, "bf16": 1, "fp16w2": 2, "fp16": 1, "fp16mix": 1}[class_precision(kclass, args.precision,
+                                                                                             args.model)]
     achieved = work / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     peak = BF16_DENSE_TFLOPS / passes
     note = f"2.5 PF/s dense bf16/fp16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
+    if class_precision(kclass, args.precision, args.model) == "fp16mix":
+        note = (f"2.5 PF/s dense fp16: the class mixes one-pass fp16 and bf16x3 launches (fp16mix plan "
+                f"{f16_plan()}), priced at the fp16 peak (the conservative choice)")
     if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
         peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
     traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model))
@@ -465,12 +551,14 @@ def main():
         m0, cfg0, _ = members[0]
         per_fwd, l_fwd = 0.0, 0
         for nb_ in [len(x) for x in _forward_sizes(chunks[0], batches[0], world)]:
-            b_, l_ = mdx23c_conv3x3_alg_bytes(cfg0, nb_, args.precision)
+            b_, l_ = mdx23c_conv3x3_alg_bytes(cfg0, nb_, args.precision, f16_plan())
             per_fwd += b_
             l_fwd += l_
         alg_bytes = round(per_fwd / max(l_fwd, 1))
+    if isinstance(traffic_src, dict):   # one algorithmic figure: this run's (the PMC file's own is for its run)
+        traffic_src.pop("algorithmic_bytes_per_launch", None)
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": KDESC[kclass],
+            "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": kdesc(kclass, args.precision, args.model),
             "launches": launches, "avg_launch_ms": round(ms / max(launches, 1), 4),
             "flop_per_launch": round(work / max(launches, 1)), "peak_note": note, "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": alg_bytes,
@@ -523,24 +611,12 @@ def main():
         line["kernel_classes"] = classes
         if "bs_roformer" in names or "htdemucs" in names:
             ams, alaunch, awork = _native.profile_read("attn")
-            line["attention"] = {"kernel": KDESC["attn"],
+            line["attention"] = {"kernel": kdesc("attn", args.precision, args.model),
                                  "achieved_tflops": round(awork / (ams * 1e-3) / 1e12, 2) if ams > 0 else 0.0,
                                  "launches": alaunch, "avg_launch_ms": round(ams / max(alaunch, 1), 4)}
-        if args.model == "mdx23c" and not args.no_parity:
-            # north_star parity, measured by the bench itself: the same model (same weights) on the
-            # reference's own full-chunk output (tests/golden/mdx23c_full_chunk.npz, the reference
-            # TFC_TDF_net run in fp32 on CPU by tests/golden/make_golden.py), per-sample RMS
-            gp = os.path.join(REPO, "tests", "golden", "mdx23c_full_chunk.npz")
-            if os.path.exists(gp):
-                g = np.load(gp, allow_pickle=False)
-                with torch.no_grad():
-                    y = members[0][0](torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
-                err = float(np.sqrt(np.mean((y.astype(np.float64) - g["y"]) ** 2)))
-                line["parity_rms"] = err
-                line["parity"] = {"rms_vs_reference": err, "gate": 1e-4, "within_gate": err <= 1e-4,
-                                  "precision": args.precision,
-                                  "fixture": "tests/golden/mdx23c_full_chunk.npz (reference TFC_TDF_net, fp32 CPU, "
-                                             "one 261120-sample chunk, same name-keyed weights)"}
+        if not args.no_parity:
+            line["parity"] = parity_leg(names, members, dev)
+            line["parity_rms"] = line["parity"]["worst_rms"]
         if world == 1 and not args.no_cpu_baseline:
             parts = [cpu_baseline(nm, cp, c, track_seconds, args.cpu_sample_chunks if len(names) == 1 else 2,
                                   config0=len(names) == 1 and not args.cpu_chunks_only)

@@ -18,6 +18,9 @@
  *                       MDX23C FLOPs) on fp16 MFMA: the activation rounded once to fp16 (2^-11) against
  *                       the fp16 hi + lo weights (2 passes) or the fp16 weights (1 pass); every other
  *                       contraction bf16x3 (MDX23C only; the other models accept BF16X3 / BF16)
+ *   SESA_PREC_F16MIX -- MDX23C: those convs per level as the plan of sesa_mdx23c_set_f16_plan says
+ *                       (default: one fp16 pass everywhere except the encoder level-1 convs, bf16x3 --
+ *                       they carry ~70 % of the fp16 rounding error at the stems)
  */
 #ifndef SESA_H_
 #define SESA_H_
@@ -40,6 +43,7 @@ extern "C" {
 #define SESA_PREC_F16W2 2 /* MDX23C: TFC 3x3 convs (T >= 32) fp16 activations x fp16 hi/lo weights, 2 passes */
 #define SESA_PREC_F16 3   /* MDX23C: TFC 3x3 convs (T >= 32) single fp16 pass; BS- / Mel-Band-Roformer: the
                              QKV / FF Linears single fp16 pass; the rest bf16x3                           */
+#define SESA_PREC_F16MIX 4 /* MDX23C: per-level plan of the T >= 32 TFC 3x3 convs (sesa_mdx23c_set_f16_plan) */
 
 int sesa_version(void);
 const char* sesa_last_error(void);
@@ -142,6 +146,11 @@ int sesa_mdx23c_set_conv_variant(int variant);
  * 0 = off (default), 1 = levels with 32 <= T <= 128, 2 = every level with T >= 32.  Initialised from
  * SESA_CONV_WINO; decided per convolution when a model is finalized (the weights are packed for it). */
 int sesa_mdx23c_set_wino(int mode);
+/* SESA_PREC_F16MIX plan (read when a model is finalized): 16 digits, encoder levels 0..7 then decoder
+ * levels 0..7, '1' = fp16, '2' = fp16 x fp16 hi/lo weights, '3' = bf16x3; NULL plan = query only.  The
+ * previous plan is copied to prev (17 bytes) when prev is not NULL.  Default "1311111111111111"
+ * (env SESA_F16_PLAN overrides it at first use). */
+int sesa_mdx23c_set_f16_plan(const char* plan, char* prev);
 
 /* ---------------------------------------------------------------------------------------
  * BS-Roformer (models/bs_roformer/bs_roformer.py:327-587, BSRoformer)

@@ -16,12 +16,15 @@ import numpy as np
 SEED_XOR = 0x5E5A
 
 
-def param_rng(name: str) -> np.random.Generator:
-    return np.random.Generator(np.random.PCG64(zlib.crc32(name.encode()) ^ SEED_XOR))
+def param_rng(name: str, seed: int = 0) -> np.random.Generator:
+    """seed 0: PCG64(crc32(name) ^ 0x5E5A); seed k > 0: a second, independent weight
+    draw for the same architecture, PCG64([crc32(name) ^ 0x5E5A, k])."""
+    key = zlib.crc32(name.encode()) ^ SEED_XOR
+    return np.random.Generator(np.random.PCG64(key if seed == 0 else [key, int(seed)]))
 
 
-def synth_param(name: str, shape, affine: str = "unit") -> np.ndarray:
-    rng = param_rng(name)
+def synth_param(name: str, shape, affine: str = "unit", seed: int = 0) -> np.ndarray:
+    rng = param_rng(name, seed)
     shape = tuple(int(s) for s in shape)
     if len(shape) >= 2:
         fan_in = int(np.prod(shape[1:]))
@@ -39,6 +42,6 @@ def synth_param(name: str, shape, affine: str = "unit") -> np.ndarray:
     return np.ones(shape, np.float32)
 
 
-def synth_state_dict(shapes, affine: str = "unit"):
+def synth_state_dict(shapes, affine: str = "unit", seed: int = 0):
     """shapes: iterable of (name, shape) in named_parameters() order."""
-    return {name: synth_param(name, shape, affine) for name, shape in shapes}
+    return {name: synth_param(name, shape, affine, seed) for name, shape in shapes}

@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -52,7 +53,8 @@ struct ConvW {
   int kind = 0, C_in = 0, C_out = 0, n_cols = 0, bn = 64, param = -1;
   int64_t w_off = 0;  // uint16 offset into the packed weight blob
   bool wino = false;  // packed for conv3x3_wino_kernel (decided at finalize, conv3x3_wino_selected)
-  bool f16 = false;   // main chunks packed fp16 hi / lo (SESA_PREC_F16 / F16W2 direct 3x3 convs, finalize)
+  bool f16 = false;   // main chunks packed fp16 hi / lo (SESA_PREC_F16 / F16W2 / F16MIX direct 3x3 convs, finalize)
+  int f16c = 0;       // launch_conv mode of an f16 conv: 2 = fp16 x fp16 hi / lo weights, 3 = one fp16 pass
 };
 struct TdfW {
   int M = 0, K = 0, param = -1;
@@ -329,6 +331,32 @@ void pack_norm(sesa_mdx23c* m, Norm& n, std::vector<float>& aff) {
   aff.insert(aff.end(), m->params[n.beta].host.begin(), m->params[n.beta].host.end());
 }
 
+// ---- SESA_PREC_F16MIX plan ----
+// One digit per level of the direct (T >= 32) TFC 3x3 convs: encoder levels 0..7, then decoder levels 0..7;
+// '1' = one fp16 pass, '2' = fp16 activation x fp16 hi / lo weights, '3' = bf16x3.  Default from the CPU
+// emulation's per-conv sensitivity scan (tests/emulation/emulate_mdx23c_levels.py): the
+// rounding error of the encoder level-1 convs dominates the stems' deviation, the decoder convs contribute
+// ~2 % of it.
+constexpr char kF16PlanDefault[17] = "1311111111111111";
+std::mutex g_plan_mu;
+char g_f16_plan[17] = {0};
+
+int f16_plan_mode(int precision, bool enc, int level) {
+  if (precision == SESA_PREC_F16) return 3;
+  if (precision == SESA_PREC_F16W2) return 2;
+  if (precision != SESA_PREC_F16MIX) return 0;
+  char d;
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    if (!g_f16_plan[0]) {
+      const char* e = getenv("SESA_F16_PLAN");
+      memcpy(g_f16_plan, e && strlen(e) == 16 && strspn(e, "123") == 16 ? e : kF16PlanDefault, 16);
+    }
+    d = g_f16_plan[(enc ? 0 : 8) + (level < 7 ? level : 7)];
+  }
+  return d == '1' ? 3 : d == '2' ? 2 : 0;
+}
+
 // ---- forward ----
 struct Tensor {
   float* p = nullptr;
@@ -343,7 +371,6 @@ struct Fwd {
   int B;
   int x3;
   char* ws;
-  int f16c = 0;          // launch_conv mode of the w.f16 convs (2 = SESA_PREC_F16W2, 3 = SESA_PREC_F16)
   size_t off = 0;        // float region bump offset (bytes)
   size_t peak = 0;       // high-water mark of `off` (block temporaries are released, see stack())
   size_t stats_off = 0;  // stats region bump offset (bytes), relative to stats_base
@@ -408,7 +435,7 @@ struct Fwd {
                        : w.kind == CONV1X1 ? SESA_KCLASS_CONV1X1
                        : w.kind == CONV2X2S2 ? SESA_KCLASS_DOWN : SESA_KCLASS_UP;
     void* tok = profile_begin(st);
-    rc = launch_conv(w.kind, w.bn, w.f16 ? f16c : x3, a, B, st);
+    rc = launch_conv(w.kind, w.bn, w.f16 ? w.f16c : x3, a, B, st);
     profile_end(tok, st, kclass,
                 2.0 * B * T_out * F_out * (double)w.n_cols * (w.C_in * taps + (xin ? xin->C_in : 0)));
   }
@@ -635,7 +662,7 @@ extern "C" int sesa_mdx23c_create(const sesa_mdx23c_config* cfg, sesa_mdx23c** o
   SESA_REQUIRE(c.num_subbands > 0 && c.dim_f % c.num_subbands == 0 && c.dim_f <= c.n_fft / 2, SESA_ERR_INVALID,
                "mdx23c: bad dim_f / num_subbands");
   SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16 || c.precision == SESA_PREC_F16W2 ||
-                   c.precision == SESA_PREC_F16,
+                   c.precision == SESA_PREC_F16 || c.precision == SESA_PREC_F16MIX,
                SESA_ERR_INVALID, "mdx23c: bad precision %d", c.precision);
   const int F0 = c.dim_f / c.num_subbands;
   const int n = c.num_scales;
@@ -717,15 +744,17 @@ extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
   std::vector<uint16_t> blob;
   std::vector<float> aff;
   auto pc = [&](ConvW& w) { pack_conv(m->params[w.param], w, blob); };
-  // the fp16 precisions: the direct (T >= 32) TFC 3x3 convs only; everything else stays bf16x3
-  const bool f16p = m->cfg.precision == SESA_PREC_F16W2 || m->cfg.precision == SESA_PREC_F16;
-  auto pstack = [&](Stack& s) {
+  // the fp16 precisions: the direct (T >= 32) TFC 3x3 convs only; everything else stays bf16x3.
+  // SESA_PREC_F16MIX: per level and side from the plan (f16_plan_mode)
+  auto pstack = [&](Stack& s, bool enc, int level) {
+    const int md = f16_plan_mode(m->cfg.precision, enc, level);
     for (auto& b : s.blocks) {
       b.conv1.wino = b.conv2.wino = false;
-      b.conv1.f16 = f16p && b.T >= 32 && !conv3x3_wino_selected(b.T, b.in_c, b.c) &&
+      b.conv1.f16 = md != 0 && b.T >= 32 && !conv3x3_wino_selected(b.T, b.in_c, b.c) &&
                     !conv3x3_m16_selected(b.T, b.c, b.c, b.in_c);
-      b.conv2.f16 = f16p && b.T >= 32 && !conv3x3_wino_selected(b.T, b.c, b.c) &&
+      b.conv2.f16 = md != 0 && b.T >= 32 && !conv3x3_wino_selected(b.T, b.c, b.c) &&
                     !conv3x3_m16_selected(b.T, b.c, b.c, b.in_c);
+      b.conv1.f16c = b.conv2.f16c = md;
       if (conv3x3_wino_selected(b.T, b.in_c, b.c)) pack_conv_wino(m->params[b.conv1.param], b.conv1, blob);
       else pc(b.conv1);
       if (conv3x3_wino_selected(b.T, b.c, b.c))
@@ -742,15 +771,15 @@ extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
   };
   pc(m->first_conv);
   for (size_t i = 0; i < m->enc.size(); ++i) {
-    pstack(m->enc[i]);
+    pstack(m->enc[i], true, (int)i);
     pc(m->down[i]);
     pack_norm(m, m->down_norm[i], aff);
   }
-  pstack(m->bottleneck);
+  pstack(m->bottleneck, true, (int)m->enc.size());
   for (size_t i = 0; i < m->dec.size(); ++i) {
     pc(m->up[i]);
     pack_norm(m, m->up_norm[i], aff);
-    pstack(m->dec[i]);
+    pstack(m->dec[i], false, (int)(m->dec.size() - 1 - i));
   }
   pc(m->final0);
   pc(m->final2);
@@ -774,7 +803,6 @@ extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
 namespace {
 void plan_sizes(sesa_mdx23c* m, int batch, size_t* float_bytes, size_t* stats_bytes) {
   Fwd f{m, nullptr, true, batch, m->cfg.precision == SESA_PREC_BF16 ? 0 : 1, nullptr};
-  f.f16c = m->cfg.precision == SESA_PREC_F16 ? 3 : 2;
   f.run(nullptr, nullptr);
   *float_bytes = f.peak;
   *stats_bytes = f.stats_off;
@@ -801,7 +829,6 @@ extern "C" int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, fl
   char* ws = reinterpret_cast<char*>(workspace);
   SESA_CHECK_HIP(hipMemsetAsync(ws + fb, 0, sb, st));  // norm statistics accumulate atomically
   Fwd f{m, st, false, batch, m->cfg.precision == SESA_PREC_BF16 ? 0 : 1, ws};
-  f.f16c = m->cfg.precision == SESA_PREC_F16 ? 3 : 2;
   f.stats_base = ws + fb;
   f.stats_cap = sb;
   f.float_cap = fb;
@@ -820,3 +847,17 @@ extern "C" int sesa_mdx23c_destroy(sesa_mdx23c* m) {
 extern "C" int sesa_mdx23c_set_conv_variant(int variant) { return set_conv3x3_variant(variant); }
 
 extern "C" int sesa_mdx23c_set_wino(int mode) { return set_conv3x3_wino(mode); }
+
+extern "C" int sesa_mdx23c_set_f16_plan(const char* plan, char* prev) {
+  clear_error();
+  SESA_REQUIRE(!plan || (strlen(plan) == 16 && strspn(plan, "123") == 16), SESA_ERR_INVALID,
+               "set_f16_plan: 16 digits of 1 (fp16), 2 (fp16w2), 3 (bf16x3) expected");
+  (void)f16_plan_mode(SESA_PREC_F16MIX, true, 0);  // resolve the default / environment first
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  if (prev) {
+    memcpy(prev, g_f16_plan, 16);
+    prev[16] = 0;
+  }
+  if (plan) memcpy(g_f16_plan, plan, 16);
+  return SESA_OK;
+}

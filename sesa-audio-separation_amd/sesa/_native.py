@@ -14,6 +14,7 @@ SESA_PREC_BF16X3 = 0
 SESA_PREC_BF16 = 1
 SESA_PREC_F16W2 = 2
 SESA_PREC_F16 = 3
+SESA_PREC_F16MIX = 4
 
 
 class SesaMdx23cConfig(ctypes.Structure):
@@ -72,6 +73,7 @@ SIGNATURES = {
     "sesa_mdx23c_destroy": (c_int, [c_void_p]),
     "sesa_mdx23c_set_conv_variant": (c_int, [c_int]),
     "sesa_mdx23c_set_wino": (c_int, [c_int]),
+    "sesa_mdx23c_set_f16_plan": (c_int, [c_char_p, c_char_p]),
     "sesa_bsr_create": (c_int, [ctypes.POINTER(SesaBsrConfig), ctypes.POINTER(c_void_p)]),
     "sesa_bsr_num_params": (c_int, [c_void_p]),
     "sesa_bsr_param_info": (c_int, [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64)]),

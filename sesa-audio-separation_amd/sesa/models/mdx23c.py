@@ -28,11 +28,12 @@ class TFC_TDF_net(NativeModule):
     """Reference-compatible MDX23C module (torch.nn.Module) backed by the native HIP forward."""
 
     _prefix = "mdx23c"
-    # fp16 / fp16w2: the TFC 3x3 convs of the T >= 32 levels on fp16 MFMA (include/sesa.h SESA_PREC_F16*)
-    _precisions = ("bf16x3", "bf16", "fp16w2", "fp16")
+    # fp16 / fp16w2: the TFC 3x3 convs of the T >= 32 levels on fp16 MFMA (include/sesa.h SESA_PREC_F16*);
+    # fp16mix: per level as sesa_mdx23c_set_f16_plan says (default: fp16 except the encoder level-1 convs)
+    _precisions = ("bf16x3", "bf16", "fp16w2", "fp16", "fp16mix")
     _amp_precision = "fp16"
     _prec_codes = {"bf16x3": N.SESA_PREC_BF16X3, "bf16": N.SESA_PREC_BF16, "fp16w2": N.SESA_PREC_F16W2,
-                   "fp16": N.SESA_PREC_F16}
+                   "fp16": N.SESA_PREC_F16, "fp16mix": N.SESA_PREC_F16MIX}
 
     def __init__(self, config, precision="bf16x3"):
         super().__init__(precision)

@@ -74,6 +74,18 @@ def _runs(group):
         j = k
 
 
+_SIDE_STREAMS = {}
+
+
+def side_streams(device, n):
+    """n side streams of `device`, created once per process and reused by every call: each stream keys
+    its own model workspace (NativeModule.workspace), so fresh streams per call would grow that cache."""
+    pool = _SIDE_STREAMS.setdefault(device.index, [])
+    while len(pool) < n:
+        pool.append(torch.cuda.Stream(device))
+    return pool[:n]
+
+
 def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, streams=1):
     """gather -> forward -> OLA of this rank's chunks into a [rows, span_max] result buffer (HIP).
 
@@ -92,7 +104,7 @@ def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, 
     flat = plan["flat"]
     win = _Windows(plan, device)
     main = torch.cuda.current_stream(device)
-    pool = [main] + [torch.cuda.Stream(device) for _ in range(max(1, int(streams)) - 1)]
+    pool = [main] + side_streams(device, max(1, int(streams)) - 1)
     xbufs = [None] * len(pool)
     freed = [None] * len(pool)    # event on main after the OLA that consumed the stream's last forward
     for st in pool[1:]:

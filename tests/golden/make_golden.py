@@ -16,6 +16,8 @@ Fixtures:
   mdx23c_small_vocals.npz TFC_TDF_net.forward, single-target reduced config
   demix_small_*.npz       inference_pytorch.demix_pytorch_optimized on the reduced model
   mdx23c_full_chunk.npz   (--full) one 261120-sample chunk through the full vocals config
+  mdx23c_full_{sines,loud,wseed2}.npz  (--only full_levels) the same model on the §8(d) sines signal,
+                          on 0.3-RMS white noise, and a second weight draw
   ensemble.npz            ensemble.AudioEnsembleEngine.process_waveform/process_spectral
   demix_full_10s.npz      (--only demix_full) BASELINE configs[0]: demix_pytorch_optimized, full vocals
                           config, 10 s mix, 13 chunks
@@ -82,11 +84,11 @@ def load_cfg(name):
         return yaml.safe_load(f)
 
 
-def build_ref_model(cfg_dict, affine):
+def build_ref_model(cfg_dict, affine, seed=0):
     from models.mdx23c_tfc_tdf_v3 import TFC_TDF_net
     model = TFC_TDF_net(to_attr(cfg_dict)).eval()
     shapes = [(n, tuple(p.shape)) for n, p in model.named_parameters()]
-    sd = synth_state_dict(shapes, affine=affine)
+    sd = synth_state_dict(shapes, affine=affine, seed=seed)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     return model, shapes
 
@@ -94,6 +96,21 @@ def build_ref_model(cfg_dict, affine):
 def mix_signal(seed, n):
     rng = np.random.default_rng(seed)
     return (0.1 * rng.standard_normal((2, n))).astype(np.float32)
+
+
+def sines_signal(seed, n, sr=44100):
+    """SURVEY §8(d)'s second synthetic signal: per channel, 20 sines at amplitude 0.02 with log-uniform
+    random frequencies in [40 Hz, 16 kHz] and uniform random phases, plus 0.05-std white noise (seed 1);
+    a non-white spectrum with tonal peaks."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n, dtype=np.float64) / sr
+    out = np.empty((2, n), np.float64)
+    for c in range(2):
+        f = np.exp(rng.uniform(np.log(40.0), np.log(16000.0), 20))
+        ph = rng.uniform(0.0, 2 * np.pi, 20)
+        out[c] = (0.02 * np.sin(2 * np.pi * f[:, None] * t[None] + ph[:, None])).sum(0)
+        out[c] += 0.05 * rng.standard_normal(n)
+    return out.astype(np.float32)
 
 
 def save(name, **arrays):
@@ -129,6 +146,24 @@ def gen_forward(cfg_name, out_name, batch, seed, affine):
     x = np.stack([mix_signal(seed + b, C) for b in range(batch)])
     y = model(torch.from_numpy(x)).numpy()
     save(out_name, x=x, y=y, affine=np.array(affine))
+
+
+@torch.inference_mode()
+def gen_full_levels():
+    """Full-width MDX23C vocals chunk beyond the quiet white-noise golden: the §8(d)
+    seed-1 sines + noise signal, white noise at 0.3 RMS (seed 5, about -10 dBFS), and the 0.1-RMS seed-0
+    chunk through an independent second weight draw (seed 2, random norm affine)."""
+    cfg = load_cfg("config_vocals_mdx23c.yaml")
+    C = cfg["audio"]["chunk_size"]
+    model, _ = build_ref_model(cfg, "unit")
+    for name, x in (("mdx23c_full_sines.npz", sines_signal(1, C)),
+                    ("mdx23c_full_loud.npz", (0.3 * np.random.default_rng(5).standard_normal((2, C))).astype(np.float32))):
+        y = model(torch.from_numpy(x[None])).numpy()
+        save(name, x=x[None], y=y, affine=np.array("unit"), weight_seed=np.array(0))
+    model, _ = build_ref_model(cfg, "random", seed=2)
+    x = mix_signal(0, C)[None]
+    y = model(torch.from_numpy(x)).numpy()
+    save("mdx23c_full_wseed2.npz", x=x, y=y, affine=np.array("random"), weight_seed=np.array(2))
 
 
 @torch.inference_mode()
@@ -235,6 +270,8 @@ def main():
         gen_stress()
     if "demix_full" in todo:
         gen_demix_full()
+    if "full_levels" in todo:
+        gen_full_levels()
     if args.full or "full" in todo:
         gen_forward("config_vocals_mdx23c.yaml", "mdx23c_full_chunk.npz", 1, 0, "unit")
 
