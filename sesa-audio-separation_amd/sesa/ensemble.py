@@ -47,7 +47,7 @@ def blend_device(waves, method, weights=None, buffer=32768):
 
 
 def ensemble_separate(members, mix_d, stem="vocals", method="avg_wave", weights=None, buffer=32768, rank=None,
-                      world=None, exec_batch=None, group=None):
+                      world=None, exec_batch=None, group=None, demix_hooks=None, blend_fn=None):
     """Multi-model ensemble of one track, all on the device (BASELINE configs[4]).
 
     The GUI's ensemble flow (processing.py:266-363 runs inference.py once per model, then
@@ -56,7 +56,9 @@ def ensemble_separate(members, mix_d, stem="vocals", method="avg_wave", weights=
     group (sesa/parallel.py: contiguous chunk ranges per rank, one RCCL all_gather per model), the
     members' ``stem`` outputs are stacked and blended with ``sesa_blend_f32`` (ensemble.py:258-407
     semantics, float64).  Returns (blend [2, L] float64, {member index: stem [2, L] float32}).
-    ``exec_batch``: chunks per forward, a list (one per member) or an int."""
+    ``exec_batch``: chunks per forward, a list (one per member) or an int.  ``demix_hooks`` (local_fn /
+    counter_fn / finalize_fn of demix_sharded) and ``blend_fn`` exist so the CPU test-suite can drive the
+    sharding, the collectives and the member loop over gloo ranks with the oracle's OLA and blend."""
     from .config import prefer_target_instrument
     from .parallel import demix_sharded
     stems = []
@@ -65,10 +67,11 @@ def ensemble_separate(members, mix_d, stem="vocals", method="avg_wave", weights=
         if stem not in names:
             raise ValueError(f"ensemble member {i} has no '{stem}' stem (instruments: {names})")
         eb = exec_batch[i] if isinstance(exec_batch, (list, tuple)) else (exec_batch or 8)
-        est = demix_sharded(cfg, model, mix_d, mix_d.device, rank=rank, world=world, exec_batch=eb, group=group)
+        est = demix_sharded(cfg, model, mix_d, mix_d.device, rank=rank, world=world, exec_batch=eb, group=group,
+                            **(demix_hooks or {}))
         stems.append(est[names.index(stem)])
     x = torch.stack(stems)
-    return blend_device(x, method, weights, buffer), {i: s for i, s in enumerate(stems)}
+    return (blend_fn or blend_device)(x, method, weights, buffer), {i: s for i, s in enumerate(stems)}
 
 
 class AudioEnsembleEngine:

@@ -31,7 +31,7 @@ class TFC_TDF_net(NativeModule):
     # fp16 / fp16w2: the TFC 3x3 convs of the T >= 32 levels on fp16 MFMA (include/sesa.h SESA_PREC_F16*);
     # fp16mix: per level as sesa_mdx23c_set_f16_plan says (default: fp16 except the encoder level-1 convs)
     _precisions = ("bf16x3", "bf16", "fp16w2", "fp16", "fp16mix")
-    _amp_precision = "fp16"
+    _amp_precision = "fp16mix"  # --enable_amp: fp16 TFC convs except the encoder level-1 ones (every fixture <= 1e-4)
     _prec_codes = {"bf16x3": N.SESA_PREC_BF16X3, "bf16": N.SESA_PREC_BF16, "fp16w2": N.SESA_PREC_F16W2,
                    "fp16": N.SESA_PREC_F16, "fp16mix": N.SESA_PREC_F16MIX}
 

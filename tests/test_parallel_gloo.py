@@ -96,16 +96,33 @@ def _demucs_cfg():
                  "inference": {"num_overlap": 4, "batch_size": 2}})
 
 
-def _worker(rank, world, port, bs, q, mode="generic"):
+class StandIn2:
+    """A second, different stand-in member (ensemble tests)."""
+
+    def __call__(self, x):
+        return torch.stack([0.7 * x + 0.02 * torch.roll(x, -3, -1), 0.3 * x], 1)
+
+
+def _worker(rank, world, port, bs, q, mode="generic", L=L_TRACK):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from sesa.parallel import demix_sharded
         cfg = _demucs_cfg() if mode == "demucs" else _cfg(bs)
-        est = demix_sharded(cfg, StandIn(), torch.from_numpy(_mix()), rank=rank, world=world,
-                            local_fn=cpu_local, finalize_fn=cpu_finalize, counter_fn=make_cpu_counter(cfg),
-                            mode=mode)
+        mix = torch.from_numpy(_mix()[:, :L])
+        if mode == "ensemble":
+            from oracle.ensemble import blend
+            from sesa.ensemble import ensemble_separate
+            hooks = dict(local_fn=cpu_local, finalize_fn=cpu_finalize, counter_fn=make_cpu_counter(cfg))
+            out, stems = ensemble_separate([(cfg, StandIn()), (cfg, StandIn2())], mix, "vocals", "avg_wave",
+                                           weights=[0.6, 0.4], rank=rank, world=world, demix_hooks=hooks,
+                                           blend_fn=lambda x, m, w, b: torch.from_numpy(blend(x.numpy(), m, w, b)))
+            est = out
+        else:
+            est = demix_sharded(cfg, StandIn(), mix, rank=rank, world=world,
+                                local_fn=cpu_local, finalize_fn=cpu_finalize, counter_fn=make_cpu_counter(cfg),
+                                mode=mode)
         if rank == 0:
             q.put(est.numpy())
     finally:
@@ -165,3 +182,56 @@ def test_shard_plan_covers_every_chunk_once():
         for (lo, hi), (s, e) in zip(p["ranges"], p["spans"]):
             for (st, n, _, _) in p["flat"][lo:hi]:
                 assert s <= st and st + n <= e
+
+
+def _run_world(world, mode, bs=1, L=L_TRACK):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    pc = mp.start_processes(_worker, args=(world, port, bs, q, mode, L), nprocs=world, join=False,
+                            start_method="spawn")
+    est = q.get()
+    while not pc.join(timeout=180):
+        pass
+    return est
+
+
+# World 8 (the driver's scaling node): a 13-chunk track (97 000 samples of the reduced config, chunk 64 512 at
+# overlap 4) gives ranges of 2 chunks and an EMPTY rank 7 (sesa/parallel.py shard_ranges); the demucs-mode
+# plan and the ensemble member loop (one all_gather per member, then the blend) at the same world size.
+L13 = 97000
+
+
+def test_world8_generic_with_empty_rank():
+    from oracle.demix import demix as odemix
+    from sesa.parallel import shard_plan
+    p = shard_plan(_cfg(1), L13, 8)
+    assert len(p["flat"]) == 13 and p["ranges"][7][0] == p["ranges"][7][1]
+    est = _run_world(8, "generic", L=L13)
+    ref = odemix(_cfg(1), StandIn(), _mix()[:, :L13], batch_size=1)
+    ref = np.stack([ref["vocals"], ref["other"]])
+    assert est.shape == ref.shape
+    assert np.abs(est - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max())
+
+
+def test_world8_demucs_mode():
+    from oracle.demix import demix_demucs_mode
+    est = _run_world(8, "demucs")
+    ref = demix_demucs_mode(_demucs_cfg(), StandIn(), _mix())
+    ref = np.stack([ref["vocals"], ref["other"]])
+    assert est.shape == ref.shape
+    assert np.abs(est - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max())
+
+
+def test_world8_ensemble_two_members():
+    """ensemble_separate over 8 gloo ranks (each member chunk-sharded, its own all_gather) + avg_wave blend
+    with weights, against the single-process oracle demix of each member and the oracle blend."""
+    from oracle.demix import demix as odemix
+    from oracle.ensemble import blend
+    est = _run_world(8, "ensemble", L=L13)
+    mix = _mix()[:, :L13]
+    v1 = odemix(_cfg(1), StandIn(), mix, batch_size=1)["vocals"]
+    v2 = odemix(_cfg(1), StandIn2(), mix, batch_size=1)["vocals"]
+    ref = blend(np.stack([v1, v2]), "avg_wave", [0.6, 0.4], 32768)
+    assert est.shape == ref.shape
+    assert np.abs(est - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max())
