@@ -78,3 +78,40 @@ def test_ensemble_separate_rejects_missing_stem():
     m, c = get_model_from_config("scnet", os.path.join(CONFIGS, "config_scnet_small.yaml"))
     with pytest.raises(ValueError):
         ensemble_separate([(c, m)], torch.zeros(2, 100), "guitar")
+
+
+FULL_MEMBERS = (("mdx23c", "config_vocals_mdx23c.yaml"), ("bs_roformer", "config_bs_roformer_vocals.yaml"),
+                ("scnet", "config_musdb18_scnet.yaml"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precisions", [("bf16x3", "bf16x3", "bf16x3"), ("fp16mix", "fp16", "bf16x3")],
+                         ids=["bf16x3", "bench"])
+def test_full_width_ensemble_matches_reference(golden, precisions):
+    """BASELINE configs[4] at full width: the three full-size members (the bench line's precisions: MDX23C
+    fp16mix, BS-Roformer fp16 Linears, SCNet bf16x3 -- and all bf16x3) on a 3 s mix, each stem and the
+    avg_wave (weighted) / median_fft blends against the REAL reference composition
+    (tests/golden/make_golden_ensemble_full.py: reference demix_pytorch_optimized per member, reference
+    AudioEnsembleEngine blend).  Gate: per-sample RMS <= 1e-4."""
+    from sesa.ensemble import ensemble_separate
+    from sesa.utils import get_model_from_config
+    from sesa.weights import synth_model_state, synth_state_dict
+    g = golden("ensemble_full.npz")
+    dev = torch.device("cuda:0")
+    members = []
+    for (kind, cfg_name), prec in zip(FULL_MEMBERS, precisions):
+        m, c = get_model_from_config(kind, os.path.join(CONFIGS, cfg_name))
+        m.load_state_dict(synth_state_dict(m, affine="unit") if kind == "mdx23c" else
+                          synth_model_state(m, affine="random"), strict=True)
+        m.set_precision(prec)
+        members.append((c, m))
+    mix_d = torch.from_numpy(g["mix"]).to(dev)
+    for method, key, w in (("avg_wave", "blend_avg_wave", list(g["weights"])), ("median_fft", "blend_median_fft", None)):
+        out, stems = ensemble_separate(members, mix_d, "vocals", method, weights=w, rank=0, world=1, exec_batch=2)
+        for i, (kind, _) in enumerate(FULL_MEMBERS):
+            err = rms(stems[i].cpu().numpy(), g[f"vocals_{kind}"])
+            print(f"{precisions} {kind} stem rms {err:.3e}")
+            assert err <= 1e-4, kind
+        err = rms(out.cpu().numpy(), g[key])
+        print(f"{precisions} {method} blend rms {err:.3e}")
+        assert out.shape == g[key].shape and err <= 1e-4

@@ -174,6 +174,23 @@ def test_demix_matches_reference(dev, path):
         assert rms(out[k], g[k]) <= RMS_GATE, k
 
 
+def test_side_streams_bit_identical_and_workspaces_bounded(dev):
+    """local_accumulate_device with streams = 2 / 3 (forwards alternate between the current stream and side
+    streams that are created once per process, sesa/parallel.py side_streams) equals streams = 1 bit for bit,
+    and repeated calls do not grow the model's per-(device, stream) workspace cache."""
+    from sesa.parallel import demix_sharded
+    m, c = _model("config_mdx23c_small.yaml", "random")
+    rng = np.random.default_rng(2)
+    mix = torch.from_numpy((0.1 * rng.standard_normal((2, 400000))).astype(np.float32)).to(dev)
+    a = demix_sharded(c, m, mix, dev, rank=0, world=1, exec_batch=3, streams=1)
+    for streams in (2, 3):
+        for _ in range(3):
+            b = demix_sharded(c, m, mix, dev, rank=0, world=1, exec_batch=3, streams=streams)
+            torch.cuda.synchronize()
+            assert torch.equal(a, b), streams
+    assert len(m._ws) <= 3
+
+
 def test_sharded_path_single_rank_matches_demix(dev):
     """bench.py's step (sesa/parallel.py at world 1) equals the plain device demix bit-for-bit."""
     from sesa.demix import demix_device

@@ -1,13 +1,17 @@
 #!/bin/bash
-# Round 4: MDX23C parity on the level / seed fixtures (every precision) and a same-box A/B of the fp16mix
-# plans against fp16 / fp16w2 (configs[1] headline bench, no CPU leg).
+# Round 4: MDX23C parity on the level / seed fixtures (every precision), the --enable_amp gate per model, the
+# full-width ensemble, side streams; then a same-box A/B of the fp16mix plans against fp16 / fp16w2
+# (configs[1] headline bench, no CPU leg).
 set -e
 O=gpurun_out/r04ab
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 echo "[r04ab] $(date +%T) parity"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread \
-  -k "levels or matrix" > $O/parity.txt 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_amp_precision.py tests/test_ensemble_models.py \
+  -v --timeout 300 --timeout-method thread \
+  -k "levels or matrix or amp or full_width or side_streams" > $O/parity.txt 2>&1 || rc=$?
+# plain test failures (exit 1) still allow the bench; a crash, abort or time limit ends the script here
+if [ "${rc:-0}" != 0 ]; then echo "[r04ab] parity rc=$rc"; [ "$rc" = 1 ] || exit "$rc"; fi
 run() {
   echo "[r04ab] $(date +%T) $1"
   timeout -k 10 300 env $2 python bench.py --precision $3 --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_$1.json 2> $O/bench_$1.err
