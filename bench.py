@@ -136,7 +136,7 @@ def default_precision(model):
 
 
 # kernel classes whose kernels run in the MDX23C precision mode; every other class is bf16x3 in the fp16 modes
-MDX_CLASSES = ("conv3x3", "conv1x1", "down", "up", "tdf", "act")
+MDX_CLASSES = ("conv3x3", "conv3x3_x3", "conv1x1", "down", "up", "tdf", "act")
 
 
 def class_precision(kclass, precision, model="mdx23c"):
@@ -181,7 +181,8 @@ def conv_plan_modes(precision, plan=None):
 
 def mdx23c_conv3x3_alg_bytes(cfg, batch, precision="bf16x3", plan=None):
     """Algorithmic HBM bytes of the conv3x3 class over one MDX23C forward of `batch` chunks, and its launch
-    count: each TFC 3x3 conv reads its input once -- fp32 for the fused-activation kernel (a bf16x3 / bf16
+    count (in the fp16 modes the class -- and so this count -- is the fp16 convs only; the bf16x3 ones are
+    conv3x3_x3): each TFC 3x3 conv reads its input once -- fp32 for the fused-activation kernel (a bf16x3 / bf16
     conv with T >= 32, C_out <= 128), else the act_split planes: bf16 hi + lo 4 B, one fp16 (the fp16 modes)
     or bf16 plane 2 B -- the fused 1x1 shortcut's raw input (4 B) for conv2, and writes its fp32 output
     (4 B); weights per coefficient 4 B (bf16 hi + lo, fp16 hi + lo), 2 B (bf16 or fp16 alone); the T < 32
@@ -191,12 +192,15 @@ def mdx23c_conv3x3_alg_bytes(cfg, batch, precision="bf16x3", plan=None):
     n, nb, c0, g = int(m.num_scales), int(m.num_blocks_per_scale), int(m.num_channels), int(m.growth)
     T0, F0 = int(cfg.audio.dim_t), int(cfg.audio.dim_f) // int(m.num_subbands)
     modes = conv_plan_modes(precision, plan)
+    f16mode = precision.startswith("fp16")   # then the conv3x3 class holds only the fp16 launches
     total, launches = 0.0, 0
 
     def stack(T, F, in_c, c, enc, lv):
         nonlocal total, launches
         pos = batch * T * F
         md = modes[(0 if enc else 8) + min(lv, 7)] if T >= 32 else ("b" if precision == "bf16" else "3")
+        if f16mode and md not in "12":
+            return
         if md in "12":
             a_in, wb = 2.0, (2.0 if md == "1" else 4.0)
         else:
@@ -603,8 +607,8 @@ def main():
                            "avg_launch_ms": round(kms / kn, 4), "bytes_per_launch": round(kbytes / kn)}
         line["hbm_kernels"] = {"peak_gbs": 8000.0, **hbm}
         classes = {}
-        for kc in ("conv3x3", "conv1x1", "down", "up", "tdf", "act", "tokgemm", "attn", "lstm", "simt", "hconv",
-                   "stft", "istft", "ola"):
+        for kc in ("conv3x3", "conv3x3_x3", "conv1x1", "down", "up", "tdf", "act", "tokgemm", "attn", "lstm", "simt",
+                   "hconv", "stft", "istft", "ola"):
             kms, kn, kw = _native.profile_read(kc)
             if kn:
                 classes[kc] = {"ms_per_step": round(kms / args.steps, 2), "launches": kn}

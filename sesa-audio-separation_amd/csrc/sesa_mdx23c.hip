@@ -431,7 +431,11 @@ struct Fwd {
       a.x_chunks = xin->C_in / kConvBK;
     }
     const int taps = w.kind == CONV3X3 ? 9 : (w.kind == CONV2X2S2 ? 4 : 1);
-    const int kclass = w.kind == CONV3X3 ? SESA_KCLASS_CONV3X3
+    // in the fp16 modes the conv3x3 class holds only the fp16 launches (one precision, one roofline peak);
+    // the 3x3 convs that stay bf16x3 there (plan '3', T < 32) are their own class
+    const bool f16mode = m->cfg.precision == SESA_PREC_F16 || m->cfg.precision == SESA_PREC_F16W2 ||
+                         m->cfg.precision == SESA_PREC_F16MIX;
+    const int kclass = w.kind == CONV3X3 ? (f16mode && !w.f16 ? SESA_KCLASS_CONV3X3_X3 : SESA_KCLASS_CONV3X3)
                        : w.kind == CONV1X1 ? SESA_KCLASS_CONV1X1
                        : w.kind == CONV2X2S2 ? SESA_KCLASS_DOWN : SESA_KCLASS_UP;
     void* tok = profile_begin(st);
