@@ -479,10 +479,12 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 // holds only the images the mode reads (one A, one W: 55 KB); the shortcut stages keep their bf16 hi / lo
 // layout (78 KB), so a stage is the larger of the two.
 constexpr int kActMaxC = 1024;
-template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0, bool MI4 = false>
+template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0, bool MI4 = false, bool SCR = false,
+          int SCD = 2>
 __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   static_assert(F16 == 0 || X3, "the fp16 modes keep the shortcut chunks bf16x3");
   static_assert(!MI4 || (F16 == 1 && !ACT), "MI4: fp16 single pass on pre-activated planes");
+  static_assert(!SCR || (XTRA && X3), "SCR: the bf16x3 fused shortcut from registers");
   constexpr bool ALO = X3 && F16 == 0;  // main chunks read an A lo image
   constexpr bool WLO = X3 && F16 != 1;  // main chunks read a W lo image
   constexpr int NT = 512;
@@ -851,8 +853,91 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
     }
     __syncthreads();
   }
-  // ---- fused 1x1 shortcut chunks (centre tap), same double-buffered pipeline ----
-  if (XTRA && a.x_chunks > 0) {
+  // ---- fused 1x1 shortcut chunks (centre tap) ----
+  if constexpr (XTRA && SCR) {
+    // Register-direct form: every lane loads its own A fragments straight from the raw fp32 block input
+    // (inner position (t0 + row, f0 + l32), channels 8h..8h+7 of the chunk: 32 contiguous bytes, the
+    // MFMA's row / k layout) and its B fragments from the packed W1 image (same byte layout as the LDS copy),
+    // splits A into bf16 hi / lo in registers and runs the bf16x3 MFMAs in the same order as the LDS form
+    // (bit-identical results).  No LDS and no barrier: each wave streams its own rows with SCD chunks in
+    // flight, so the phase is bounded by bytes in flight per CU, not by one chunk's latency per barrier.
+    const int nx = a.x_chunks;
+    const char* w1 = reinterpret_cast<const char*>(wblk + (int64_t)n_main * W_BYTES);
+    // the W1 images (hi + lo, 4 KiB per chunk) of up to kScrPiece chunks at a time live in LDS (free once the
+    // main loop's last barrier has passed): copied by LDS-DMA, one barrier per piece, then ds_read_b128 per
+    // fragment -- registers stay for the x stream
+    constexpr int kScrPiece = (2 * STAGE) / (2 * W1_BYTES) < 32 ? (2 * STAGE) / (2 * W1_BYTES) : 32;
+    auto copy_w1 = [&](int k0, int k1) {
+      const int pieces = (k1 - k0) * (2 * W1_BYTES / 1024);
+      for (int q = wm; q < pieces; q += 8)
+        __builtin_amdgcn_global_load_lds(w1 + (int64_t)k0 * 2 * W1_BYTES + q * 1024 + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(smem + q * 1024), 16, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    };
+    f32x4 xa[SCD][MI][2];
+    auto ld_row = [&](int s, int i, int kx) {
+      const int k0 = kx * kConvBK;
+      const int sx = k0 < a.xin.C_split ? 0 : 1;
+      const Src xs = pick_src(a.xin, sx);
+      const int cl0 = k0 - (sx ? a.xin.C_split : 0) + 8 * h;
+      const int t = min(t0 + wm * MI + i, a.T_in - 1);
+      const f32x4* q =
+          reinterpret_cast<const f32x4*>(xs.ptr + (((int64_t)b * a.T_in + t) * a.F_in + f0 + l32) * xs.C + cl0);
+      xa[s][i][0] = q[0];
+      xa[s][i][1] = q[1];
+    };
+    int piece0 = 0, piece1 = min(nx, kScrPiece);
+    copy_w1(piece0, piece1);
+    Unroll<0, SCD>::run([&](auto S) {
+      constexpr int s = decltype(S)::value;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) ld_row(s, i, min(s, nx - 1));
+    });
+    for (int kx0 = 0; kx0 < nx; kx0 += SCD) {
+      Unroll<0, SCD>::run([&](auto S) {
+        constexpr int s = decltype(S)::value;
+        const int kx = kx0 + s;
+        if (kx < nx) {
+          if (kx == piece1) {   // next piece of W1 images (every wave reaches this with the same kx)
+            __syncthreads();    // all reads of the previous piece are done
+            piece0 = piece1;
+            piece1 = min(nx, piece1 + kScrPiece);
+            copy_w1(piece0, piece1);
+          }
+          const char* wl = smem + (kx - piece0) * 2 * W1_BYTES;
+          bf16x8 bh[NI], bl[NI];
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int p = j * 32 + l32;
+            const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+            bh[j] = *reinterpret_cast<const bf16x8*>(wl + off);
+            bl[j] = *reinterpret_cast<const bf16x8*>(wl + W1_BYTES + off);
+          }
+          const bool refill = kx + SCD < nx;
+          // row by row: split row i, refill its registers with chunk kx + SCD, then its MFMAs -- so only one
+          // row's hi / lo fragments are live beside the in-flight loads
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const bool ok = t0 + wm * MI + i < a.T_in;
+            __bf16 hv[8], lv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) split_bf16(ok ? xa[s][i][q >> 2][q & 3] : 0.f, hv[q], lv[q]);
+            const bf16x8 ah = bf16x8{hv[0], hv[1], hv[2], hv[3], hv[4], hv[5], hv[6], hv[7]};
+            const bf16x8 al = bf16x8{lv[0], lv[1], lv[2], lv[3], lv[4], lv[5], lv[6], lv[7]};
+            if (refill) ld_row(s, i, kx + SCD);
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+              acc[i][j] = mfma32(al, bh[j], acc[i][j]);
+              acc[i][j] = mfma32(ah, bl[j], acc[i][j]);
+              acc[i][j] = mfma32(ah, bh[j], acc[i][j]);
+            }
+          }
+        }
+      });
+    }
+    __syncthreads();   // the epilogue's statistics reduction reuses the LDS
+  } else if (XTRA && a.x_chunks > 0) {
     const int nx = a.x_chunks;
     load_ext(0);
     store_ext(smem);

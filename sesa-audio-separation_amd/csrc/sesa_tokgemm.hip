@@ -1024,7 +1024,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // fp32 rows -> bf16 hi / lo planes (+ RMSNorm row scale): one wave per row, f32x4 per lane-step.
-// F16: one fp16 plane (round to nearest even) -- the A operand of the fp16 single-pass Linears.
+// F16: one fp16 plane (round to nearest even) -- the A operand of the fp16 single-pass Linears.  With a
+// row_scale output the fp16 plane holds x * row_scale (the RMS-normalised row, |value| <= sqrt(K)), not the raw
+// residual stream: a raw |x| > 65504 would round to inf in fp16, and the fp16 GEMMs then skip EP_RS.
 template <bool F16>
 __global__ void __launch_bounds__(256) tok_split_kernel(const float* __restrict__ x, int64_t x_ld, int64_t M, int K,
                                                         uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
@@ -1034,20 +1036,32 @@ __global__ void __launch_bounds__(256) tok_split_kernel(const float* __restrict_
   if (m >= M) return;
   const float* xr = x + m * x_ld;
   float ss = 0.f;
-  for (int k = lane * 4; k < K; k += 256) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + k);
-    if constexpr (F16) {
+  if constexpr (F16) {
+    float rs = 1.f;
+    if (row_scale) {   // pass 1: the row's sum of squares (the second pass re-reads the row from L1 / L2)
+      for (int k = lane * 4; k < K; k += 256) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(xr + k);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ss = fmaf(v[q], v[q], ss);
+      }
+#pragma unroll
+      for (int s = 32; s >= 1; s >>= 1) ss += __shfl_xor(ss, s);
+      rs = sqrtf((float)K) / fmaxf(sqrtf(ss), 1e-12f);
+      if (lane == 0) row_scale[m] = rs;
+    }
+    for (int k = lane * 4; k < K; k += 256) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xr + k);
       uint32_t w[2];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        ss = fmaf(v[2 * q], v[2 * q], ss);
-        ss = fmaf(v[2 * q + 1], v[2 * q + 1], ss);
-        w[q] = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v[2 * q]) |
-               ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v[2 * q + 1]) << 16);
-      }
+      for (int q = 0; q < 2; ++q)
+        w[q] = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(v[2 * q] * rs)) |
+               ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(v[2 * q + 1] * rs)) << 16);
       *reinterpret_cast<uint2*>(hi + m * p_ld + k) = make_uint2(w[0], w[1]);
-      continue;
     }
+    return;
+  }
+  for (int k = lane * 4; k < K; k += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + k);
     __bf16 h[4], l[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1107,12 +1121,13 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
     // the specialised forms); SESA_TOKGEMM_GLDS=0 selects the register-staged kernel for A/B runs
     static const int glds = getenv("SESA_TOKGEMM_GLDS") ? atoi(getenv("SESA_TOKGEMM_GLDS")) : 1;
     int ep = -1;
-    // x3 == 2: fp16 A planes x fp16 weight images, one pass (SESA_PREC_F16 Linears; LDS-DMA kernel only)
+    // x3 == 2: fp16 A planes x fp16 weight images, one pass (SESA_PREC_F16 Linears; LDS-DMA kernel only).
+    // A rownorm fp16 A plane is already row-scaled by tok_split_kernel<true>, so those epilogues skip EP_RS.
     const bool f16 = x3 == 2;
     if ((glds || f16) && x3 && a.k8 && a.a_ld % 8 == 0 && !a.glu && !a.conv && a.o_ld % 4 == 0 &&
         (a.act == TOK_ACT_NONE || a.act == TOK_ACT_GELU) && (!a.rope || (a.dim_head == 64 && !a.residual)) &&
         (!a.out_hi || a.out_lo || f16) && (!a.residual || a.n4)) {
-      ep = (a.rownorm ? EP_RS : 0) | (a.rope ? EP_ROPE : 0) | (a.act == TOK_ACT_GELU ? EP_GELU : 0) |
+      ep = (a.rownorm && !f16 ? EP_RS : 0) | (a.rope ? EP_ROPE : 0) | (a.act == TOK_ACT_GELU ? EP_GELU : 0) |
            (a.residual ? EP_RES : 0) | (a.out_hi ? EP_SPLIT : 0) | (f16 ? EP_F16 : 0);
     }
     const dim3 gbig((unsigned)(((a.M + 255) / 256) * ((a.n_tiles_n + 1) / 2)), (unsigned)a.n_groups);
@@ -1128,9 +1143,9 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
       case EP_GELU | EP_SPLIT: SESA_GLDS(EP_GELU | EP_SPLIT) break;
       case EP_SPLIT: SESA_GLDS(EP_SPLIT) break;                       // q / k / v planes for attention
       case EP_RS | EP_ROPE | EP_SPLIT: SESA_GLDS(EP_RS | EP_ROPE | EP_SPLIT) break;
-      case EP_F16 | EP_RS | EP_GELU | EP_SPLIT: SESA_GLDS(EP_F16 | EP_RS | EP_GELU | EP_SPLIT) break;  // FF1
+      case EP_F16 | EP_GELU | EP_SPLIT: SESA_GLDS(EP_F16 | EP_GELU | EP_SPLIT) break;  // FF1 (A pre-scaled)
       case EP_F16 | EP_RES: SESA_GLDS(EP_F16 | EP_RES) break;                                         // FF2
-      case EP_F16 | EP_RS | EP_ROPE: SESA_GLDS(EP_F16 | EP_RS | EP_ROPE) break;                       // QKV
+      case EP_F16 | EP_ROPE: SESA_GLDS(EP_F16 | EP_ROPE) break;                       // QKV (A pre-scaled)
       default: ep = -1;
     }
     SESA_REQUIRE(!f16 || ep >= 0, SESA_ERR_INVALID, "tok_gemm: no fp16 kernel for this epilogue / shape");

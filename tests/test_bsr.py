@@ -211,3 +211,29 @@ def test_forward_fp16_linears_match_reference(golden, dev, fixture, cfg_name, me
     err = rms(y, g["y"])
     print(f"{fixture} (fp16 Linears): rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
     assert np.isfinite(y).all() and err <= RMS_GATE
+
+
+@pytest.mark.gpu
+def test_fp16_linears_large_residual_stream(golden, dev):
+    """fp16 Linears with a residual stream far outside fp16 range: the band-split Linears scaled by 1e5 make
+    |X| ~ 1e5 (> 65504).  The fp16 A plane holds the RMS-normalised row (tok_split_kernel<true>), so nothing
+    overflows; against the oracle (PyTorch-CPU fp32 restatement, pinned to the reference goldens) on the same
+    scaled weights, same 1e-4 gate."""
+    from oracle import bs_roformer as ob
+    g = golden("bsr_small.npz")
+    cfg_path = os.path.join(CONFIGS, "config_bs_roformer_small.yaml")
+    ocfg = ob.load_cfg(cfg_path)
+    sd = ob.synth_params(ocfg, str(g["affine"]))
+    for k in sd:
+        if k.startswith("band_split.to_features.") and (k.endswith(".1.weight") or k.endswith(".1.bias")):
+            sd[k] = (sd[k] * np.float32(1e5)).astype(np.float32)
+    with torch.inference_mode():
+        ref = ob.forward(ob.to_torch(sd), ocfg, torch.from_numpy(g["x"])).numpy()
+    from sesa.utils import get_model_from_config
+    m, _ = get_model_from_config("bs_roformer", cfg_path)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    m.set_precision("fp16")
+    y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    err = rms(y, ref)
+    print(f"large residual (|X| ~ 1e5) fp16 Linears: rms {err:.3e} (ref rms {rms(ref, 0):.3e})")
+    assert np.isfinite(y).all() and err <= RMS_GATE

@@ -6,10 +6,12 @@ set -e
 O=gpurun_out/r04ab
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+echo "[r04ab] $(date +%T) conv_bench f16 (shortcut phase: LDS vs register-direct)"
+timeout -k 10 300 ./tools/conv_bench 57 f16 > $O/conv_f16.txt 2>&1
 echo "[r04ab] $(date +%T) parity"
 timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_amp_precision.py tests/test_ensemble_models.py \
   -v --timeout 300 --timeout-method thread \
-  -k "levels or matrix or amp or full_width or side_streams" > $O/parity.txt 2>&1 || rc=$?
+  tests/test_bsr.py -k "levels or matrix or amp or full_width or side_streams or fp16" > $O/parity.txt 2>&1 || rc=$?
 # plain test failures (exit 1) still allow the bench; a crash, abort or time limit ends the script here
 if [ "${rc:-0}" != 0 ]; then echo "[r04ab] parity rc=$rc"; [ "$rc" = 1 ] || exit "$rc"; fi
 run() {
