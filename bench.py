@@ -54,7 +54,7 @@ CFG_DIR = os.path.join(REPO, "sesa-audio-separation_amd", "sesa", "configs")
 MODELS = {
     "mdx23c": ("config_vocals_mdx23c.yaml", 2.4341e12, "conv3x3"),
     "bs_roformer": ("config_bs_roformer_vocals.yaml", 8.5923e12, "tokgemm"),
-    "scnet": ("config_musdb18_scnet.yaml", 4.072e11, "lstm"),
+    "scnet": ("config_musdb18_scnet.yaml", 4.072e11, None),
     "htdemucs": ("config_musdb18_htdemucs.yaml", 4.857e11, None),
 }
 ENSEMBLE = ("mdx23c", "bs_roformer", "scnet")
@@ -78,12 +78,15 @@ TRACK_SECONDS = {"htdemucs": 1800.0}
 # rank's last forward is not a small remainder (169 chunks at N=1 -> 3 forwards of 57; 22 per rank at
 # N=8 -> one forward of 22)
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
+FP32_VECTOR_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table (fp32 vector)
 KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "tokgemm": "tok_gemm_glds_kernel + tok_gemm_kernel (token-major Linear layers, bf16x3 "
                     "v_mfma_f32_32x32x16_bf16 / v_mfma_f32_16x16x32_bf16)",
          "lstm": "scn_lstm_mfma_kernel (bi-LSTM recurrence, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "hconv": "tok_gemm_kernel<conv> (HTDemucs implicit-GEMM convolutions, v_mfma_f32_32x32x16_bf16)",
-         "attn": "attn_kernel (flash attention, S^T = K Q^T, bf16x3 v_mfma_f32_32x32x16_bf16)"}
+         "attn": "attn_kernel (flash attention, S^T = K Q^T, bf16x3 v_mfma_f32_32x32x16_bf16)",
+         "simt": "SCNet fp32 VALU kernels (scn_cm_in / scn_cm_out ConvolutionModule, scn_sdconv / scn_convtr band "
+                 "convs, scn_rfft / scn_irfft feature conversion)"}
 
 
 def kdesc(kclass, precision, model):
@@ -114,7 +117,8 @@ _MDX_SRC = ("sesa_tapgemm.hip", "sesa_tapgemm.hpp", "sesa_common.hpp", "sesa_mdx
 _TOK_SRC = ("sesa_tokgemm.hip", "sesa_tokgemm.hpp", "sesa_common.hpp")
 KSRC = {"conv3x3": _MDX_SRC, "tdf": _MDX_SRC, "act": _MDX_SRC, "conv1x1": _MDX_SRC, "down": _MDX_SRC,
         "up": _MDX_SRC, "tokgemm": _TOK_SRC + ("sesa_bsroformer.hip",), "attn": _TOK_SRC + ("sesa_bsroformer.hip",),
-        "hconv": _TOK_SRC + ("sesa_htdemucs.hip",), "lstm": ("sesa_scnet.hip", "sesa_tokgemm.hpp", "sesa_common.hpp")}
+        "hconv": _TOK_SRC + ("sesa_htdemucs.hip",), "lstm": ("sesa_scnet.hip", "sesa_tokgemm.hpp", "sesa_common.hpp"),
+        "simt": ("sesa_scnet.hip", "sesa_common.hpp"), "conv3x3_x3": _MDX_SRC}
 
 
 def kernel_sources_sha16(kclass):
@@ -531,7 +535,7 @@ def main():
     # dominant kernel class: the model's own, or the class with the most kernel time
     kclass = MODELS[args.model][2]
     if kclass is None:
-        kclass = max(("conv3x3", "tokgemm", "lstm", "hconv", "attn"), key=lambda k: _native.profile_read(k)[0])
+        kclass = max(("conv3x3", "tokgemm", "lstm", "hconv", "attn", "simt"), key=lambda k: _native.profile_read(k)[0])
     ms, launches, work = _native.profile_read(kclass)
     # MFMA passes per algorithmic FLOP of the dominant class (fp16 has the same dense peak as bf16); in the
     # fp16 modes the conv3x3 class is the fp16 direct convs (the T < 32 tap_gemm 3x3s, ~2 % of its FLOPs,
@@ -549,6 +553,10 @@ def main():
                 f"{f16_plan()}), priced at the fp16 peak (the conservative choice)")
     if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
         peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
+    bound = "mfma"
+    if kclass == "simt":  # SCNet's fp32 VALU kernels (band convs, ConvolutionModule, feature-conversion DFTs)
+        peak, bound = FP32_VECTOR_TFLOPS, "valu"
+        note = "157.3 TF/s fp32 vector FMA peak (MI355X_MICROARCH.md chip table; these kernels use no MFMA)"
     traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model))
     alg_bytes = None
     if kclass == "conv3x3":
@@ -561,7 +569,7 @@ def main():
         alg_bytes = round(per_fwd / max(l_fwd, 1))
     if isinstance(traffic_src, dict):   # one algorithmic figure: this run's (the PMC file's own is for its run)
         traffic_src.pop("algorithmic_bytes_per_launch", None)
-    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+    roof = {"bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": kdesc(kclass, args.precision, args.model),
             "launches": launches, "avg_launch_ms": round(ms / max(launches, 1), 4),
             "flop_per_launch": round(work / max(launches, 1)), "peak_note": note, "traffic_source": traffic_src,

@@ -443,7 +443,7 @@ extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
   const int dim = c.dim, inner = m->inner;
   std::vector<uint16_t> blob;
   std::vector<float> bias;
-  const bool f16p = c.precision == SESA_PREC_F16;  // QKV / FF1 / FF2 weight images in fp16 (one-pass Linears)
+  const bool f16p = c.precision == SESA_PREC_F16;  // QKV / out / FF1 / FF2 weight images in fp16 (one-pass Linears)
   std::vector<float2> rope;
   // band split: W' = W diag(gamma) (RMSNorm folded)
   m->band.groups.clear();
@@ -477,7 +477,7 @@ extern "C" int sesa_bsr_finalize(sesa_bsr* m, void* stream) {
     L.qkv.groups = {g};
     const auto& Wo = P(m, p + ".0.to_out.0.weight");
     g = pack_group(dim, inner, [&](int n, int k) { return Wo[(int64_t)n * inner + k]; }, false, [](int) { return 0.f; },
-                   blob, bias);
+                   blob, bias, f16p);
     g.x_off = g.o_off = 0;
     L.out.groups = {g};
     const auto& W1 = P(m, p + ".1.net.1.weight");
@@ -684,8 +684,9 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
   float* XG = reinterpret_cast<float*>(ws + pl.xg);
   float* H2 = reinterpret_cast<float*>(ws + pl.h2);
   float* MASKG = reinterpret_cast<float*>(ws + pl.maskg);
-  // SESA_PREC_F16: the QKV / FF1 / FF2 Linears one fp16 pass (fp16 A planes, fp16 weight images; tok_gemm
-  // x3 = 2); band split, attention, out-projection and mask MLPs bf16x3
+  // SESA_PREC_F16: the QKV / out-projection / FF1 / FF2 Linears one fp16 pass (fp16 A planes, fp16 weight
+  // images; tok_gemm x3 = 2) and the attention's QK^T / PV one fp16 pass (attn_f16_kernel); band split and
+  // mask MLPs bf16x3
   const bool f16 = c.precision == SESA_PREC_F16;
   const int x3 = c.precision == SESA_PREC_BF16 ? 0 : 1;
   const int ch = c.audio_channels, dim = c.dim;
@@ -783,7 +784,8 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
       a.g_off = 3 * m->inner;
       a.out = AO;
       a.out_hi = AOhi;
-      a.out_lo = AOlo;
+      a.out_lo = f16 ? nullptr : AOlo;
+      a.out_f16 = f16;   // fp16: one fp16 plane, the fp16 out-projection's A
       a.o_ld = m->inner;
       if (qp) {
         a.qkv_hi = QKVhi;
@@ -806,14 +808,14 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
         a.pstride = 1;
       }
       void* t0 = profile_begin(st);
-      rc = launch_attention(a, x3, st);
+      rc = launch_attention(a, f16 ? 2 : x3, st);   // fp16: QK^T / PV on one fp16 pass
       profile_end(t0, st, SESA_KCLASS_ATTN, 4.0 * (double)a.n_seq * c.heads * (double)a.L * a.L * c.dim_head);
     }
     {
       TokGemmArgs a = gemm_args(m, L.out, AO, m->inner, X, dim, M);
-      pre(a, AOhi, AOlo, m->inner);
+      pre(a, AOhi, f16 ? AOhi : AOlo, m->inner);
       a.residual = X;
-      gemm(a, L.out, M);
+      gemm(a, L.out, M, f16);
     }
     split_x();
     {

@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 // layout (78 KB), so a stage is the larger of the two.
 constexpr int kActMaxC = 1024;
 template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0, bool MI4 = false, bool SCR = false,
-          int SCD = 2>
+          int SCD = 2, bool ORD = false>
 __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   static_assert(F16 == 0 || X3, "the fp16 modes keep the shortcut chunks bf16x3");
   static_assert(!MI4 || (F16 == 1 && !ACT), "MI4: fp16 single pass on pre-activated planes");
@@ -761,198 +761,214 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   constexpr std::true_type kExt{};
 
   // ---- main chunks: straight-line pipelined body, clamped (redundant) prefetch at the tail ----
-  load_main(0);
-  if constexpr (ACT) __syncthreads();   // the LDS affine table, before the first staging step reads it
-  store_main(smem, 0);
-  load_main(min(1, n_main - 1));
-  __syncthreads();
-  for (int kc = 0; kc < n_main; ++kc) {
-    char* cur = smem + (kc & 1) * STAGE;
-    char* nxt = smem + ((kc + 1) & 1) * STAGE;
-    Frags fr[2];
-    if constexpr (MI4) {
-      // dx-major: the 6 halo-row A fragments of column shift dx, then the 3 dy taps (B double-buffered)
-      const char* Wm = cur + WOFF_M;
-      auto read_b = [&](bf16x8* bq, int tap) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int p = tap * BN + j * 32 + l32;
-          bq[j] = *reinterpret_cast<const bf16x8*>(Wm + p * 32 + ((h ^ ((p >> 3) & 1)) << 4));
-        }
-      };
-      bf16x8 bq[2][NI];
-      read_b(bq[0], 0);
-      Unroll<0, 3>::run([&](auto DX) {
-        constexpr int dx = decltype(DX)::value;
-        bf16x8 ar[MI + 2];
-#pragma unroll
-        for (int r = 0; r < MI + 2; ++r) {
-          const int p = (wm * MI + r) * HW + l32 + dx;
-          ar[r] = *reinterpret_cast<const bf16x8*>(cur + p * 32 + ((h ^ ((p >> 3) & 1)) << 4));
-        }
-        Unroll<0, 3>::run([&](auto DY) {
-          constexpr int dy = decltype(DY)::value, q = dx * 3 + dy;  // q: order of this tap
-          constexpr int nq = q + 1, ntap = (nq % 3) * 3 + nq / 3;   // the next tap in dx-major order
-          if (nq < 9) read_b(bq[nq & 1], ntap);
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NI; ++j) acc[i][j] = mfma32h(ar[i + dy], bq[q & 1][j], acc[i][j]);
-          if (q == 1) {
+  auto main_phase = [&]() __attribute__((always_inline)) {
+    load_main(0);
+    if constexpr (ACT) __syncthreads();   // the LDS affine table, before the first staging step reads it
+    store_main(smem, 0);
+    load_main(min(1, n_main - 1));
+    __syncthreads();
+    for (int kc = 0; kc < n_main; ++kc) {
+      char* cur = smem + (kc & 1) * STAGE;
+      char* nxt = smem + ((kc + 1) & 1) * STAGE;
+      Frags fr[2];
+      if constexpr (MI4) {
+        // dx-major: the 6 halo-row A fragments of column shift dx, then the 3 dy taps (B double-buffered)
+        const char* Wm = cur + WOFF_M;
+        auto read_b = [&](bf16x8* bq, int tap) __attribute__((always_inline)) {
+  #pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int p = tap * BN + j * 32 + l32;
+            bq[j] = *reinterpret_cast<const bf16x8*>(Wm + p * 32 + ((h ^ ((p >> 3) & 1)) << 4));
+          }
+        };
+        bf16x8 bq[2][NI];
+        read_b(bq[0], 0);
+        Unroll<0, 3>::run([&](auto DX) {
+          constexpr int dx = decltype(DX)::value;
+          bf16x8 ar[MI + 2];
+  #pragma unroll
+          for (int r = 0; r < MI + 2; ++r) {
+            const int p = (wm * MI + r) * HW + l32 + dx;
+            ar[r] = *reinterpret_cast<const bf16x8*>(cur + p * 32 + ((h ^ ((p >> 3) & 1)) << 4));
+          }
+          Unroll<0, 3>::run([&](auto DY) {
+            constexpr int dy = decltype(DY)::value, q = dx * 3 + dy;  // q: order of this tap
+            constexpr int nq = q + 1, ntap = (nq % 3) * 3 + nq / 3;   // the next tap in dx-major order
+            if (nq < 9) read_b(bq[nq & 1], ntap);
+  #pragma unroll
+            for (int i = 0; i < MI; ++i)
+  #pragma unroll
+              for (int j = 0; j < NI; ++j) acc[i][j] = mfma32h(ar[i + dy], bq[q & 1][j], acc[i][j]);
+            if (q == 1) {
+              store_main(nxt, min(kc + 1, n_main - 1));
+              load_main(min(kc + 2, n_main - 1));
+            }
+          });
+        });
+        __syncthreads();
+        continue;
+      }
+      read_frags(fr[0], cur, 0, 0, 0, W_BYTES, kMain);
+      if constexpr (!ACT) {
+        Unroll<0, 9>::run([&](auto T) {
+          constexpr int tap = decltype(T)::value;
+          if (tap + 1 < 9) read_frags(fr[(tap + 1) & 1], cur, (tap + 1) / 3, (tap + 1) % 3, tap + 1, W_BYTES, kMain);
+          mfmas(fr[tap & 1], kMain);
+          if (tap == 1) {
+            // stage chunk kc+1 (in registers since the previous iteration) under the MFMAs, then start
+            // loading chunk kc+2; past the end both are harmless repeats of the last chunk
             store_main(nxt, min(kc + 1, n_main - 1));
             load_main(min(kc + 2, n_main - 1));
           }
         });
-      });
-      __syncthreads();
-      continue;
-    }
-    read_frags(fr[0], cur, 0, 0, 0, W_BYTES, kMain);
-    if constexpr (!ACT) {
-      Unroll<0, 9>::run([&](auto T) {
-        constexpr int tap = decltype(T)::value;
-        if (tap + 1 < 9) read_frags(fr[(tap + 1) & 1], cur, (tap + 1) / 3, (tap + 1) % 3, tap + 1, W_BYTES, kMain);
-        mfmas(fr[tap & 1], kMain);
-        if (tap == 1) {
-          // stage chunk kc+1 (in registers since the previous iteration) under the MFMAs, then start
-          // loading chunk kc+2; past the end both are harmless repeats of the last chunk
-          store_main(nxt, min(kc + 1, n_main - 1));
-          load_main(min(kc + 2, n_main - 1));
-        }
-      });
-    } else {
-      // ACT: the staging of chunk kc+1 is VALU-heavy (~27 VALU per element, ~6 per MFMA), and left to
-      // the scheduler it clumps after one tap, idling the matrix pipe while both waves of a SIMD do it
-      // together.  So it is cut into 12 slices -- one (item, channel pair) each, ~54 VALU -- pinned by
-      // sched_barrier between the 36 three-MFMA accumulator groups of the iteration (one slice after
-      // every third group); an item's LDS write and its reload with chunk kc+2 follow its last pair.
-      const int ks = min(kc + 1, n_main - 1), kl = min(kc + 2, n_main - 1);
-      load_aff(ks);
-      Unroll<0, 9>::run([&](auto T) {
-        constexpr int tap = decltype(T)::value;
-        if (tap + 1 < 9) read_frags(fr[(tap + 1) & 1], cur, (tap + 1) / 3, (tap + 1) % 3, tap + 1, W_BYTES, kMain);
-        Unroll<0, MI * NI>::run([&](auto G) {
-          constexpr int g = decltype(G)::value, gi = 4 * tap + g;
-          mfma_group(fr[tap & 1], g / NI, g % NI, kMain);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (gi == 0) {
-            store_w(nxt);
-            load_w(kl);
-          }
-          if constexpr (gi % 3 == 1 && gi / 3 < 4 * P_ITEMS) {
-            constexpr int sl = gi / 3, it = sl / 4, q = sl % 4;
-            xform_pair(std::integral_constant<int, it>{}, std::integral_constant<int, q>{});
-            if constexpr (q == 3) {
-              write_item(std::integral_constant<int, it>{}, nxt);
-              load_item(std::integral_constant<int, it>{}, kl);
+      } else {
+        // ACT: the staging of chunk kc+1 is VALU-heavy (~27 VALU per element, ~6 per MFMA), and left to
+        // the scheduler it clumps after one tap, idling the matrix pipe while both waves of a SIMD do it
+        // together.  So it is cut into 12 slices -- one (item, channel pair) each, ~54 VALU -- pinned by
+        // sched_barrier between the 36 three-MFMA accumulator groups of the iteration (one slice after
+        // every third group); an item's LDS write and its reload with chunk kc+2 follow its last pair.
+        const int ks = min(kc + 1, n_main - 1), kl = min(kc + 2, n_main - 1);
+        load_aff(ks);
+        Unroll<0, 9>::run([&](auto T) {
+          constexpr int tap = decltype(T)::value;
+          if (tap + 1 < 9) read_frags(fr[(tap + 1) & 1], cur, (tap + 1) / 3, (tap + 1) % 3, tap + 1, W_BYTES, kMain);
+          Unroll<0, MI * NI>::run([&](auto G) {
+            constexpr int g = decltype(G)::value, gi = 4 * tap + g;
+            mfma_group(fr[tap & 1], g / NI, g % NI, kMain);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (gi == 0) {
+              store_w(nxt);
+              load_w(kl);
             }
-          }
-          __builtin_amdgcn_sched_barrier(0);
+            if constexpr (gi % 3 == 1 && gi / 3 < 4 * P_ITEMS) {
+              constexpr int sl = gi / 3, it = sl / 4, q = sl % 4;
+              xform_pair(std::integral_constant<int, it>{}, std::integral_constant<int, q>{});
+              if constexpr (q == 3) {
+                write_item(std::integral_constant<int, it>{}, nxt);
+                load_item(std::integral_constant<int, it>{}, kl);
+              }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          });
         });
-      });
-    }
-    __syncthreads();
-  }
-  // ---- fused 1x1 shortcut chunks (centre tap) ----
-  if constexpr (XTRA && SCR) {
-    // Register-direct form: every lane loads its own A fragments straight from the raw fp32 block input
-    // (inner position (t0 + row, f0 + l32), channels 8h..8h+7 of the chunk: 32 contiguous bytes, the
-    // MFMA's row / k layout) and its B fragments from the packed W1 image (same byte layout as the LDS copy),
-    // splits A into bf16 hi / lo in registers and runs the bf16x3 MFMAs in the same order as the LDS form
-    // (bit-identical results).  No LDS and no barrier: each wave streams its own rows with SCD chunks in
-    // flight, so the phase is bounded by bytes in flight per CU, not by one chunk's latency per barrier.
-    const int nx = a.x_chunks;
-    const char* w1 = reinterpret_cast<const char*>(wblk + (int64_t)n_main * W_BYTES);
-    // the W1 images (hi + lo, 4 KiB per chunk) of up to kScrPiece chunks at a time live in LDS (free once the
-    // main loop's last barrier has passed): copied by LDS-DMA, one barrier per piece, then ds_read_b128 per
-    // fragment -- registers stay for the x stream
-    constexpr int kScrPiece = (2 * STAGE) / (2 * W1_BYTES) < 32 ? (2 * STAGE) / (2 * W1_BYTES) : 32;
-    auto copy_w1 = [&](int k0, int k1) {
-      const int pieces = (k1 - k0) * (2 * W1_BYTES / 1024);
-      for (int q = wm; q < pieces; q += 8)
-        __builtin_amdgcn_global_load_lds(w1 + (int64_t)k0 * 2 * W1_BYTES + q * 1024 + lane * 16,
-                                         (__attribute__((address_space(3))) void*)(smem + q * 1024), 16, 0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __syncthreads();
-    };
-    f32x4 xa[SCD][MI][2];
-    auto ld_row = [&](int s, int i, int kx) {
-      const int k0 = kx * kConvBK;
-      const int sx = k0 < a.xin.C_split ? 0 : 1;
-      const Src xs = pick_src(a.xin, sx);
-      const int cl0 = k0 - (sx ? a.xin.C_split : 0) + 8 * h;
-      const int t = min(t0 + wm * MI + i, a.T_in - 1);
-      const f32x4* q =
-          reinterpret_cast<const f32x4*>(xs.ptr + (((int64_t)b * a.T_in + t) * a.F_in + f0 + l32) * xs.C + cl0);
-      xa[s][i][0] = q[0];
-      xa[s][i][1] = q[1];
-    };
-    int piece0 = 0, piece1 = min(nx, kScrPiece);
-    copy_w1(piece0, piece1);
-    Unroll<0, SCD>::run([&](auto S) {
-      constexpr int s = decltype(S)::value;
-#pragma unroll
-      for (int i = 0; i < MI; ++i) ld_row(s, i, min(s, nx - 1));
-    });
-    for (int kx0 = 0; kx0 < nx; kx0 += SCD) {
+    }
+  };
+  // ---- fused 1x1 shortcut chunks (centre tap) ----
+  auto shortcut_phase = [&]() __attribute__((always_inline)) {
+    if constexpr (XTRA && SCR) {
+      // Register-direct form: every lane loads its own A fragments straight from the raw fp32 block input
+      // (inner position (t0 + row, f0 + l32), channels 8h..8h+7 of the chunk: 32 contiguous bytes, the
+      // MFMA's row / k layout) and its B fragments from the packed W1 image (same byte layout as the LDS copy),
+      // splits A into bf16 hi / lo in registers and runs the bf16x3 MFMAs in the same order as the LDS form
+      // (bit-identical results).  No LDS and no barrier: each wave streams its own rows with SCD chunks in
+      // flight, so the phase is bounded by bytes in flight per CU, not by one chunk's latency per barrier.
+      const int nx = a.x_chunks;
+      const char* w1 = reinterpret_cast<const char*>(wblk + (int64_t)n_main * W_BYTES);
+      // the W1 images (hi + lo, 4 KiB per chunk) of up to kScrPiece chunks at a time live in LDS (free once the
+      // main loop's last barrier has passed): copied by LDS-DMA, one barrier per piece, then ds_read_b128 per
+      // fragment -- registers stay for the x stream
+      constexpr int kScrPiece = (2 * STAGE) / (2 * W1_BYTES) < 32 ? (2 * STAGE) / (2 * W1_BYTES) : 32;
+      auto copy_w1 = [&](int k0, int k1) {
+        const int pieces = (k1 - k0) * (2 * W1_BYTES / 1024);
+        for (int q = wm; q < pieces; q += 8)
+          __builtin_amdgcn_global_load_lds(w1 + (int64_t)k0 * 2 * W1_BYTES + q * 1024 + lane * 16,
+                                           (__attribute__((address_space(3))) void*)(smem + q * 1024), 16, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      };
+      f32x4 xa[SCD][MI][2];
+      auto ld_row = [&](int s, int i, int kx) {
+        const int k0 = kx * kConvBK;
+        const int sx = k0 < a.xin.C_split ? 0 : 1;
+        const Src xs = pick_src(a.xin, sx);
+        const int cl0 = k0 - (sx ? a.xin.C_split : 0) + 8 * h;
+        const int t = min(t0 + wm * MI + i, a.T_in - 1);
+        const f32x4* q =
+            reinterpret_cast<const f32x4*>(xs.ptr + (((int64_t)b * a.T_in + t) * a.F_in + f0 + l32) * xs.C + cl0);
+        xa[s][i][0] = q[0];
+        xa[s][i][1] = q[1];
+      };
+      int piece0 = 0, piece1 = min(nx, kScrPiece);
+      copy_w1(piece0, piece1);
       Unroll<0, SCD>::run([&](auto S) {
         constexpr int s = decltype(S)::value;
-        const int kx = kx0 + s;
-        if (kx < nx) {
-          if (kx == piece1) {   // next piece of W1 images (every wave reaches this with the same kx)
-            __syncthreads();    // all reads of the previous piece are done
-            piece0 = piece1;
-            piece1 = min(nx, piece1 + kScrPiece);
-            copy_w1(piece0, piece1);
-          }
-          const char* wl = smem + (kx - piece0) * 2 * W1_BYTES;
-          bf16x8 bh[NI], bl[NI];
-#pragma unroll
-          for (int j = 0; j < NI; ++j) {
-            const int p = j * 32 + l32;
-            const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
-            bh[j] = *reinterpret_cast<const bf16x8*>(wl + off);
-            bl[j] = *reinterpret_cast<const bf16x8*>(wl + W1_BYTES + off);
-          }
-          const bool refill = kx + SCD < nx;
-          // row by row: split row i, refill its registers with chunk kx + SCD, then its MFMAs -- so only one
-          // row's hi / lo fragments are live beside the in-flight loads
-#pragma unroll
-          for (int i = 0; i < MI; ++i) {
-            const bool ok = t0 + wm * MI + i < a.T_in;
-            __bf16 hv[8], lv[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) split_bf16(ok ? xa[s][i][q >> 2][q & 3] : 0.f, hv[q], lv[q]);
-            const bf16x8 ah = bf16x8{hv[0], hv[1], hv[2], hv[3], hv[4], hv[5], hv[6], hv[7]};
-            const bf16x8 al = bf16x8{lv[0], lv[1], lv[2], lv[3], lv[4], lv[5], lv[6], lv[7]};
-            if (refill) ld_row(s, i, kx + SCD);
-#pragma unroll
+  #pragma unroll
+        for (int i = 0; i < MI; ++i) ld_row(s, i, min(s, nx - 1));
+      });
+      for (int kx0 = 0; kx0 < nx; kx0 += SCD) {
+        Unroll<0, SCD>::run([&](auto S) {
+          constexpr int s = decltype(S)::value;
+          const int kx = kx0 + s;
+          if (kx < nx) {
+            if (kx == piece1) {   // next piece of W1 images (every wave reaches this with the same kx)
+              __syncthreads();    // all reads of the previous piece are done
+              piece0 = piece1;
+              piece1 = min(nx, piece1 + kScrPiece);
+              copy_w1(piece0, piece1);
+            }
+            const char* wl = smem + (kx - piece0) * 2 * W1_BYTES;
+            bf16x8 bh[NI], bl[NI];
+  #pragma unroll
             for (int j = 0; j < NI; ++j) {
-              acc[i][j] = mfma32(al, bh[j], acc[i][j]);
-              acc[i][j] = mfma32(ah, bl[j], acc[i][j]);
-              acc[i][j] = mfma32(ah, bh[j], acc[i][j]);
+              const int p = j * 32 + l32;
+              const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+              bh[j] = *reinterpret_cast<const bf16x8*>(wl + off);
+              bl[j] = *reinterpret_cast<const bf16x8*>(wl + W1_BYTES + off);
+            }
+            const bool refill = kx + SCD < nx;
+            // row by row: split row i, refill its registers with chunk kx + SCD, then its MFMAs -- so only one
+            // row's hi / lo fragments are live beside the in-flight loads
+  #pragma unroll
+            for (int i = 0; i < MI; ++i) {
+              const bool ok = t0 + wm * MI + i < a.T_in;
+              __bf16 hv[8], lv[8];
+  #pragma unroll
+              for (int q = 0; q < 8; ++q) split_bf16(ok ? xa[s][i][q >> 2][q & 3] : 0.f, hv[q], lv[q]);
+              const bf16x8 ah = bf16x8{hv[0], hv[1], hv[2], hv[3], hv[4], hv[5], hv[6], hv[7]};
+              const bf16x8 al = bf16x8{lv[0], lv[1], lv[2], lv[3], lv[4], lv[5], lv[6], lv[7]};
+              if (refill) ld_row(s, i, kx + SCD);
+  #pragma unroll
+              for (int j = 0; j < NI; ++j) {
+                acc[i][j] = mfma32(al, bh[j], acc[i][j]);
+                acc[i][j] = mfma32(ah, bl[j], acc[i][j]);
+                acc[i][j] = mfma32(ah, bh[j], acc[i][j]);
+              }
             }
           }
-        }
-      });
-    }
-    __syncthreads();   // the epilogue's statistics reduction reuses the LDS
-  } else if (XTRA && a.x_chunks > 0) {
-    const int nx = a.x_chunks;
-    load_ext(0);
-    store_ext(smem);
-    load_ext(min(1, nx - 1));
-    __syncthreads();
-    for (int kx = 0; kx < nx; ++kx) {
-      char* cur = smem + (kx & 1) * STAGE;
-      char* nxt = smem + ((kx + 1) & 1) * STAGE;
-      Frags fr;
-      read_frags(fr, cur, 1, 1, 0, W1_BYTES, kExt);
-      mfmas(fr, kExt);
-      store_ext(nxt);
-      load_ext(min(kx + 2, nx - 1));
+        });
+      }
+      __syncthreads();   // the epilogue's statistics reduction reuses the LDS
+    } else if (XTRA && a.x_chunks > 0) {
+      const int nx = a.x_chunks;
+      load_ext(0);
+      store_ext(smem);
+      load_ext(min(1, nx - 1));
       __syncthreads();
+      for (int kx = 0; kx < nx; ++kx) {
+        char* cur = smem + (kx & 1) * STAGE;
+        char* nxt = smem + ((kx + 1) & 1) * STAGE;
+        Frags fr;
+        read_frags(fr, cur, 1, 1, 0, W1_BYTES, kExt);
+        mfmas(fr, kExt);
+        store_ext(nxt);
+        load_ext(min(kx + 2, nx - 1));
+        __syncthreads();
+      }
     }
+  };
+  // ORD: with a fused shortcut, every other group of 8 workgroups runs the shortcut phase (HBM-bound: the
+  // raw block input, 4 B per channel) BEFORE the main phase (MFMA-bound).  At one workgroup per CU the grid's
+  // workgroups otherwise move through the two phases in lockstep -- the whole chip MFMA-bound, then the whole
+  // chip HBM-bound; split orders keep half the CUs in each.  (Only the fp32 summation order of the two
+  // phases' contributions differs between the orders.)
+  if (ORD && XTRA && ((blockIdx.x >> 3) & 1)) {
+    shortcut_phase();
+    main_phase();
+  } else {
+    main_phase();
+    shortcut_phase();
   }
 
   if constexpr (EPI == 2) {

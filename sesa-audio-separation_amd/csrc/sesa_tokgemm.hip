@@ -1023,6 +1023,196 @@ __global__ void __launch_bounds__(kThreads, 2) attn_kernel(AttnArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// attn_f16_kernel: the same flash attention (S^T = K Q^T, P^T from registers, V^T by transposing LDS
+// reads, gates in the epilogue) with QK^T and PV on ONE v_mfma_f32_32x32x16_f16 pass each: q / sqrt(dh),
+// k, v and the block's P = exp(s - m) rounded once to fp16, softmax statistics (m, l) and the O accumulator
+// in fp32 (CPU emulation on the BS-Roformer vocals chunk: 3.0e-7 RMS, tests/emulation/emulate_bsr_attn16.py).
+// The fp16 K / V images are half the bf16 hi + lo pair, so K / V are DOUBLE-BUFFERED in the same 32 KiB:
+// block kb + 1 is converted and stored into the other stage under block kb's MFMAs, block kb + 2 loads
+// into registers, one barrier per block (the bf16x3 kernel: single stage, two barriers).
+// Output: fp32 rows, or (out_f16) one fp16 plane -- the A operand of the fp16 out-projection.
+__device__ __forceinline__ f32x16 mfma32h_(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+__device__ __forceinline__ uint32_t pack2h_(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
+}
+
+__global__ void __launch_bounds__(kThreads, 2) attn_f16_kernel(AttnArgs a) {
+  constexpr int IMG = kKB * kHD * 2;                      // one fp16 [64 key][64 d] image
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];   // [stage][K, V]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hl = lane >> 5;
+  const int head = blockIdx.y;
+  const int seq = blockIdx.z;
+  const int64_t sbase = (int64_t)(seq / a.sdiv) * a.smul_a + (int64_t)(seq % a.sdiv) * a.smul_b;
+  auto token = [&](int p) -> int64_t { return sbase + (int64_t)p * a.pstride; };
+  const float* kvb = a.kv ? a.kv : a.qkv;
+  const int64_t kv_ld = a.kv ? a.kv_ld : a.ld;
+  const int Lk = a.Lk > 0 ? a.Lk : a.L;
+  auto ktoken = [&](int p) -> int64_t { return a.kv ? (int64_t)seq * a.kv_smul + p : token(p); };
+  const int dh = a.dh > 0 ? a.dh : kHD;
+  const float qscale = dh == kHD ? 0.125f : 1.0f / sqrtf((float)dh);
+  const int q_pos = blockIdx.x * 128 + wave * 32 + l32;
+  const bool q_ok = q_pos < a.L;
+
+  bf16x8 qf[4];   // fp16 bits: Q[q][16 ks + 8 hl + j] / sqrt(dh)
+  {
+    const float* qp = a.qkv + token(q_ok ? q_pos : 0) * a.ld + head * dh;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int d0 = 16 * ks + 8 * hl;
+      const f32x4 v0 = q_ok && d0 < dh ? *reinterpret_cast<const f32x4*>(qp + d0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 v1 = q_ok && d0 + 4 < dh ? *reinterpret_cast<const f32x4*>(qp + d0 + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const u32x4 w = {pack2h_(v0[0] * qscale, v0[1] * qscale), pack2h_(v0[2] * qscale, v0[3] * qscale),
+                       pack2h_(v1[0] * qscale, v1[1] * qscale), pack2h_(v1[2] * qscale, v1[3] * qscale)};
+      qf[ks] = __builtin_bit_cast(bf16x8, w);
+    }
+  }
+  f32x16 o[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  f32x4 kreg[4], vreg[4];
+  auto load_block = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + i * kThreads;
+      const int key = e >> 4, dq = (e & 15) * 4;
+      const int p = kb * kKB + key;
+      const bool ok = p < Lk && dq < dh;
+      const float* row = kvb + ktoken(ok ? p : 0) * kv_ld + head * dh + (ok ? dq : 0);
+      kreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.k_off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      vreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.v_off) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_block = [&](char* stg) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + i * kThreads;
+      const int key = e >> 4, dq = (e & 15) * 4;
+      const int off = swz(key, dq >> 3) + ((dq & 4) << 1);
+      *reinterpret_cast<uint2*>(stg + off) =
+          make_uint2(pack2h_(kreg[i][0], kreg[i][1]), pack2h_(kreg[i][2], kreg[i][3]));
+      *reinterpret_cast<uint2*>(stg + IMG + off) =
+          make_uint2(pack2h_(vreg[i][0], vreg[i][1]), pack2h_(vreg[i][2], vreg[i][3]));
+    }
+  };
+  const int tg = lane >> 4, ti = lane & 15;
+  const int tr_q = ti >> 2, tp = ti & 3, th = tg >> 1;
+  auto vt_frag = [&](const char* V, int ks, int db) -> bf16x8 {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const int d = db * 32 + 16 * (tg & 1) + 4 * tp;
+    const int key0 = 32 * (ks >> 1) + 16 * (ks & 1) + 4 * th + tr_q;
+    // a transposing 16-bit read is a pure data movement: the fp16 bits travel in a bf16 container
+    const bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) bf16x4*)(V + swz(key0, d >> 3) + ((d & 7) << 1)));
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) bf16x4*)(V + swz(key0 + 8, d >> 3) + ((d & 7) << 1)));
+    return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  const int n_blocks = (Lk + kKB - 1) / kKB;
+  load_block(0);
+  store_block(smem);
+  if (n_blocks > 1) load_block(1);
+  __syncthreads();
+  for (int kb = 0; kb < n_blocks; ++kb) {
+    const char* K = smem + (kb & 1) * 2 * IMG;
+    const char* V = K + IMG;
+    f32x16 s[2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[rb][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(K + swz(rb * 32 + l32, 2 * ks + hl));
+        s[rb] = mfma32h_(kf, qf[ks], s[rb]);
+      }
+    }
+    // stage block kb + 1 (in registers since the previous iteration) into the other buffer -- every wave
+    // finished reading it before the previous iteration's barrier -- then start loading block kb + 2
+    if (kb + 1 < n_blocks) {
+      store_block(smem + ((kb + 1) & 1) * 2 * IMG);
+      if (kb + 2 < n_blocks) load_block(kb + 2);
+    }
+    float bmax = -INFINITY;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb * kKB + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        if (key >= Lk) s[rb][r] = -INFINITY;
+        bmax = fmaxf(bmax, s[rb][r]);
+      }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+    const float m_new = fmaxf(m_run, bmax);
+    const float alpha = __expf(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __expf(s[rb][r] - m_new);
+        s[rb][r] = p;
+        psum += p;
+      }
+    psum += __shfl_xor(psum, 32);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int r0 = 8 * (ks & 1);
+      const f32x16& sv = s[ks >> 1];
+      const u32x4 w = {pack2h_(sv[r0], sv[r0 + 1]), pack2h_(sv[r0 + 2], sv[r0 + 3]), pack2h_(sv[r0 + 4], sv[r0 + 5]),
+                       pack2h_(sv[r0 + 6], sv[r0 + 7])};
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, w);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) o[db] = mfma32h_(vt_frag(V, ks, db), pf, o[db]);
+    }
+    __syncthreads();
+  }
+
+  if (!q_ok) return;
+  const int64_t tq = token(q_pos);
+  const float gate = a.g_off >= 0 ? sigmoidf_(a.qkv[tq * a.ld + a.g_off + head]) : 1.f;
+  const float scale = gate / l_run;
+  const int64_t obase = tq * a.o_ld + head * dh;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = db * 32 + 8 * g4 + 4 * hl;
+      if (d >= dh) continue;
+      f32x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = o[db][4 * g4 + q] * scale;
+      if (a.out_hi && a.out_f16) {
+        *reinterpret_cast<uint2*>(a.out_hi + obase + d) = make_uint2(pack2h_(v[0], v[1]), pack2h_(v[2], v[3]));
+      } else if (a.out_hi) {
+        __bf16 hi[4], lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) split_bf16(v[q], hi[q], lo[q]);
+        *reinterpret_cast<uint2*>(a.out_hi + obase + d) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
+        if (a.out_lo)
+          *reinterpret_cast<uint2*>(a.out_lo + obase + d) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
+      } else {
+        *reinterpret_cast<f32x4*>(a.out + obase + d) = v;
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // fp32 rows -> bf16 hi / lo planes (+ RMSNorm row scale): one wave per row, f32x4 per lane-step.
 // F16: one fp16 plane (round to nearest even) -- the A operand of the fp16 single-pass Linears.  With a
 // row_scale output the fp16 plane holds x * row_scale (the RMS-normalised row, |value| <= sqrt(K)), not the raw
@@ -1203,7 +1393,12 @@ int launch_attention(const AttnArgs& a, int x3, hipStream_t st) {
   SESA_REQUIRE(!pre || ((!a.kv || a.kv_hi) && (a.dh == 0 || a.dh % 8 == 0) && a.ld % 8 == 0 && a.k_off % 4 == 0 &&
                         a.v_off % 4 == 0 && (!x3 || (a.qkv_lo && (!a.kv || a.kv_lo)))),
                SESA_ERR_INVALID, "attention: pre-split planes need dh %% 8, 8-B aligned offsets and the lo planes");
-  if (pre) {
+  // x3 == 2: QK^T and PV on one fp16 pass (fp32 QKV rows; SESA_PREC_F16 of BS- / Mel-Band-Roformer)
+  SESA_REQUIRE(x3 != 2 || !pre, SESA_ERR_INVALID, "attention: the fp16 kernel reads fp32 q / k / v rows");
+  SESA_REQUIRE(!a.out_f16 || (a.out_hi && x3 == 2), SESA_ERR_INVALID, "attention: fp16 output plane from the fp16 kernel");
+  if (x3 == 2) {
+    hipLaunchKernelGGL(attn_f16_kernel, grid, dim3(kThreads), 0, st, a);
+  } else if (pre) {
     if (x3) hipLaunchKernelGGL((attn_kernel<true, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((attn_kernel<false, true>), grid, dim3(kThreads), 0, st, a);
   } else if (x3) {

@@ -116,6 +116,7 @@ struct AttnArgs {
   const uint16_t* qkv_lo;
   const uint16_t* kv_hi;
   const uint16_t* kv_lo;
+  int out_f16;                // with out_hi: one fp16 plane (the fp16 kernel, x3 == 2; the fp16 out-projection's A)
 };
 
 

@@ -92,7 +92,8 @@ def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, 
     ``streams`` > 1: consecutive forwards alternate between the current stream and side streams (each
     with its own input buffer and model workspace) so that one forward's memory-bound phases can overlap
     another's MFMA-bound ones; the OLA of every forward stays on the current stream, in chunk order,
-    after an event on its forward's stream (the result is bit-identical to streams = 1)."""
+    after an event on its forward's stream (the result equals streams = 1 up to the order of the norm
+    statistics' fp64 atomic adds, which concurrent forwards interleave)."""
     from . import ops
     C = plan["chunk"]
     n_ch = mix_d.shape[0]

@@ -34,8 +34,12 @@ def test_conv3x3_alg_bytes_by_precision():
     b3, n3 = bench.mdx23c_conv3x3_alg_bytes(c, 57, "bf16x3")
     bw, nw = bench.mdx23c_conv3x3_alg_bytes(c, 57, "fp16w2")
     b1, n1 = bench.mdx23c_conv3x3_alg_bytes(c, 57, "fp16")
-    assert n3 == nw == n1 == 2 * 9                       # 9 TFC_TDF stacks x (conv1, conv2)
-    assert b1 < bw < b3                                   # fp16 plane (2 B) inputs, then 2 B weights
+    assert n3 == 2 * 9                                    # 9 TFC_TDF stacks x (conv1, conv2)
+    assert nw == n1 == 2 * 8                              # fp16 modes: the class is the T >= 32 fp16 convs only
+    assert b1 / n1 < bw / nw                              # 2 B weights instead of 4
+    # fp16mix: the plan's '3' levels leave the class (they are conv3x3_x3)
+    bm, nm = bench.mdx23c_conv3x3_alg_bytes(c, 57, "fp16mix", "1311111111111111")
+    assert nm == 2 * 7 and bm < b1                       # encoder level 1 (one block here) leaves
     # level 0 (fused fp32 input) is precision-independent apart from the weights
     b3_l0 = 57 * 256 * 1024 * (128 * 4 + 128 * 4) + 9 * 128 * 128 * 4
     assert b3 > 2 * b3_l0
@@ -44,7 +48,8 @@ def test_conv3x3_alg_bytes_by_precision():
 def test_fp16_modes_are_mdx23c_only():
     from sesa.models.mdx23c import TFC_TDF_net
     from sesa.models.native import NativeModule
-    assert "fp16" in TFC_TDF_net._precisions and TFC_TDF_net._amp_precision == "fp16"
+    assert "fp16" in TFC_TDF_net._precisions and "fp16mix" in TFC_TDF_net._precisions
+    assert TFC_TDF_net._amp_precision == "fp16mix"
     assert "fp16" not in NativeModule._precisions and NativeModule._amp_precision == "bf16"
 
 
