@@ -17,7 +17,7 @@ def _vocals_cfg():
 
 
 def test_default_precision():
-    assert bench.default_precision("mdx23c") == bench.default_precision("ensemble") == "fp16"
+    assert bench.default_precision("mdx23c") == bench.default_precision("ensemble") == "fp16mix"
     assert bench.default_precision("bs_roformer") == "fp16"
     for m in ("htdemucs", "scnet"):
         assert bench.default_precision(m) == "bf16x3"
@@ -25,6 +25,9 @@ def test_default_precision():
     assert bench.class_precision("conv3x3", "fp16") == "fp16"
     assert bench.class_precision("tokgemm", "fp16") == "bf16x3"
     assert bench.class_precision("tokgemm", "fp16", "bs_roformer") == "fp16"
+    assert bench.class_precision("attn", "fp16mix", "ensemble") == "fp16"
+    assert bench.class_precision("attn", "fp16", "htdemucs") == "bf16x3"
+    assert bench.class_precision("conv3x3", "fp16mix") == "fp16mix"
     assert bench.class_precision("hconv", "fp16", "ensemble") == "bf16x3"
     assert bench.class_precision("tokgemm", "bf16") == "bf16"
 
