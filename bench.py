@@ -121,7 +121,9 @@ _TOK_SRC = ("sesa_tokgemm.hip", "sesa_tokgemm.hpp", "sesa_common.hpp")
 KSRC = {"conv3x3": _MDX_SRC, "tdf": _MDX_SRC, "act": _MDX_SRC, "conv1x1": _MDX_SRC, "down": _MDX_SRC,
         "up": _MDX_SRC, "tokgemm": _TOK_SRC + ("sesa_bsroformer.hip",), "attn": _TOK_SRC + ("sesa_bsroformer.hip",),
         "hconv": _TOK_SRC + ("sesa_htdemucs.hip",), "lstm": ("sesa_scnet.hip", "sesa_tokgemm.hpp", "sesa_common.hpp"),
-        "simt": ("sesa_scnet.hip", "sesa_common.hpp"), "conv3x3_x3": _MDX_SRC}
+        "simt": ("sesa_scnet.hip", "sesa_common.hpp"), "conv3x3_x3": _MDX_SRC,
+        "stft": ("sesa_spectral.hip", "sesa_common.hpp"), "istft": ("sesa_spectral.hip", "sesa_common.hpp"),
+        "ola": ("sesa_ola.hip", "sesa_common.hpp")}
 
 
 def kernel_sources_sha16(kclass):
@@ -185,6 +187,21 @@ def conv_plan_modes(precision, plan=None):
     if precision == "fp16mix":
         return plan
     return {"fp16": "1", "fp16w2": "2", "bf16x3": "3", "bf16": "b"}[precision] * 16
+
+
+def stream_counter_bytes(kclass, model, precision):
+    """(HBM counter bytes per step, provenance) of a streaming class from profiles/pmc_<class>.json when it was
+    measured on this tree's sources for the same workload (model, precision); (None, reason) otherwise."""
+    pmc = os.path.join(REPO, "profiles", f"pmc_{kclass}.json")
+    if not os.path.exists(pmc):
+        return None, f"no profiles/pmc_{kclass}.json"
+    with open(pmc) as f:
+        d = json.load(f)
+    if d.get("src_sha16") != kernel_sources_sha16(kclass):
+        return None, f"profiles/pmc_{kclass}.json measured on other sources ({d.get('src_sha16')}): not reported"
+    if (d.get("model"), d.get("precision")) != (model, precision):
+        return None, f"profiles/pmc_{kclass}.json measured on {d.get('model')} / {d.get('precision')}: not reported"
+    return d.get("hbm_bytes_per_step"), {"file": f"profiles/pmc_{kclass}.json", "git_sha": d.get("git_sha")}
 
 
 def mdx23c_conv3x3_alg_bytes(cfg, batch, precision="bf16x3", plan=None):
@@ -620,6 +637,14 @@ def main():
                 gbs = kbytes / (kms * 1e-3) / 1e9
                 hbm[kc] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / 8000.0, 4), "launches": kn,
                            "avg_launch_ms": round(kms / kn, 4), "bytes_per_launch": round(kbytes / kn)}
+                # rocprofv3 counter bytes of one step of this workload (profiles/pmc_<class>.json, tools/pmc_stream.py)
+                cb, src = stream_counter_bytes(kc, args.model, args.precision)
+                hbm[kc]["counter_source"] = src
+                if cb:
+                    cgbs = cb * args.steps / (kms * 1e-3) / 1e9
+                    hbm[kc].update(counter_bytes_per_step=cb, counter_gbs=round(cgbs, 1),
+                                   counter_frac=round(cgbs / 8000.0, 4),
+                                   counter_over_algorithmic=round(cb * args.steps / kbytes, 3))
         line["hbm_kernels"] = {"peak_gbs": 8000.0, **hbm}
         classes = {}
         for kc in ("conv3x3", "conv3x3_x3", "conv1x1", "down", "up", "tdf", "act", "tokgemm", "attn", "lstm", "simt",

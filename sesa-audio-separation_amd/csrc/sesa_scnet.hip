@@ -18,6 +18,7 @@
 //   scn_sdconv_kernel       SD layer band conv (kernel k x 1, stride s x 1) into the band's F range
 //   scn_cm_in_kernel        ConvolutionModule head, one workgroup per (b, f) row: GroupNorm(1, C)
 //                           stats, normalise-on-load, conv1d k3 (weights in LDS), GLU
+//   scn_cm_in_rb_kernel     the same, register-blocked (4 positions x 2 hidden units per thread): the default
 //   scn_cm_out_kernel       ConvolutionModule tail per row: depthwise k3, GroupNorm(1, h), Swish,
 //                           1x1 conv, residual (+ the SD block's GELU after the last layer)
 //   tok_gemm (conv mode)    3x3 conv over (F, T) as an implicit GEMM, K = 9 taps x C (MFMA, bf16x3):
@@ -292,6 +293,93 @@ __global__ void __launch_bounds__(kST) scn_cm_in_kernel(CmArgs a) {
         }
       }
       U[(int64_t)t * h + j] = ga * sigm(gg);
+    }
+  }
+}
+
+// scn_cm_in_rb_kernel: the same ConvolutionModule head (GroupNorm(1, C) stats, normalise-on-load, conv1d
+// k3 C -> 2h, GLU), register-blocked: each thread owns CM_TB consecutive positions x CM_JB hidden units (both
+// GLU halves: 2 CM_TB CM_JB accumulators), so per input channel c it reads CM_TB + 2 normalised inputs and 6
+// CM_JB weights from LDS for 6 CM_TB CM_JB FMAs (2.7 FMAs per LDS read at 4 x 2, against 0.67 in
+// scn_cm_in_kernel's one-output-per-thread loop, which is LDS-issue-bound).  Same fp32 arithmetic per
+// output (the k3 taps and channels accumulate in the same order), so the outputs are identical to
+// scn_cm_in_kernel's.  Tile: 256 threads x CM_TB x CM_JB / h positions.
+constexpr int CM_TB = 4, CM_JB = 2;
+__host__ __device__ constexpr int cm_rb_tt(int h) { return kST * CM_TB * CM_JB / h; }
+
+__global__ void __launch_bounds__(kST) scn_cm_in_rb_kernel(CmArgs a) {
+  extern __shared__ __align__(16) float sm[];
+  const int C = a.C, h = a.h, T = a.T;
+  const int TT = cm_rb_tt(h);
+  float* Ws = sm;                                    // [C][3][2h]
+  float* xs = Ws + 6 * h * C;                        // [TT + 2][C]
+  double* red = reinterpret_cast<double*>(xs + (TT + 2) * C);
+  const int row = blockIdx.x;
+  const int64_t b = row / a.n_f;
+  const int f = a.f_off + row % a.n_f;
+  const float* xr = a.X + ((b * a.F_all + f) * T) * C;
+  double s = 0, ss = 0;
+  for (int i = threadIdx.x; i < T * C; i += kST) {
+    const double v = xr[i];
+    s += v;
+    ss += v * v;
+  }
+  block_sum2(s, ss, red);
+  const double n = (double)T * C;
+  const double mu = s / n;
+  const double var = fmax(ss / n - mu * mu, 0.0);
+  const float mean = (float)mu, rstd = (float)(1.0 / sqrt(var + 1e-5));
+  for (int i = threadIdx.x; i < 6 * h * C; i += kST) Ws[i] = a.W1[i];
+  float* U = a.U + (int64_t)row * T * h;
+  const int nj = h / CM_JB;
+  const int jb = threadIdx.x % nj, tb = threadIdx.x / nj;   // lanes of one position block share its x reads
+  const int j0 = jb * CM_JB;
+  for (int t0 = 0; t0 < T; t0 += TT) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < (TT + 2) * C; i += kST) {
+      const int tl = i / C, c = i - tl * C;
+      const int t = t0 - 1 + tl;
+      xs[i] = (t >= 0 && t < T) ? (xr[(int64_t)t * C + c] - mean) * rstd * a.g1[c] + a.be1[c] : 0.f;
+    }
+    __syncthreads();
+    float ga[CM_TB][CM_JB], gg[CM_TB][CM_JB];
+#pragma unroll
+    for (int r = 0; r < CM_TB; ++r)
+#pragma unroll
+      for (int q = 0; q < CM_JB; ++q) {
+        ga[r][q] = a.b1[j0 + q];
+        gg[r][q] = a.b1[j0 + q + h];
+      }
+    const int tl0 = tb * CM_TB;
+    // tap-major over the same (dt, c) order as scn_cm_in_kernel
+#pragma unroll
+    for (int dt = 0; dt < 3; ++dt) {
+      for (int c = 0; c < C; ++c) {
+        float xv[CM_TB];
+#pragma unroll
+        for (int r = 0; r < CM_TB; ++r) xv[r] = xs[(tl0 + r + dt) * C + c];
+        const float* w = Ws + c * 6 * h + dt * 2 * h + j0;
+        float wa[CM_JB], wg[CM_JB];
+#pragma unroll
+        for (int q = 0; q < CM_JB; ++q) {
+          wa[q] = w[q];
+          wg[q] = w[q + h];
+        }
+#pragma unroll
+        for (int r = 0; r < CM_TB; ++r)
+#pragma unroll
+          for (int q = 0; q < CM_JB; ++q) {
+            ga[r][q] = fmaf(wa[q], xv[r], ga[r][q]);
+            gg[r][q] = fmaf(wg[q], xv[r], gg[r][q]);
+          }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < CM_TB; ++r) {
+      const int t = t0 + tl0 + r;
+      if (t >= T) continue;
+#pragma unroll
+      for (int q = 0; q < CM_JB; ++q) U[(int64_t)t * h + j0 + q] = ga[r][q] * sigm(gg[r][q]);
     }
   }
 }
@@ -1240,6 +1328,12 @@ Plan plan(const sesa_scnet* m, int B) {
 }
 
 size_t cm_in_lds(int C, int h) { return (size_t)(6 * h * C + (512 / h + 2) * C) * 4 + 16 * 8 + 16; }
+size_t cm_in_rb_lds(int C, int h) { return (size_t)(6 * h * C + (cm_rb_tt(h) + 2) * C) * 4 + 16 * 8 + 16; }
+// SESA_SCN_CM_RB=0: the one-output-per-thread ConvolutionModule head (A/B of scn_cm_in_rb_kernel)
+bool scn_cm_rb_on(int C, int h) {
+  static const bool off = getenv("SESA_SCN_CM_RB") && std::string(getenv("SESA_SCN_CM_RB")) == "0";
+  return !off && h % CM_JB == 0 && (kST * CM_TB * CM_JB) % h == 0 && cm_in_rb_lds(C, h) <= 160 * 1024;
+}
 size_t cm_out_lds(int T, int C, int h) { return (size_t)(2 * T * h + h * C + 1) * 4 + 16 * 8 + 16; }
 
 double gemm_flops(const Gemm& gm, int64_t M) {
@@ -1647,6 +1741,8 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
                                      160 * 1024));
   SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_out_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024));
+  SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_in_rb_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
   SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_in_gen_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024));
   SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_out_gen_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1778,7 +1874,10 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
           hipLaunchKernelGGL(scn_cm_out_gen_kernel, dim3(rows), dim3(kST), cm_out_gen_lds(L.Cout, L.h), st, a);
           SESA_CHECK_LAUNCH();
         } else {
-          hipLaunchKernelGGL(scn_cm_in_kernel, dim3(rows), dim3(kST), cm_in_lds(L.Cout, L.h), st, a);
+          if (scn_cm_rb_on(L.Cout, L.h))
+            hipLaunchKernelGGL(scn_cm_in_rb_kernel, dim3(rows), dim3(kST), cm_in_rb_lds(L.Cout, L.h), st, a);
+          else
+            hipLaunchKernelGGL(scn_cm_in_kernel, dim3(rows), dim3(kST), cm_in_lds(L.Cout, L.h), st, a);
           SESA_CHECK_LAUNCH();
           hipLaunchKernelGGL(scn_cm_out_kernel, dim3(rows), dim3(kST), cm_out_lds(T, L.Cout, L.h), st, a);
           SESA_CHECK_LAUNCH();

@@ -2746,6 +2746,13 @@ bool conv3x3_mi4_enabled() {
   return v;
 }
 
+// SESA_CONV_ORD=0: every workgroup of a conv with a fused shortcut runs the main phase first (A/B of the split
+// phase order, conv3x3_db_kernel<ORD>)
+bool conv3x3_ord_enabled() {
+  static const bool v = !(getenv("SESA_CONV_ORD") && std::string(getenv("SESA_CONV_ORD")) == "0");
+  return v;
+}
+
 bool tap_bn128_enabled() {
   static const bool v = !(getenv("SESA_TAP_BN128") && std::string(getenv("SESA_TAP_BN128")) == "0");
   return v;
@@ -2883,17 +2890,24 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
           SESA_REQUIRE(a.xin.C_in % kConvBK == 0 && a.xin.C_split % kConvBK == 0 && a.xin.src[0].mode == SRC_RAW &&
                            a.xin.src[1].mode == SRC_RAW,
                        SESA_ERR_INVALID, "conv3x3: fused shortcut must be a raw input, C_in multiple of %d", kConvBK);
-#define SESA_DB(X3V, XTRAV, F16V)                                                                            \
-  do {                                                                                                      \
-    if (act) hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, true, F16V>), grid, dim3(512), 0, st, a);  \
-    else hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, false, F16V>), grid, dim3(512), 0, st, a);     \
+        const bool ord = conv3x3_ord_enabled();
+#define SESA_DB(X3V, XTRAV, F16V)                                                                                     \
+  do {                                                                                                               \
+    if (act) hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, true, F16V>), grid, dim3(512), 0, st, a);           \
+    else if (XTRAV && ord)                                                                                           \
+      hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, false, F16V, false, false, 2, true>), grid, dim3(512), 0, \
+                         st, a);                                                                                     \
+    else hipLaunchKernelGGL((conv3x3_db_kernel<X3V, XTRAV, 0, false, F16V>), grid, dim3(512), 0, st, a);              \
   } while (0)
         // xmode 2 = fp16 x fp16 hi/lo weights (F16 = 2), 3 = fp16 single pass (F16 = 1; on pre-activated
         // planes the 32-row MI4 tile unless SESA_CONV_MI4=0)
         if (xmode == 3 && !act && conv3x3_mi4_enabled()) {
           const dim3 g32((unsigned)(((a.T_out + 31) / 32) * (a.F_out / kTF) * ((a.n_cols + 63) / 64)), 1u,
                          (unsigned)batch);
-          if (a.x_chunks > 0) hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true>), g32, dim3(512), 0, st, a);
+          if (a.x_chunks > 0 && ord)
+            hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, false, 2, true>), g32, dim3(512), 0, st, a);
+          else if (a.x_chunks > 0)
+            hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true>), g32, dim3(512), 0, st, a);
           else hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0, false, 1, true>), g32, dim3(512), 0, st, a);
         } else if (a.x_chunks > 0) {
           if (xmode == 3) SESA_DB(true, true, 1);

@@ -18,4 +18,13 @@ run() {
 run bsr_fp16 fp=1 fp16
 run bsr_bf16x3 fp=1 bf16x3
 run bsr_fp16b fp=1 fp16
+mrun() {
+  echo "[r04b] $(date +%T) mdx $1"
+  timeout -k 10 300 env $2 python bench.py --precision $3 --steps 10 --warmup 2 --no-cpu-baseline > $O/mdx_$1.json 2> $O/mdx_$1.err
+}
+mrun mix_ord1 SESA_CONV_ORD=1 fp16mix
+mrun mix_ord0 SESA_CONV_ORD=0 fp16mix
+mrun fp16_ord1 SESA_CONV_ORD=1 fp16
+mrun fp16_ord0 SESA_CONV_ORD=0 fp16
+mrun mix_ord1b SESA_CONV_ORD=1 fp16mix
 echo "[r04b] $(date +%T) done"
