@@ -151,6 +151,10 @@ int sesa_mdx23c_set_wino(int mode);
  * previous plan is copied to prev (17 bytes) when prev is not NULL.  Default "1311111111111111"
  * (env SESA_F16_PLAN overrides it at first use). */
 int sesa_mdx23c_set_f16_plan(const char* plan, char* prev);
+/* SESA_PREC_F16MIX plan of the TDF Linears (same layout; '1' = one fp16 pass, '3' = bf16x3; only Linears of
+ * the LDS-DMA kernel's shapes run fp16).  Default "3333311111111111": the decoder stacks in fp16 (env
+ * SESA_TDF_PLAN overrides it at first use). */
+int sesa_mdx23c_set_tdf_plan(const char* plan, char* prev);
 
 /* ---------------------------------------------------------------------------------------
  * BS-Roformer (models/bs_roformer/bs_roformer.py:327-587, BSRoformer)

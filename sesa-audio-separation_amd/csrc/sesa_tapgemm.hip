@@ -2234,6 +2234,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) tdf_kernel(TdfArgs a) {
 // ([column tile][chunk][hi: 128 n x 32 k][lo], the image swizzle included).  Without it the second
 // Linear converts every U element once per 256-row block of its output (4x at level 0), and its
 // staging is VALU-issue-bound.  One workgroup per (column tile, chunk); thread = column x 8 k.
+template <bool F16 = false>
 __global__ void __launch_bounds__(512) tdf_u_split_kernel(TdfArgs a) {
   constexpr int BN = 128, ROWB = kTdfBK * 2;
   const int64_t ntile = blockIdx.x;
@@ -2273,6 +2274,10 @@ __global__ void __launch_bounds__(512) tdf_u_split_kernel(TdfArgs a) {
   uint32_t hw[4], lw[4];
 #pragma unroll
   for (int e = 0; e < 8; e += 2) {
+    if constexpr (F16) {   // one fp16 image (the lo image is not read by the fp16 GEMM)
+      hw[e / 2] = pack2h(v[e], v[e + 1]);
+      continue;
+    }
     __bf16 h0, l0, h1, l1;
     split_bf16(v[e], h0, l0);
     split_bf16(v[e + 1], h1, l1);
@@ -2282,7 +2287,7 @@ __global__ void __launch_bounds__(512) tdf_u_split_kernel(TdfArgs a) {
   char* dst = reinterpret_cast<char*>(a.u_planes) + blk * (kTdfBK * BN * 4);
   const int off = n * ROWB + ((kq ^ ((n >> 2) & 3)) << 4);
   *reinterpret_cast<uint4*>(dst + off) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-  *reinterpret_cast<uint4*>(dst + BN * ROWB + off) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  if constexpr (!F16) *reinterpret_cast<uint4*>(dst + BN * ROWB + off) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2301,9 +2306,11 @@ __global__ void __launch_bounds__(512) tdf_u_split_kernel(TdfArgs a) {
 //     (channels), so U rows (U_OUT) and NHWC rows (+ the residual, prefetched into registers under the
 //     last chunk) are written as full 128-B lines; per-column statistics (fp32 over 16-value runs, fp64
 //     beyond) reduced through LDS.
-template <bool X3, bool U_IN, bool U_OUT, int BM, bool PRE = false>
+// F16 (X3 = false): W and B images in fp16, one v_mfma_f32_32x32x16_f16 pass (SESA_PREC_F16MIX TDF plan).
+template <bool X3, bool U_IN, bool U_OUT, int BM, bool PRE = false, bool F16 = false>
 __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   static_assert(!PRE || U_IN, "pre-split B images exist for the tiled U input only");
+  static_assert(!F16 || !X3, "fp16: one pass");
   constexpr int BN = 128;
   constexpr int WM = BM / 64, WN = 8 / WM;
   constexpr int MI = 2, NI = BN / WN / 32;
@@ -2421,6 +2428,10 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
     uint32_t hw[4], lw[4];
 #pragma unroll
     for (int e = 0; e < 8; e += 2) {
+      if constexpr (F16) {
+        hw[e / 2] = pack2h(v[e], v[e + 1]);
+        continue;
+      }
       __bf16 h0, l0, h1, l1;
       split_bf16(v[e], h0, l0);
       split_bf16(v[e + 1], h1, l1);
@@ -2507,7 +2518,8 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
             acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
             acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
           }
-          acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+          if constexpr (F16) acc[i][j] = mfma32h(ah[i], bh[j], acc[i][j]);
+          else acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
         }
     }
     // W(kc + 1) and X(kc + 2) landed (only X(kc + 3), issued last, may stay in flight; the residual
@@ -2746,10 +2758,12 @@ bool conv3x3_mi4_enabled() {
   return v;
 }
 
-// SESA_CONV_ORD=0: every workgroup of a conv with a fused shortcut runs the main phase first (A/B of the split
-// phase order, conv3x3_db_kernel<ORD>)
+// SESA_CONV_ORD=1: every other group of 8 workgroups of a conv with a fused shortcut runs the shortcut phase
+// first (conv3x3_db_kernel<ORD>).  Off: measured slower -- conv_bench 57 f16 L0 7.37 -> 8.11 ms, the headline
+// 249.0x -> 246.9x same box (profiles/r04_ord_*): the shortcut phase is bound by the bytes one CU keeps in
+// flight, not by the chip's HBM bandwidth, so desynchronising the phases buys nothing.
 bool conv3x3_ord_enabled() {
-  static const bool v = !(getenv("SESA_CONV_ORD") && std::string(getenv("SESA_CONV_ORD")) == "0");
+  static const bool v = getenv("SESA_CONV_ORD") && std::string(getenv("SESA_CONV_ORD")) == "1";
   return v;
 }
 
@@ -3023,6 +3037,13 @@ int tdf_variant() {  // SESA_TDF_VARIANT=old: the round-1 register-staged tdf_ke
 }
 }  // namespace
 
+// the LDS-DMA TDF kernel takes this Linear (and so may run it in fp16, x3 == 2; the host packs those
+// weights as fp16 images): C % 128 == 0, K % 32 == 0, 128 or 256 row blocks, one normalised / raw source
+bool tdf_dma_eligible(int C, int K, int M) {
+  const int bm = tdf_block_rows(M);
+  return tdf_variant() == 0 && C % 128 == 0 && K % kTdfBK == 0 && (bm == 256 || bm == 128);
+}
+
 int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io) {
   TdfArgs b = a;
   b.batch = batch;
@@ -3031,16 +3052,19 @@ int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transpos
     const int C = a.in.src[0].C;
     const int bm = tdf_block_rows(a.M);
     const int mode = a.in.src[0].mode;
-    if (tdf_variant() == 0 && C % 128 == 0 && a.K % kTdfBK == 0 && (bm == 256 || bm == 128) &&
-        (mode == SRC_NORM_GELU || mode == SRC_RAW) && a.in.C_split == a.in.C_in && a.in.C_in == C) {
+    const bool dma_ok = tdf_dma_eligible(C, a.K, a.M) && (mode == SRC_NORM_GELU || mode == SRC_RAW) &&
+                        a.in.C_split == a.in.C_in && a.in.C_in == C;
+    SESA_REQUIRE(x3 != 2 || dma_ok, SESA_ERR_INVALID, "tdf: the fp16 mode needs the LDS-DMA kernel's shapes");
+    if (dma_ok) {
       const int64_t n_tiles = (int64_t)batch * a.T * C / 128;
       const int64_t grid = (n_tiles + 7) / 8 * 8 * ((a.M + bm - 1) / bm);
       SESA_REQUIRE(grid < (1ll << 31), SESA_ERR_INVALID, "tdf: grid too large");
       const dim3 g((unsigned)grid), blk(512);
-#define SESA_TDF_DMA(UI, UO, BMV)                                                              \
-  do {                                                                                         \
-    if (x3) hipLaunchKernelGGL((tdf_dma_kernel<true, UI, UO, BMV>), g, blk, 0, st, b);         \
-    else hipLaunchKernelGGL((tdf_dma_kernel<false, UI, UO, BMV>), g, blk, 0, st, b);           \
+#define SESA_TDF_DMA(UI, UO, BMV)                                                                     \
+  do {                                                                                                \
+    if (x3 == 2) hipLaunchKernelGGL((tdf_dma_kernel<false, UI, UO, BMV, false, true>), g, blk, 0, st, b); \
+    else if (x3) hipLaunchKernelGGL((tdf_dma_kernel<true, UI, UO, BMV>), g, blk, 0, st, b);            \
+    else hipLaunchKernelGGL((tdf_dma_kernel<false, UI, UO, BMV>), g, blk, 0, st, b);                  \
   } while (0)
       if (transposed_io == 0) {
         if (bm == 256) SESA_TDF_DMA(false, true, 256);
@@ -3048,12 +3072,16 @@ int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transpos
       } else if (b.u_planes && (a.M + bm - 1) / bm >= 3) {
         // act(U) once per element, then the GEMM copies B images (measured: a win where the in-kernel
         // conversion would run >= 3x per element -- level 0 -- neutral at 2x, a loss at 1x)
-        hipLaunchKernelGGL(tdf_u_split_kernel, dim3((unsigned)n_tiles, (unsigned)a.n_chunks), dim3(512), 0, st, b);
+        if (x3 == 2)
+          hipLaunchKernelGGL(tdf_u_split_kernel<true>, dim3((unsigned)n_tiles, (unsigned)a.n_chunks), dim3(512), 0, st, b);
+        else
+          hipLaunchKernelGGL(tdf_u_split_kernel<false>, dim3((unsigned)n_tiles, (unsigned)a.n_chunks), dim3(512), 0, st, b);
         SESA_CHECK_LAUNCH();
-#define SESA_TDF_PRE(BMV)                                                                       \
-  do {                                                                                          \
-    if (x3) hipLaunchKernelGGL((tdf_dma_kernel<true, true, false, BMV, true>), g, blk, 0, st, b);  \
-    else hipLaunchKernelGGL((tdf_dma_kernel<false, true, false, BMV, true>), g, blk, 0, st, b);    \
+#define SESA_TDF_PRE(BMV)                                                                               \
+  do {                                                                                                  \
+    if (x3 == 2) hipLaunchKernelGGL((tdf_dma_kernel<false, true, false, BMV, true, true>), g, blk, 0, st, b); \
+    else if (x3) hipLaunchKernelGGL((tdf_dma_kernel<true, true, false, BMV, true>), g, blk, 0, st, b);        \
+    else hipLaunchKernelGGL((tdf_dma_kernel<false, true, false, BMV, true>), g, blk, 0, st, b);              \
   } while (0)
         if (bm == 256) SESA_TDF_PRE(256);
         else SESA_TDF_PRE(128);

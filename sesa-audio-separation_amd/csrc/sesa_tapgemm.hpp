@@ -95,6 +95,7 @@ int set_conv3x3_variant(int v);
 bool tap_bn128_enabled();  // SESA_TAP_BN128=0 disables the 128-column down / up tiles (A/B)  // 0 = conv3x3_db_kernel, 1 = conv3x3_m16_kernel; returns the previous
 int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transposed_io);
 int tdf_block_rows(int M);
+bool tdf_dma_eligible(int C, int K, int M);
 // floats of the tiled U^T buffer [n/128][ceil(M/32)][128][32] for n_cols = B*T*C columns
 int64_t tdf_u_floats(int64_t n_cols, int M);  // BM chosen for a TDF Linear with M output rows (weights packed to match)
 

@@ -74,6 +74,7 @@ SIGNATURES = {
     "sesa_mdx23c_set_conv_variant": (c_int, [c_int]),
     "sesa_mdx23c_set_wino": (c_int, [c_int]),
     "sesa_mdx23c_set_f16_plan": (c_int, [c_char_p, c_char_p]),
+    "sesa_mdx23c_set_tdf_plan": (c_int, [c_char_p, c_char_p]),
     "sesa_bsr_create": (c_int, [ctypes.POINTER(SesaBsrConfig), ctypes.POINTER(c_void_p)]),
     "sesa_bsr_num_params": (c_int, [c_void_p]),
     "sesa_bsr_param_info": (c_int, [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64)]),

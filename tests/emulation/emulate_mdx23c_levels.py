@@ -38,9 +38,21 @@ def w_f16x2(w):
     return hi + (w - hi).half().float()
 
 
-def make(per_conv):
+def make(per_conv, tdf=None):
+    """tdf: None, or a set of TDF stack indices (call order: encoder L0..L4, bottleneck, decoder L4..L0 = 0..10)
+    whose two Linears run with fp16 activations and weights."""
     ns = types.SimpleNamespace(**{k: getattr(F, k) for k in dir(F) if not k.startswith("_")})
     idx = [0]
+    lin = [0]
+
+    def linear(inp, w, *a, **k):
+        stack = lin[0] // 4          # 2 blocks x 2 Linears per TFC_TDF stack
+        lin[0] += 1
+        if tdf and stack in tdf:
+            return F.linear(f16(inp), f16(w), *a, **k)
+        return F.linear(inp, w, *a, **k)
+
+    ns.linear = linear
 
     def conv2d(inp, w, *a, **k):
         if w.shape[-1] == 3 and inp.shape[2] >= 32:
@@ -68,9 +80,9 @@ def load(fixture):
     return _cache[fixture]
 
 
-def run(fixture, per_conv):
+def run(fixture, per_conv, tdf=None):
     params, x, ref = load(fixture)
-    om.F, idx = make(per_conv)
+    om.F, idx = make(per_conv, tdf)
     try:
         with torch.inference_mode():
             y = om.forward(params, CFG, x).numpy().astype(np.float64)
@@ -104,6 +116,16 @@ def main():
                 pc = NAMED.get(m, plan_to_convs(m[5:]) if m.startswith("plan:") else m)
                 r, rel, mx, rr = run(fx, pc)
                 print(f"{fx:28s} {m:12s} rms {r:.3e} rel {rel:.3e} max {mx:.3e} (ref rms {rr:.3e})", flush=True)
+    elif what == "tdfscan":   # fp16 TDF Linears of one stack at a time, on top of a conv plan
+        fx = sys.argv[2]
+        pc = plan_to_convs(sys.argv[3]) if len(sys.argv) > 3 else "3" * 32
+        base = run(fx, pc)[0]
+        print(f"conv plan alone: rms {base:.3e}", flush=True)
+        for st in range(11):
+            r = run(fx, pc, {st})[0]
+            print(f"tdf stack {st:2d} fp16: rms {r:.3e} (added {max(r * r - base * base, 0) ** 0.5:.3e})", flush=True)
+        r = run(fx, pc, set(range(6, 11)))[0]
+        print(f"decoder TDF stacks (6-10) fp16: rms {r:.3e}", flush=True)
     elif what == "scan":
         fx = sys.argv[2]
         lo, hi = (int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "0:32").split(":"))
