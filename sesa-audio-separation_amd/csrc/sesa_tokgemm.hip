@@ -1039,7 +1039,11 @@ __device__ __forceinline__ uint32_t pack2h_(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
 }
 
-__global__ void __launch_bounds__(kThreads, 2) attn_f16_kernel(AttnArgs a) {
+// NW: waves per workgroup (32 queries each): 4 (128 queries) for long sequences, 2 (64 queries) where L <= 64
+// (BS-Roformer's band attention, L = 62: a 128-query tile would compute half of its MFMAs on padding).
+template <int NW>
+__global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
+  constexpr int NTH = NW * 64, QB = NW * 32, NIT = kKB * 16 / NTH;   // staging items per thread
   constexpr int IMG = kKB * kHD * 2;                      // one fp16 [64 key][64 d] image
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG];   // [stage][K, V]
   const int tid = threadIdx.x;
@@ -1055,7 +1059,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_f16_kernel(AttnArgs a) {
   auto ktoken = [&](int p) -> int64_t { return a.kv ? (int64_t)seq * a.kv_smul + p : token(p); };
   const int dh = a.dh > 0 ? a.dh : kHD;
   const float qscale = dh == kHD ? 0.125f : 1.0f / sqrtf((float)dh);
-  const int q_pos = blockIdx.x * 128 + wave * 32 + l32;
+  const int q_pos = blockIdx.x * QB + wave * 32 + l32;
   const bool q_ok = q_pos < a.L;
 
   bf16x8 qf[4];   // fp16 bits: Q[q][16 ks + 8 hl + j] / sqrt(dh)
@@ -1078,11 +1082,11 @@ __global__ void __launch_bounds__(kThreads, 2) attn_f16_kernel(AttnArgs a) {
     for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  f32x4 kreg[4], vreg[4];
+  f32x4 kreg[NIT], vreg[NIT];
   auto load_block = [&](int kb) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + i * kThreads;
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + i * NTH;
       const int key = e >> 4, dq = (e & 15) * 4;
       const int p = kb * kKB + key;
       const bool ok = p < Lk && dq < dh;
@@ -1093,8 +1097,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_f16_kernel(AttnArgs a) {
   };
   auto store_block = [&](char* stg) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + i * kThreads;
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + i * NTH;
       const int key = e >> 4, dq = (e & 15) * 4;
       const int off = swz(key, dq >> 3) + ((dq & 4) << 1);
       *reinterpret_cast<uint2*>(stg + off) =
@@ -1397,7 +1401,10 @@ int launch_attention(const AttnArgs& a, int x3, hipStream_t st) {
   SESA_REQUIRE(x3 != 2 || !pre, SESA_ERR_INVALID, "attention: the fp16 kernel reads fp32 q / k / v rows");
   SESA_REQUIRE(!a.out_f16 || (a.out_hi && x3 == 2), SESA_ERR_INVALID, "attention: fp16 output plane from the fp16 kernel");
   if (x3 == 2) {
-    hipLaunchKernelGGL(attn_f16_kernel, grid, dim3(kThreads), 0, st, a);
+    if (a.L <= 64)
+      hipLaunchKernelGGL(attn_f16_kernel<2>, dim3((unsigned)((a.L + 63) / 64), (unsigned)a.heads, (unsigned)a.n_seq),
+                         dim3(128), 0, st, a);
+    else hipLaunchKernelGGL(attn_f16_kernel<4>, grid, dim3(kThreads), 0, st, a);
   } else if (pre) {
     if (x3) hipLaunchKernelGGL((attn_kernel<true, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((attn_kernel<false, true>), grid, dim3(kThreads), 0, st, a);
