@@ -454,7 +454,8 @@ def main():
                     help="htdemucs chunker: generic (the live CLI path, default) or utils.demix demucs mode")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the parity forward (PMC passes: one workload only)")
-    ap.add_argument("--streams", type=int, default=1, help="forwards in flight on separate HIP streams")
+    ap.add_argument("--streams", type=int, default=1, help="forwards in flight on separate HIP streams (> 1 is refused: "
+                    "not bit-consistent, sesa/parallel.py)")
     ap.add_argument("--cpu-chunks-only", action="store_true",
                     help="mdx23c: time --cpu-sample-chunks forwards instead of the configs[0] 10 s end-to-end run")
     args = ap.parse_args()

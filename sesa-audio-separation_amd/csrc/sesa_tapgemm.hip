@@ -479,12 +479,13 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 // holds only the images the mode reads (one A, one W: 55 KB); the shortcut stages keep their bf16 hi / lo
 // layout (78 KB), so a stage is the larger of the two.
 constexpr int kActMaxC = 1024;
-template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0, bool MI4 = false, bool SCR = false,
+template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0, bool MI4 = false, int SCR = 0,
           int SCD = 2, bool ORD = false>
 __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   static_assert(F16 == 0 || X3, "the fp16 modes keep the shortcut chunks bf16x3");
   static_assert(!MI4 || (F16 == 1 && !ACT), "MI4: fp16 single pass on pre-activated planes");
-  static_assert(!SCR || (XTRA && X3), "SCR: the bf16x3 fused shortcut from registers");
+  static_assert(!SCR || (XTRA && X3), "SCR: the bf16x3 fused shortcut from registers / per-wave LDS-DMA");
+  static_assert(SCR != 2 || MI4, "SCR 2: the 32-row tile (one wave = 4 rows of 32 positions)");
   constexpr bool ALO = X3 && F16 == 0;  // main chunks read an A lo image
   constexpr bool WLO = X3 && F16 != 1;  // main chunks read a W lo image
   constexpr int NT = 512;
@@ -501,7 +502,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   constexpr int STAGE_X = XTRA ? WOFF_X + 2 * W1_BYTES : 0;
   constexpr int STAGE = MI4 ? (STAGE_M > STAGE_X ? STAGE_M : STAGE_X) : 2 * A_BYTES + 2 * W_BYTES;
   // (one LDS array: the ACT affine table sits past the two stages)
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (ACT ? 2 * kActMaxC * 4 : 0)];
+  // SCR 2: the shortcut phase's per-wave rings take the whole 160 KiB (8 waves x kScrWave)
+  constexpr int kScrWave = 2 * 8192 + 4096;
+  constexpr int SMEM_B = 2 * STAGE + (ACT ? 2 * kActMaxC * 4 : 0);
+  __shared__ __attribute__((aligned(16))) char smem[SCR == 2 && 8 * kScrWave > SMEM_B ? 8 * kScrWave : SMEM_B];
   float* act_sc = reinterpret_cast<float*>(smem + 2 * STAGE);
   float* act_sh = act_sc + kActMaxC;
 
@@ -857,7 +861,97 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   };
   // ---- fused 1x1 shortcut chunks (centre tap) ----
   auto shortcut_phase = [&]() __attribute__((always_inline)) {
-    if constexpr (XTRA && SCR) {
+    if constexpr (XTRA && SCR == 2) {
+      // Per-wave LDS-DMA ring: each wave streams only its own 4 rows x 32 positions x 16 channels of the raw
+      // fp32 block input (8 KiB = eight 1-KiB buffer_load ... lds pieces per chunk) into a private 2-slot ring
+      // and the chunk's W1 image (hi + lo, 4 KiB = four pieces) into a private slot: 20 KiB per wave, the whole
+      // 160 KiB LDS.  No barrier and no VGPR staging: a CU keeps two chunks of the input (128 KiB) in flight
+      // where the LDS-staged form keeps one (64 KiB) behind one barrier per chunk.  Every transfer is a DMA, so
+      // the compiler tracks no register loads here and the counted waits below are the only ones.
+      // x image per slot: position p = 32 row + f holds 16 channels in 64 B, its 16-B quads permuted by
+      // (f >> 2) & 3 (conflict-free ds_read_b128 groups).
+      const int nx = a.x_chunks;
+      const char* w1 = reinterpret_cast<const char*>(wblk + (int64_t)n_main * W_BYTES);
+      char* ring = smem + wm * kScrWave;
+      char* wimg = ring + 2 * 8192;
+      const __amdgpu_buffer_rsrc_t rw =
+          __builtin_amdgcn_make_buffer_rsrc((void*)const_cast<char*>(w1), (short)0, nx * 2 * W1_BYTES, 0x00020000);
+      auto issue_x = [&](int kx, int slot) {
+        const int k0 = kx * kConvBK;
+        const int sx = k0 < a.xin.C_split ? 0 : 1;
+        const Src xs = pick_src(a.xin, sx);
+        const int cl0 = k0 - (sx ? a.xin.C_split : 0);
+        const int fl = lane >> 2, qs = lane & 3;   // this lane's LDS slot: position fl of the piece, quad qs
+        // buffer resource over this batch item's image (32-bit offsets)
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)const_cast<float*>(xs.ptr + (int64_t)b * a.T_in * a.F_in * xs.C), (short)0,
+            (int)((int64_t)a.T_in * a.F_in * xs.C * 4), 0x00020000);
+#pragma unroll
+        for (int pc = 0; pc < 8; ++pc) {
+          const int i = pc >> 1, f = (pc & 1) * 16 + fl;
+          const int t = min(t0 + wm * MI + i, a.T_in - 1);
+          const int q = qs ^ ((f >> 2) & 3);        // the channel quad stored in slot qs
+          const uint32_t voff = (uint32_t)((((int64_t)t * a.F_in + f0 + f) * xs.C + cl0 + 4 * q) * 4);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rx, (__attribute__((address_space(3))) void*)(ring + slot * 8192 + pc * 1024), 16, voff, 0, 0, 0);
+        }
+      };
+      auto issue_w = [&](int kx) {
+#pragma unroll
+        for (int pc = 0; pc < 4; ++pc)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(wimg + pc * 1024), 16,
+                                                   (uint32_t)(kx * 2 * W1_BYTES + pc * 1024 + lane * 16), 0, 0, 0);
+      };
+      // the main phase's last barrier retired every wave's reads of the stages this ring overwrites.
+      // Straight-line loop unrolled by the two slots; every step issues its refills (clamped to the last chunk
+      // at the tail: harmless repeats), so the count of transfers behind a chunk's is the same on every path:
+      // issue order x(k) W1(k) x(k+1) | W1(k+1) x(k+2) | ..., and chunk k is complete once only x(k+1)'s 8
+      // pieces remain.  nx is even (host check).
+      issue_x(0, 0);
+      issue_w(0);
+      issue_x(min(1, nx - 1), 1);
+      for (int kx0 = 0; kx0 < nx; kx0 += 2) {
+        Unroll<0, 2>::run([&](auto S) {
+          constexpr int slot = decltype(S)::value;
+          const int kx = kx0 + slot;
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");    // x(kx) and W1(kx) landed
+          bf16x8 bh[NI], bl[NI];
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int p = j * 32 + l32;
+            const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+            bh[j] = *reinterpret_cast<const bf16x8*>(wimg + off);
+            bl[j] = *reinterpret_cast<const bf16x8*>(wimg + W1_BYTES + off);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // W1(kx) in registers: its slot is free
+          issue_w(min(kx + 1, nx - 1));
+          const char* img = ring + slot * 8192;
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const bool ok = t0 + wm * MI + i < a.T_in;
+            const int pb = (i * 32 + l32) * 64;
+            const int sw = (l32 >> 2) & 3;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(img + pb + (((2 * h) ^ sw) << 4));
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(img + pb + (((2 * h + 1) ^ sw) << 4));
+            __bf16 hv[8], lv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) split_bf16(ok ? (q < 4 ? x0[q] : x1[q - 4]) : 0.f, hv[q], lv[q]);
+            const bf16x8 ah = bf16x8{hv[0], hv[1], hv[2], hv[3], hv[4], hv[5], hv[6], hv[7]};
+            const bf16x8 al = bf16x8{lv[0], lv[1], lv[2], lv[3], lv[4], lv[5], lv[6], lv[7]};
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+              acc[i][j] = mfma32(al, bh[j], acc[i][j]);
+              acc[i][j] = mfma32(ah, bl[j], acc[i][j]);
+              acc[i][j] = mfma32(ah, bh[j], acc[i][j]);
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this slot's reads done before the refill
+          issue_x(min(kx + 2, nx - 1), slot);
+        });
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // the tail's repeat refills landed
+      __syncthreads();   // the epilogue's statistics reduction reuses the LDS
+    } else if constexpr (XTRA && SCR == 1) {
       // Register-direct form: every lane loads its own A fragments straight from the raw fp32 block input
       // (inner position (t0 + row, f0 + l32), channels 8h..8h+7 of the chunk: 32 contiguous bytes, the
       // MFMA's row / k layout) and its B fragments from the packed W1 image (same byte layout as the LDS copy),

@@ -95,6 +95,13 @@ def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, 
     after an event on its forward's stream (the result equals streams = 1 up to the order of the norm
     statistics' fp64 atomic adds, which concurrent forwards interleave)."""
     from . import ops
+    if int(streams) > 1:
+        # measured on MI355X (tools/streams_debug2.py, profiles/r04_streams_debug.txt): streams = 2 changed 415
+        # samples of the first group's span by up to 9e-4 while streams = 3 and every single-stream run agreed
+        # bit for bit, and a forward on a side stream alone is bit-identical -- an unresolved ordering hazard, so
+        # the overlapped form is refused rather than shipped
+        raise NotImplementedError("local_accumulate_device: streams > 1 is disabled (not bit-consistent with "
+                                  "streams = 1 on MI355X; see DESIGN.md §6)")
     C = plan["chunk"]
     n_ch = mix_d.shape[0]
     device = mix_d.device
