@@ -743,7 +743,8 @@ extern "C" int sesa_htdemucs_create(const sesa_htdemucs_config* cfg, sesa_htdemu
   SESA_REQUIRE(c.t_layers >= 0 && c.t_heads >= 1 && c.t_norm_in == 1 && c.t_norm_first == 1 && c.t_norm_out == 1 &&
                    c.t_layer_scale == 1,
                SESA_ERR_INVALID, "htdemucs: transformer must be norm_in / norm_first / norm_out / layer_scale");
-  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16, SESA_ERR_INVALID, "htdemucs: precision");
+  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16 || c.precision == SESA_PREC_F16MIX,
+               SESA_ERR_INVALID, "htdemucs: precision");
   SESA_REQUIRE(c.chunk_size > kPadSpec + kHop, SESA_ERR_INVALID, "htdemucs: chunk_size must exceed 2560 samples");
   sesa_htdemucs* m = new sesa_htdemucs();
   m->cfg = c;
@@ -1208,7 +1209,10 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   const float* Wb = m->d_f32;
   const int T = m->T, L = c.chunk_size, ach = m->ach, D = m->D;
   const int hid = (int)(m->D * c.t_hidden_scale);
-  const int x3 = c.precision == SESA_PREC_BF16X3 ? 1 : 0;
+  // SESA_PREC_F16MIX: the cross-transformer attention (QK^T, PV) on one fp16 MFMA pass with fp32 softmax
+  // statistics (attn_f16_kernel); every other contraction bf16x3
+  const bool att16 = c.precision == SESA_PREC_F16MIX;
+  const int x3 = c.precision == SESA_PREC_BF16X3 || att16 ? 1 : 0;
   const int St = c.stride, Kk = c.kernel_size, pad = Kk / 4;
   SESA_REQUIRE((int64_t)B * std::max<int64_t>((int64_t)m->fq[0].Fin * T, (int64_t)L) < (1ll << 31) / 4,
                SESA_ERR_INVALID, "htdemucs forward: batch too large");
@@ -1565,7 +1569,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       if (ps) {                // planes for the following out-projection's pre-split A
         a.out_hi = hi_of(o);
         a.out_lo = lo_of(o, (int64_t)B * Lq * D);
-        // q / k / v from the planes the projection GEMMs wrote (plin split_out)
+      }
+      if (ps && !att16) {      // q / k / v from the planes the projection GEMMs wrote (plin split_out)
         a.qkv_hi = hi_of(const_cast<float*>(q));
         a.qkv_lo = lo_of(const_cast<float*>(q), (int64_t)B * Lq * q_ld);
         if (kv) {
@@ -1574,7 +1579,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         }
       }
       void* t0 = profile_begin(st);
-      rc = launch_attention(a, x3, st);
+      rc = launch_attention(a, att16 ? 2 : x3, st);
       profile_end(t0, st, SESA_KCLASS_ATTN, 4.0 * (double)B * heads * (double)Lq * Lk * dh);
     };
     auto gn_out = [&](float* Xs, int64_t ntok, int64_t g, int64_t b, double* sts) {
@@ -1608,8 +1613,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       if (!Lx.cross) {  // MyTransformerEncoderLayer (norm_first): x += g1 SA(n1(x)); x += g2 FF(n2(x)); norm_out
         lnp(X, Hx, Mx, Lx.n1g, Lx.n1b);
         lnp(XT, Ht, Mt, Lt.n1g, Lt.n1b);
-        plin(Lx.qkv, Hx, D, Qx, 3 * D, Mx, TOK_ACT_NONE, nullptr, true);
-        plin(Lt.qkv, Ht, D, Qt, 3 * D, Mt, TOK_ACT_NONE, nullptr, true);
+        plin(Lx.qkv, Hx, D, Qx, 3 * D, Mx, TOK_ACT_NONE, nullptr, !att16);
+        plin(Lt.qkv, Ht, D, Qt, 3 * D, Mt, TOK_ACT_NONE, nullptr, !att16);
         attn(Qx, 3 * D, nullptr, 0, D, 2 * D, Ax, m->Nx, m->Nx);
         attn(Qt, 3 * D, nullptr, 0, D, 2 * D, At, m->Nt, m->Nt);
         plin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, false);
@@ -1623,10 +1628,10 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         lnp(X, Hx2, Mx, Lt.n2g, Lt.n2b);     // keys / values of xt's layer (from old x)
         float* KVt = Qx + (size_t)Mx * D;    // [Mx][2D]: xt-layer keys / values (from x)
         float* KVx = Qt + (size_t)Mt * D;    // [Mt][2D]: x-layer keys / values (from xt)
-        plin(Lx.q, Hx, D, Qx, D, Mx, TOK_ACT_NONE, nullptr, true);
-        plin(Lx.kv, Ht2, D, KVx, 2 * D, Mt, TOK_ACT_NONE, nullptr, true);
-        plin(Lt.q, Ht, D, Qt, D, Mt, TOK_ACT_NONE, nullptr, true);
-        plin(Lt.kv, Hx2, D, KVt, 2 * D, Mx, TOK_ACT_NONE, nullptr, true);
+        plin(Lx.q, Hx, D, Qx, D, Mx, TOK_ACT_NONE, nullptr, !att16);
+        plin(Lx.kv, Ht2, D, KVx, 2 * D, Mt, TOK_ACT_NONE, nullptr, !att16);
+        plin(Lt.q, Ht, D, Qt, D, Mt, TOK_ACT_NONE, nullptr, !att16);
+        plin(Lt.kv, Hx2, D, KVt, 2 * D, Mx, TOK_ACT_NONE, nullptr, !att16);
         attn(Qx, D, KVx, 2 * D, 0, D, Ax, m->Nx, m->Nt);
         attn(Qt, D, KVt, 2 * D, 0, D, At, m->Nt, m->Nx);
         plin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, false);

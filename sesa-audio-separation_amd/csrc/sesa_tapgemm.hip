@@ -2861,6 +2861,14 @@ bool conv3x3_ord_enabled() {
   return v;
 }
 
+// The fused 1x1 shortcut of the fp16 MI4 conv3x3 on the per-wave LDS-DMA ring (SCR = 2): measured
+// 4-17 % faster per level than the LDS-staged phase and bit-identical to it (profiles/
+// r04_conv_bench_f16_dmaring.txt).  SESA_CONV_SCR=0 restores the LDS-staged phase (A/B).
+bool conv3x3_scr_ring_enabled() {
+  static const bool v = !(getenv("SESA_CONV_SCR") && std::string(getenv("SESA_CONV_SCR")) == "0");
+  return v;
+}
+
 bool tap_bn128_enabled() {
   static const bool v = !(getenv("SESA_TAP_BN128") && std::string(getenv("SESA_TAP_BN128")) == "0");
   return v;
@@ -3012,7 +3020,12 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
         if (xmode == 3 && !act && conv3x3_mi4_enabled()) {
           const dim3 g32((unsigned)(((a.T_out + 31) / 32) * (a.F_out / kTF) * ((a.n_cols + 63) / 64)), 1u,
                          (unsigned)batch);
-          if (a.x_chunks > 0 && ord)
+          // the DMA ring walks chunk pairs and addresses each batch item's shortcut image with 32-bit offsets
+          const bool ring = a.x_chunks > 0 && !ord && conv3x3_scr_ring_enabled() && a.x_chunks % 2 == 0 &&
+                            (int64_t)a.T_in * a.F_in * std::max(a.xin.src[0].C, a.xin.src[1].C) * 4 < (1ll << 31);
+          if (ring)
+            hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, 2>), g32, dim3(512), 0, st, a);
+          else if (a.x_chunks > 0 && ord)
             hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, false, 2, true>), g32, dim3(512), 0, st, a);
           else if (a.x_chunks > 0)
             hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true>), g32, dim3(512), 0, st, a);

@@ -424,7 +424,10 @@ __device__ __forceinline__ uint32_t dpp_xor1u(uint32_t x) {
 // (bf16 planes out); bias always (per group).  EP_RAW / EP_NONE: ablations for tools/tokgemm_bench.hip.
 // M16: v_mfma_f32_16x16x32_bf16 blocks (8 x 4 per wave, one k-step per 32-deep chunk) instead of
 // 32x32x16 (4 x 2, two k-steps); same wave tile, accumulator count and LDS images.
-template <int EP, bool M16 = false>
+// DEPTH > 2 (EP_F16 only): compact fp16 stages (A hi plane + the two 128-column hi images, 32 KiB)
+// in a DEPTH-slot ring over the same LDS, DEPTH - 1 chunks in flight instead of one, one barrier per
+// chunk (counted vmcnt waits); the epilogue is unchanged.
+template <int EP, bool M16 = false, int DEPTH = 2>
 __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   constexpr int NT = 512, BM = 256, BK = kTokBK, WN = 4;
   constexpr int BLK = M16 ? 16 : 32;                       // MFMA block edge
@@ -459,6 +462,10 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int l32 = lane & 31, h = lane >> 5;
   const int n_chunks = (g.K + BK - 1) / BK;
+  constexpr bool CMP = (EP & EP_F16) != 0 && DEPTH > 2;   // compact fp16 ring
+  constexpr int SSZ = CMP ? A_BYTES + 2 * W_PLANE : STAGE;  // bytes per ring slot
+  static_assert(!CMP || DEPTH * SSZ <= 2 * STAGE, "ring fits the two bf16x3 stages");
+  static_assert(DEPTH == 2 || ((EP & EP_F16) != 0 && M16), "deep ring: the fp16 16x16x32 kernel only");
 
   for (int r = tid; r < BM; r += NT) {                      // ordinary loads, before any DMA is in flight
     const int m = min(m0 + r, a.M - 1);
@@ -500,8 +507,9 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
         const int q = wave + 8 * (i - APW);
         const int half = q / W_HALF, qq = q - half * W_HALF;
         const uint16_t* src = (half ? wblk1 : wblk0) + (int64_t)kc * wimg + qq * 512 + lane * 8;
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stg + A_REG + q * 1024), 16,
-                                         0, 0);
+        // compact ring: hi image half h at A_BYTES + h W_PLANE (qq < 8: the hi pieces)
+        char* dst = CMP ? stg + A_BYTES + half * W_PLANE + qq * 1024 : stg + A_REG + q * 1024;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
     }
   };
@@ -527,15 +535,16 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
       const int row = (wm * MI + i) * BLK + frow;
       const int off = row * ROWB + ((q ^ ((row >> 2) & 3)) << 4);
       f.ah[i] = *reinterpret_cast<const bf16x8*>(stg + off);
-      f.al[i] = *reinterpret_cast<const bf16x8*>(stg + A_BYTES + off);
+      if constexpr (!F16) f.al[i] = *reinterpret_cast<const bf16x8*>(stg + A_BYTES + off);
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int c = (wn * NI + j) * BLK + frow;             // 0..255
       const int r = c & (kTokBN - 1);
-      const int off = A_REG + (c >> 7) * W_IMG + r * ROWB + ((q ^ ((r >> 2) & 3)) << 4);
+      const int off = (CMP ? A_BYTES + (c >> 7) * W_PLANE : A_REG + (c >> 7) * W_IMG) + r * ROWB +
+                      ((q ^ ((r >> 2) & 3)) << 4);
       f.bh[j] = *reinterpret_cast<const bf16x8*>(stg + off);
-      f.bl[j] = *reinterpret_cast<const bf16x8*>(stg + off + W_PLANE);
+      if constexpr (!F16) f.bl[j] = *reinterpret_cast<const bf16x8*>(stg + off + W_PLANE);
     }
   };
   // EP_F16: fp16 A planes x fp16 weight images, one pass
@@ -563,13 +572,39 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   };
 
   __syncthreads();                                         // rs / rpos visible; no DMA in flight yet
+  // waves whose 64 columns all lie past the group's N (the partial last tile, e.g. BS-Roformer's
+  // 8 gate columns after q / k / v) skip their MFMAs (wave-uniform); they still issue their DMA pieces
+  const bool busy = n0 + wn * 64 < g.N;
+  if constexpr (CMP) {
+    // 4 DMA pieces per wave per chunk (2 A, 2 W): chunk kc has landed for this wave when at most
+    // 4 min(DEPTH - 2, n_chunks - 1 - kc) of its pieces are still outstanding
+#pragma unroll
+    for (int s = 0; s < DEPTH - 1; ++s)
+      if (s < n_chunks) issue(s, smem + s * SSZ);
+    for (int kc = 0; kc < n_chunks; ++kc) {
+      const int pend = min(DEPTH - 2, n_chunks - 1 - kc);
+      if (pend >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (pend == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // every wave's pieces of chunk kc landed, and every wave's reads of slot (kc - 1) % DEPTH retired
+      // (lgkmcnt(0) below) -- that slot takes chunk kc + DEPTH - 1
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kc + DEPTH - 1 < n_chunks) issue(kc + DEPTH - 1, smem + ((kc + DEPTH - 1) % DEPTH) * SSZ);
+      if (busy) {
+        Frags f0;
+        read_frags(f0, smem + (kc % DEPTH) * SSZ, 0);
+        mfmas(f0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();                          // the epilogue's LDS staging reuses the ring
+    asm volatile("" ::: "memory");
+  } else {
   issue(0, smem);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  // waves whose 64 columns all lie past the group's N (the partial last tile, e.g. BS-Roformer's
-  // 8 gate columns after q / k / v) skip their MFMAs (wave-uniform); they still issue their DMA pieces
-  const bool busy = n0 + wn * 64 < g.N;
   for (int kc = 0; kc < n_chunks; ++kc) {
     char* cur = smem + (kc & 1) * STAGE;
     // chunk kc + 1 into the other stage: its last fragment reads (iteration kc - 1) were retired
@@ -590,6 +625,7 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+  }
   }
 
   if constexpr ((EP & EP_NONE) != 0) {

@@ -33,6 +33,8 @@ class HTDemucs(NativeModule):
     """Reference-compatible HTDemucs backed by the native HIP forward."""
 
     _prefix = "htdemucs"
+    # fp16mix: the cross-transformer attention on one fp16 MFMA pass (fp32 softmax statistics), the rest bf16x3
+    _precisions = ("bf16x3", "bf16", "fp16mix")
 
     def __init__(self, sources, audio_channels=2, samplerate=44100, segment=10, precision="bf16x3", **kw):
         super().__init__(precision)
@@ -98,7 +100,8 @@ class HTDemucs(NativeModule):
             t_hidden_scale=float(k["t_hidden_scale"]), freq_emb=float(k["freq_emb"] or 0.0),
             emb_scale=float(k["emb_scale"]), t_max_period=float(k["t_max_period"]),
             t_weight_pos_embed=float(k["t_weight_pos_embed"]),
-            precision=N.SESA_PREC_BF16X3 if self.precision == "bf16x3" else N.SESA_PREC_BF16)
+            precision={"bf16x3": N.SESA_PREC_BF16X3, "bf16": N.SESA_PREC_BF16,
+                       "fp16mix": N.SESA_PREC_F16MIX}[self.precision])
 
     def _out_shape(self, B, ch, L):
         return (B, len(self.sources), ch, L)

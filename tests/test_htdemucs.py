@@ -103,12 +103,13 @@ def dev():
 
 
 @pytest.mark.gpu
-def test_forward_small_matches_reference(golden, dev):
+@pytest.mark.parametrize("precision", ["bf16x3", "fp16mix"])
+def test_forward_small_matches_reference(golden, dev, precision):
     g = golden("htdemucs_small.npz")
-    m, _ = _model("config_htdemucs_small.yaml")
+    m, _ = _model("config_htdemucs_small.yaml", precision=precision)
     y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
     err = rms(y, g["y"])
-    print(f"htdemucs small rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    print(f"htdemucs small {precision} rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
     assert y.shape == g["y"].shape and err <= RMS_GATE
 
 
@@ -133,12 +134,14 @@ def test_forward_batch_items_independent(golden, dev):
 
 
 @pytest.mark.gpu
-def test_forward_full_segment_matches_reference(golden, dev):
+@pytest.mark.parametrize("precision", ["bf16x3", "fp16mix"])
+def test_forward_full_segment_matches_reference(golden, dev, precision):
+    """fp16mix: the cross-transformer attention on one fp16 MFMA pass (QK^T, PV; fp32 softmax statistics)."""
     g = golden("htdemucs_full_segment.npz")
-    m, _ = _model("config_musdb18_htdemucs.yaml")
+    m, _ = _model("config_musdb18_htdemucs.yaml", precision=precision)
     y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
     err = rms(y, g["y"])
-    print(f"htdemucs musdb18 segment rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    print(f"htdemucs musdb18 segment {precision} rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
     assert y.shape == g["y"].shape and err <= RMS_GATE
 
 

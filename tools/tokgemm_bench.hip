@@ -58,8 +58,125 @@ float time_ms(F&& launch, int reps = 20) {
   return ts[ts.size() / 2];
 }
 
+// fp16 single-pass Linears (x3 == 2): the DEPTH-2 two-stage kernel vs the compact DEPTH-slot rings, with
+// and without the epilogue; outputs of every ring depth must equal DEPTH 2 bit for bit.
+template <int EP, int D>
+void launch_f16(const TokGemmArgs& a, dim3 g) {
+  hipLaunchKernelGGL((tok_gemm_glds_kernel<EP, true, D>), g, dim3(512), 0, 0, a);
+}
+template <int EP>
+void f16_shape(const char* name, int M, int N, int K, TokGemmArgs a, dim3 g, size_t n_out, bool planes) {
+  const double flop = 2.0 * M * (double)N * K;
+  auto rep = [&](const char* v, float ms) { printf("%-4s %-28s %9.3f %9.1f\n", name, v, ms, flop / ms * 1e-9); };
+  rep("f16 depth 2", time_ms([&] { launch_f16<EP, 2>(a, g); }));
+  rep("f16 depth 3", time_ms([&] { launch_f16<EP, 3>(a, g); }));
+  rep("f16 depth 4", time_ms([&] { launch_f16<EP, 4>(a, g); }));
+  rep("f16 depth 2 no epilogue", time_ms([&] { launch_f16<EP_F16 | EP_NONE, 2>(a, g); }));
+  rep("f16 depth 4 no epilogue", time_ms([&] { launch_f16<EP_F16 | EP_NONE, 4>(a, g); }));
+  if constexpr ((EP & EP_GELU) != 0)
+    rep("f16 depth 4 no GELU", time_ms([&] { launch_f16<EP & ~EP_GELU, 4>(a, g); }));
+  auto get = [&](auto launch) {
+    std::vector<uint16_t> r(planes ? n_out : 2 * n_out);
+    CK(hipMemset(planes ? (void*)a.out_hi : (void*)a.out, 0, planes ? n_out * 2 : n_out * 4));
+    launch();
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(r.data(), planes ? (void*)a.out_hi : (void*)a.out, r.size() * 2, hipMemcpyDeviceToHost));
+    return r;
+  };
+  const auto r2 = get([&] { launch_f16<EP, 2>(a, g); });
+  const auto r3 = get([&] { launch_f16<EP, 3>(a, g); });
+  const auto r4 = get([&] { launch_f16<EP, 4>(a, g); });
+  printf("     depth 3 %s depth 2, depth 4 %s depth 2\n", r3 == r2 ? "IDENTICAL to" : "DIFFERS from",
+         r4 == r2 ? "IDENTICAL to" : "DIFFERS from");
+}
+
+void run_f16(int M) {
+  std::mt19937 rng(1);
+  std::normal_distribution<float> nd(0.f, 1.f);
+  const int Kmax = 2048, Nmax = 2048;
+  std::vector<uint16_t> ha((size_t)M * Kmax);
+  for (auto& v : ha) v = __builtin_bit_cast(uint16_t, (_Float16)nd(rng));
+  uint16_t *a16, *ohi;
+  float *out, *res;
+  float2* rope;
+  CK(hipMalloc(&a16, ha.size() * 2));
+  CK(hipMemcpy(a16, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+  CK(hipMalloc(&out, (size_t)M * Nmax * 4));
+  CK(hipMalloc(&res, (size_t)M * Nmax * 4));
+  CK(hipMemset(res, 0, (size_t)M * Nmax * 4));
+  CK(hipMalloc(&ohi, (size_t)M * Nmax * 2));
+  {
+    std::vector<float2> t(801 * 32);
+    for (size_t i = 0; i < t.size(); ++i) t[i] = make_float2(cosf(0.01f * i), sinf(0.01f * i));
+    CK(hipMalloc(&rope, t.size() * 8));
+    CK(hipMemcpy(rope, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+  }
+  printf("fp16 single pass, M=%d\n", M);
+  const Shape shapes[] = {{"qkv", 1544, 512, 1, 1, TOK_ACT_NONE, 0, 0},
+                          {"out", 512, 512, 0, 0, TOK_ACT_NONE, 1, 0},
+                          {"ff1", 2048, 512, 0, 1, TOK_ACT_GELU, 0, 1},
+                          {"ff2", 512, 2048, 0, 0, TOK_ACT_NONE, 1, 0}};
+  for (const Shape& sh : shapes) {
+    std::vector<uint16_t> blob;
+    std::vector<float> bias;
+    Gemm gm;
+    gm.groups.push_back(pack_group(
+        sh.N, sh.K, [&](int n, int k) { return 0.02f * (float)(((n * 131 + k * 71) % 97) - 48) / 48.f; }, true,
+        [&](int n) { return 0.01f * (n % 7); }, blob, bias, true));
+    uint16_t* w;
+    float* b;
+    CK(hipMalloc(&w, blob.size() * 2));
+    CK(hipMemcpy(w, blob.data(), blob.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMalloc(&b, bias.size() * 4));
+    CK(hipMemcpy(b, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
+    upload_groups(gm);
+    TokGemmArgs a{};
+    a.w = w;
+    a.bias = b;
+    a.groups = gm.d_groups;
+    a.n_groups = 1;
+    a.n_tiles_n = gm.n_tiles_n;
+    a.k8 = gm.k8;
+    a.n4 = gm.n4;
+    a.M = M;
+    a.out = out;
+    a.o_ld = sh.N;
+    a.a_hi = a16;
+    a.a_ld = sh.K;
+    a.act = sh.act;
+    a.dim_head = 64;
+    if (sh.rope) {
+      a.rope = rope;
+      a.rope_cols = 1024;
+      a.pos_F = 62;
+      a.pos_T = 801;
+      a.pos_time = 1;
+    }
+    if (sh.resid) a.residual = res;
+    if (sh.split_out) {
+      a.out_hi = ohi;
+    }
+    const dim3 g((unsigned)(((M + 255) / 256) * ((gm.n_tiles_n + 1) / 2)));
+    const size_t n_out = (size_t)M * sh.N;
+    if (sh.rope) f16_shape<EP_F16 | EP_ROPE>(sh.name, M, sh.N, sh.K, a, g, n_out, false);
+    else if (sh.split_out) f16_shape<EP_F16 | EP_GELU | EP_SPLIT>(sh.name, M, sh.N, sh.K, a, g, n_out, true);
+    else f16_shape<EP_F16 | EP_RES>(sh.name, M, sh.N, sh.K, a, g, n_out, false);
+    CK(hipFree(w));
+    CK(hipFree(b));
+  }
+  CK(hipFree(a16));
+  CK(hipFree(out));
+  CK(hipFree(res));
+  CK(hipFree(ohi));
+  CK(hipFree(rope));
+}
+
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 198648;  // 4 chunks x 801 frames x 62 bands
+  if (argc > 2 && !strcmp(argv[2], "f16")) {
+    run_f16(M);
+    return 0;
+  }
   const bool small = argc > 2 && !strcmp(argv[2], "small");   // the parity tests' reduced BS-Roformer
   const Shape big_shapes[] = {{"qkv", 1544, 512, 1, 1, TOK_ACT_NONE, 0, 0},
                               {"out", 512, 512, 0, 0, TOK_ACT_NONE, 1, 0},
