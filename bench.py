@@ -105,6 +105,9 @@ def kdesc(kclass, precision, model):
     if kclass == "attn" and cp == "fp16":
         return ("attn_f16_kernel (flash attention, S^T = K Q^T, one v_mfma_f32_32x32x16_f16 pass for QK^T and PV, "
                 "fp32 softmax statistics, double-buffered K / V)")
+    if kclass == "hconv" and cp == "fp16":
+        return ("tok_gemm_kernel<conv, F16> (HTDemucs implicit-GEMM convolutions and 1x1 rewrites, operand rounded "
+                "once to fp16 in the staging, one v_mfma_f32_32x32x16_f16 pass) + htd_dc_conv_valu (fp32 VALU)")
     if kclass == "tokgemm" and cp == "fp16":
         return ("tok_gemm_glds_kernel<EP_F16> (QKV / out-projection / FF Linears, one v_mfma_f32_16x16x32_f16 pass) + "
                 "bf16x3 token GEMMs (band split, mask MLPs: v_mfma_f32_32x32x16_bf16 / 16x16x32_bf16)")
@@ -152,11 +155,14 @@ MDX_CLASSES = ("conv3x3", "conv3x3_x3", "conv1x1", "down", "up", "tdf", "act")
 def class_precision(kclass, precision, model="mdx23c"):
     """The precision a kernel class's launches run in for a bench line of `model` in `precision` (the PMC
     stamp bench.py compares): the MDX23C classes follow the MDX23C mode; the token GEMMs and the attention
-    follow BS-Roformer's fp16 mode (bs_roformer, ensemble); every other class is bf16x3 in the fp16 modes."""
+    follow BS-Roformer's fp16 mode (bs_roformer, ensemble); HTDemucs fp16mix runs its attention and convs fp16;
+    every other class is bf16x3 in the fp16 modes."""
     if not precision.startswith("fp16") or kclass in MDX_CLASSES:
         return precision
     if kclass in ("tokgemm", "attn") and model in ("bs_roformer", "ensemble"):
         return "fp16"
+    if kclass in ("hconv", "attn") and model == "htdemucs" and precision == "fp16mix":
+        return "fp16"         # HTDemucs fp16mix: attention and implicit-GEMM convs fp16, Linears bf16x3
     return "bf16x3"
 
 

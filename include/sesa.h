@@ -21,8 +21,8 @@
  *   SESA_PREC_F16MIX -- MDX23C: those convs per level as the plan of sesa_mdx23c_set_f16_plan says
  *                       (default: one fp16 pass everywhere except the encoder level-1 convs, bf16x3 --
  *                       they carry ~70 % of the fp16 rounding error at the stems);
- *                       HTDemucs: the cross-transformer attention (QK^T, PV) on one fp16 pass with
- *                       fp32 softmax statistics, every other contraction bf16x3
+ *                       HTDemucs: the cross-transformer attention (QK^T, PV; fp32 softmax statistics),
+ *                       the implicit-GEMM convs and 1x1 rewrites on one fp16 pass, the Linears bf16x3
  */
 #ifndef SESA_H_
 #define SESA_H_
@@ -46,7 +46,7 @@ extern "C" {
 #define SESA_PREC_F16 3   /* MDX23C: TFC 3x3 convs (T >= 32) single fp16 pass; BS- / Mel-Band-Roformer: the
                              QKV / FF Linears single fp16 pass; the rest bf16x3                           */
 #define SESA_PREC_F16MIX 4 /* MDX23C: per-level plan of the T >= 32 TFC 3x3 convs (sesa_mdx23c_set_f16_plan);
-                              HTDemucs: fp16 attention */
+                              HTDemucs: fp16 attention + convs */
 
 int sesa_version(void);
 const char* sesa_last_error(void);

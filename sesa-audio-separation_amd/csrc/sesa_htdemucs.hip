@@ -927,6 +927,9 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
   std::vector<uint16_t> blob;
   std::vector<float> bias;
   auto single = [&](Gemm& gm, const TokGroup& g) { gm.groups = {g}; };
+  // fp16mix: the conv-family weights (encoder / transposed / DConv / rewrite convs) as fp16 images for the
+  // fp16 single-pass implicit GEMMs; the transformer Linears stay bf16 hi / lo
+  const bool f16w = c.precision == SESA_PREC_F16MIX;
   std::vector<double> f64;
   auto pack_dconv = [&](std::vector<DcLayer>& out, const std::string& p, int C, int h) {
     for (auto& L : out)
@@ -944,7 +947,7 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                            const int tap = k / C, ci = k - tap * C;
                            return W1[((size_t)n * C + ci) * 3 + tap];
                          },
-                         true, [&](int n) { return B1[n]; }, blob, bias));
+                         true, [&](int n) { return B1[n]; }, blob, bias, f16w));
       L.b1 = putp(q + ".0.bias");
       if (const int Hv = dc_valu_h(h)) {
         std::vector<float> wv((size_t)3 * C * Hv, 0.f), bv((size_t)Hv, 0.f);
@@ -1006,7 +1009,7 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                      const int tap = k / C, ci = k - tap * C;
                      return W[((size_t)src * C + ci) * taps + tap];
                    },
-                   true, [&](int n) { return Bv[(n & 1) ? (n >> 1) + C : (n >> 1)]; }, blob, bias));
+                   true, [&](int n) { return Bv[(n & 1) ? (n >> 1) + C : (n >> 1)]; }, blob, bias, f16w));
   };
   for (int i = 0; i < c.depth; ++i) {
     for (int br = 0; br < 2; ++br) {
@@ -1023,7 +1026,7 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                              const int tap = k / Cp, ci = k - tap * Cp;
                              return ci < Cin ? W[((size_t)n * Cin + ci) * K + tap] : 0.f;
                            },
-                           true, [&](int n) { return Bv[n]; }, blob, bias));
+                           true, [&](int n) { return Bv[n]; }, blob, bias, f16w));
       }
       pack_rewrite(B.rewrite, ep, B.Cout, 1);
       if (c.dconv_mode & 1) pack_dconv(B.edc, ep, B.Cout, B.h);
@@ -1040,7 +1043,7 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                                const int u = k / Ci, ci = k - u * Ci;
                                return W[((size_t)ci * Co + co) * K + r + St * u];
                              },
-                             true, [&](int n) { return Bv[n % Co]; }, blob, bias));
+                             true, [&](int n) { return Bv[n % Co]; }, blob, bias, f16w));
       }
     }
   }
@@ -1210,9 +1213,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   const int T = m->T, L = c.chunk_size, ach = m->ach, D = m->D;
   const int hid = (int)(m->D * c.t_hidden_scale);
   // SESA_PREC_F16MIX: the cross-transformer attention (QK^T, PV) on one fp16 MFMA pass with fp32 softmax
-  // statistics (attn_f16_kernel); every other contraction bf16x3
+  // statistics (attn_f16_kernel) and the implicit-GEMM convs + 1x1 rewrites on one fp16 pass (operand rounded
+  // once to fp16, fp16 weight images); the transformer / channel Linears bf16x3
   const bool att16 = c.precision == SESA_PREC_F16MIX;
   const int x3 = c.precision == SESA_PREC_BF16X3 || att16 ? 1 : 0;
+  const int cx = att16 ? 2 : x3;   // the implicit-GEMM convs and the 1x1 rewrite: fp16 single pass in fp16mix
   const int St = c.stride, Kk = c.kernel_size, pad = Kk / 4;
   SESA_REQUIRE((int64_t)B * std::max<int64_t>((int64_t)m->fq[0].Fin * T, (int64_t)L) < (1ll << 31) / 4,
                SESA_ERR_INVALID, "htdemucs forward: batch too large");
@@ -1305,7 +1310,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       fprintf(stderr, "[htd conv] M %d N %d K %d taps %d Cin %d phases %d glu %d act %d x2 %d\n", a.M,
               gm.groups[0].N, gm.groups[0].K, g.n_taps, Cin, phases, glu, act, x2 != nullptr);
     void* t0 = profile_begin(st);
-    rc = launch_tok_gemm(a, x3, st);
+    rc = launch_tok_gemm(a, cx, st);
     profile_end(t0, st, SESA_KCLASS_HCONV, gemm_flops(gm, a.M));
   };
   auto lin = [&](const Gemm& gm, const float* xin, int64_t x_ld, float* o, int64_t o_ld, int64_t M, int act,
@@ -1350,7 +1355,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     a.M = (int)M;
     a.glu = 1;
     void* t0 = profile_begin(st);
-    rc = launch_tok_gemm(a, x3, st);
+    rc = launch_tok_gemm(a, cx, st);
     profile_end(t0, st, SESA_KCLASS_HCONV, gemm_flops(gm, M));
   };
   auto dconv = [&](const std::vector<DcLayer>& layers, float* X, int rows, int Tn, int C, int h) {

@@ -59,6 +59,8 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf
 // L2), so block b runs on XCD b % 8.  Tile t = (XCD, b / 8) packed XCD-major keeps consecutive tiles
 // -- the N tiles of one M tile, which share the A rows -- on one XCD's L2 instead of fetching the A
 // rows once per XCD.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
 __device__ __forceinline__ int xcd_tile(int b, int nb) {
   const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
   return x * q + min(x, r) + i;
@@ -72,8 +74,12 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 // applied at store time).
 // BN: output columns per tile, 128 (the packed weight row block) or 64 (one half of it, for the narrow
 // implicit-GEMM convs of HTDemucs: N = 24 / 32 / 48 / 64 fill a 128-column tile to 19-50 %).
-template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB, bool CONV, bool PRE, int BN = kTokBN>
+// F16 (X3 = false): the A operand rounded once to fp16 and the fp16 weight image (pack_group(..., f16)), one
+// v_mfma_f32_32x32x16_f16 pass -- the implicit-GEMM convs of HTDemucs' fp16mix precision.
+template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB, bool CONV, bool PRE, int BN = kTokBN,
+          bool F16 = false>
 __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a) {
+  static_assert(!F16 || (!X3 && !PRE), "fp16: one pass on fp32 rows / conv gathers");
   constexpr int BK = kTokBK;
   static_assert(BN == kTokBN || BN == kTokBN / 2, "tile width");
   static_assert((NT / 64) == (BM / (32 * MI)) * WN && BN == WN * NI * 32, "tile");
@@ -217,9 +223,20 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
           if (a.geo.x2 && ok) v += a2reg[i][q];
         }
         ss[i] = fmaf(v * count, v, ss[i]);
-        split_bf16(v, hi[q], lo[q]);
+        if constexpr (F16) areg[i][q] = v;   // (the fp16 pack below reads the final values)
+        else split_bf16(v, hi[q], lo[q]);
       }
       const int off = row * ROWB + ((((akq >> 3) ^ ((row >> 2) & 3))) << 4) + ((akq & 4) << 1);
+      if constexpr (F16) {
+        const f32x4 v = areg[i];
+        const uint32_t m = ok ? 0xffffffffu : 0u;
+        const auto h2 = [](float x, float y) {
+          return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x) |
+                 ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)y) << 16);
+        };
+        *reinterpret_cast<uint2*>(Ahi + off) = make_uint2(h2(v[0], v[1]) & m, h2(v[2], v[3]) & m);
+        continue;
+      }
       *reinterpret_cast<uint2*>(Ahi + off) = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
       if (X3) *reinterpret_cast<uint2*>(Alo + off) = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
     }
@@ -252,7 +269,10 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
           acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
           acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
         }
-        acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+        if constexpr (F16)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, ah[i]),
+                                                             __builtin_bit_cast(f16x8, bh[j]), acc[i][j], 0, 0, 0);
+        else acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
       }
   };
 
@@ -411,7 +431,6 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
 // each are staged once into the freed LDS by LDS-DMA: the rotary (cos, sin) rows of the tile's tokens
 // (64 KiB), the residual in two 128-row halves (128 KiB each).
 enum : int { EP_RS = 1, EP_ROPE = 2, EP_GELU = 4, EP_RES = 8, EP_SPLIT = 16, EP_RAW = 32, EP_NONE = 64, EP_F16 = 128 };
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float dpp_xor1(float x) {  // lane ^ 1 (quad_perm [1, 0, 3, 2])
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
@@ -1312,7 +1331,7 @@ __global__ void __launch_bounds__(256) tok_split_kernel(const float* __restrict_
 
 int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
   SESA_REQUIRE(a.n_groups >= 1 && a.n_tiles_n >= 1 && a.M >= 0, SESA_ERR_INVALID, "tok_gemm: bad grid");
-  SESA_REQUIRE(x3 != 2 || (a.a_hi && !a.conv), SESA_ERR_INVALID, "tok_gemm: the fp16 mode takes pre-split fp16 A");
+  SESA_REQUIRE(x3 != 2 || !a.a_hi || !a.conv, SESA_ERR_INVALID, "tok_gemm: fp16 conv gathers take fp32 input");
   SESA_REQUIRE(!(a.out_hi && a.residual) && (a.out_hi || a.out), SESA_ERR_INVALID,
                "tok_gemm: split epilogue takes no residual; an output is required");
   if (a.M == 0) return SESA_OK;
@@ -1331,7 +1350,15 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
     SESA_REQUIRE(!a.a_hi, SESA_ERR_INVALID, "tok_gemm conv: pre-split A is for token rows");
     // SESA_HCONV_VARIANT=1: the double-buffered 512-thread 256 x 128 tile for the implicit-GEMM convs (A/B)
     static const int hv = getenv("SESA_HCONV_VARIANT") ? atoi(getenv("SESA_HCONV_VARIANT")) : 0;
-    if (a.bn64) {
+    if (x3 == 2) {
+      // fp16 single pass (fp16 weight images): 64- or 128-column tiles
+      if (a.bn64)
+        hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 1, false, true, false, 64, true>), grid, dim3(256), 0,
+                           st, a);
+      else
+        hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true, false, 128, true>), grid, dim3(256),
+                           0, st, a);
+    } else if (a.bn64) {
       // 64-column tiles (the caller asked for them and counted n_tiles_n in 64-column units)
       if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 1, false, true, false, 64>), grid, dim3(256), 0, st, a);
       else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 1, false, true, false, 64>), grid, dim3(256), 0, st, a);
@@ -1386,6 +1413,10 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
     }
     if (x3) hipLaunchKernelGGL((tok_gemm_kernel<true, 256, 128, 2, 2, 2, false, false, true>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, false, true>), grid, dim3(256), 0, st, a);
+  } else if (x3 == 2) {
+    // fp32 rows rounded once to fp16 in the staging, fp16 weight images, one pass
+    hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, false, false, 128, true>), grid, dim3(256), 0,
+                       st, a);
   } else if (variant == 1) {
     const int64_t mt = (a.M + 255) / 256;
     dim3 g1((unsigned)(mt * a.n_tiles_n), (unsigned)a.n_groups);

@@ -33,7 +33,8 @@ class HTDemucs(NativeModule):
     """Reference-compatible HTDemucs backed by the native HIP forward."""
 
     _prefix = "htdemucs"
-    # fp16mix: the cross-transformer attention on one fp16 MFMA pass (fp32 softmax statistics), the rest bf16x3
+    # fp16mix: the cross-transformer attention (fp32 softmax statistics), the implicit-GEMM convs and the 1x1
+    # rewrites on one fp16 MFMA pass; the transformer / channel Linears bf16x3
     _precisions = ("bf16x3", "bf16", "fp16mix")
 
     def __init__(self, sources, audio_channels=2, samplerate=44100, segment=10, precision="bf16x3", **kw):

@@ -7,7 +7,8 @@ precisions put on fp16 MFMA (sesa_mdx23c.hip); everything else stays ~fp32 (bf16
 Usage:
   python tests/emulation/emulate_mdx23c_levels.py modes  [fixture ...]   # fp32 / fp16 / fp16w2 / mixes
   python tests/emulation/emulate_mdx23c_levels.py scan   fixture [lo:hi]  # fp16 on one conv at a time
-MODES may also name a libsesa SESA_PREC_F16MIX plan as plan:<16 digits>.  Per-conv modes are written as a 32-character string over {3: bf16x3/fp32, 2: fp16w2, 1: fp16}, conv order =
+MODES may also name a libsesa SESA_PREC_F16MIX plan as plan:<16 digits>.  Per-conv modes are written as a 32-character string over {3: bf16x3/fp32, 2: fp16w2, 1: fp16,
+4: fp16 weights x the activation as fp16 hi + lo (two passes)}, conv order =
 call order (encoder L0 block0 tfc1, tfc2, block1 tfc1, tfc2, L1 ..., decoder L3 ... L0).
 """
 import os
@@ -62,6 +63,8 @@ def make(per_conv, tdf=None):
                 return F.conv2d(f16(inp), f16(w), *a, **k)
             if m == "2":
                 return F.conv2d(f16(inp), w_f16x2(w), *a, **k)
+            if m == "4":   # activation as fp16 hi + lo (~exact), fp16 weights: two passes
+                return F.conv2d(inp, f16(w), *a, **k)
         return F.conv2d(inp, w, *a, **k)
 
     ns.conv2d = conv2d
@@ -111,10 +114,12 @@ def main():
     if what == "modes":
         fixtures = sys.argv[2:] or FIXTURES
         modes = os.environ.get("MODES", "fp32,fp16,fp16w2").split(",")
+        # TDF=lo-hi: those TDF stacks' Linears in fp16 too (the fp16mix default: stacks 5-10)
+        tdf = set(range(*(int(v) + i for i, v in enumerate(os.environ["TDF"].split("-"))))) if os.environ.get("TDF") else None
         for fx in fixtures:
             for m in modes:
                 pc = NAMED.get(m, plan_to_convs(m[5:]) if m.startswith("plan:") else m)
-                r, rel, mx, rr = run(fx, pc)
+                r, rel, mx, rr = run(fx, pc, tdf)
                 print(f"{fx:28s} {m:12s} rms {r:.3e} rel {rel:.3e} max {mx:.3e} (ref rms {rr:.3e})", flush=True)
     elif what == "tdfscan":   # fp16 TDF Linears of one stack at a time, on top of a conv plan
         fx = sys.argv[2]
