@@ -1392,6 +1392,15 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
 #define SESA_GLDS(EPV)                                                                                 \
   if (m16) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true>), gbig, dim3(512), 0, st, a);            \
   else hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, false>), gbig, dim3(512), 0, st, a);
+    // fp16: the compact-stage ring, DEPTH - 1 chunks in flight (SESA_TOKGEMM_DEPTH = 2 | 3 | 4; 16x16x32 only)
+    static const int depth = [] {
+      const int d = getenv("SESA_TOKGEMM_DEPTH") ? atoi(getenv("SESA_TOKGEMM_DEPTH")) : 2;
+      return d == 3 || d == 4 ? d : 2;
+    }();
+#define SESA_GLDS16(EPV)                                                                                   \
+  if (m16 && depth == 4) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 4>), gbig, dim3(512), 0, st, a); \
+  else if (m16 && depth == 3) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 3>), gbig, dim3(512), 0, st, a); \
+  else SESA_GLDS(EPV)
     switch (ep) {
       case 0: SESA_GLDS(0) break;
       case EP_RS | EP_ROPE: SESA_GLDS(EP_RS | EP_ROPE) break;
@@ -1400,12 +1409,13 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
       case EP_GELU | EP_SPLIT: SESA_GLDS(EP_GELU | EP_SPLIT) break;
       case EP_SPLIT: SESA_GLDS(EP_SPLIT) break;                       // q / k / v planes for attention
       case EP_RS | EP_ROPE | EP_SPLIT: SESA_GLDS(EP_RS | EP_ROPE | EP_SPLIT) break;
-      case EP_F16 | EP_GELU | EP_SPLIT: SESA_GLDS(EP_F16 | EP_GELU | EP_SPLIT) break;  // FF1 (A pre-scaled)
-      case EP_F16 | EP_RES: SESA_GLDS(EP_F16 | EP_RES) break;                                         // FF2
-      case EP_F16 | EP_ROPE: SESA_GLDS(EP_F16 | EP_ROPE) break;                       // QKV (A pre-scaled)
+      case EP_F16 | EP_GELU | EP_SPLIT: SESA_GLDS16(EP_F16 | EP_GELU | EP_SPLIT) break;  // FF1 (A pre-scaled)
+      case EP_F16 | EP_RES: SESA_GLDS16(EP_F16 | EP_RES) break;                                         // FF2
+      case EP_F16 | EP_ROPE: SESA_GLDS16(EP_F16 | EP_ROPE) break;                       // QKV (A pre-scaled)
       default: ep = -1;
     }
     SESA_REQUIRE(!f16 || ep >= 0, SESA_ERR_INVALID, "tok_gemm: no fp16 kernel for this epilogue / shape");
+#undef SESA_GLDS16
 #undef SESA_GLDS
     if (ep >= 0) {
       SESA_CHECK_LAUNCH();
