@@ -163,6 +163,8 @@ def class_precision(kclass, precision, model="mdx23c"):
         return "fp16"
     if kclass in ("hconv", "attn") and model == "htdemucs" and precision == "fp16mix":
         return "fp16"         # HTDemucs fp16mix: attention and implicit-GEMM convs fp16, Linears bf16x3
+    if kclass == "tokgemm" and model == "scnet" and precision == "fp16mix":
+        return "fp16"         # SCNet fp16mix: token GEMMs fp16, the LSTM recurrence bf16x3
     return "bf16x3"
 
 

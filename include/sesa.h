@@ -22,7 +22,9 @@
  *                       (default: one fp16 pass everywhere except the encoder level-1 convs, bf16x3 --
  *                       they carry ~70 % of the fp16 rounding error at the stems);
  *                       HTDemucs: the cross-transformer attention (QK^T, PV; fp32 softmax statistics),
- *                       the implicit-GEMM convs and 1x1 rewrites on one fp16 pass, the Linears bf16x3
+ *                       the implicit-GEMM convs and 1x1 rewrites on one fp16 pass, the Linears bf16x3;
+ *                       SCNet: the token GEMMs (3x3 convs, LSTM input projections, Linears) on one fp16
+ *                       pass, the LSTM recurrence bf16x3
  */
 #ifndef SESA_H_
 #define SESA_H_
@@ -46,7 +48,7 @@ extern "C" {
 #define SESA_PREC_F16 3   /* MDX23C: TFC 3x3 convs (T >= 32) single fp16 pass; BS- / Mel-Band-Roformer: the
                              QKV / FF Linears single fp16 pass; the rest bf16x3                           */
 #define SESA_PREC_F16MIX 4 /* MDX23C: per-level plan of the T >= 32 TFC 3x3 convs (sesa_mdx23c_set_f16_plan);
-                              HTDemucs: fp16 attention + convs */
+                              HTDemucs: fp16 attention + convs; SCNet: fp16 token GEMMs */
 
 int sesa_version(void);
 const char* sesa_last_error(void);

@@ -1360,7 +1360,8 @@ extern "C" int sesa_scnet_create(const sesa_scnet_config* cfg, sesa_scnet** out)
   SESA_REQUIRE(c.conv_kernel == 3, SESA_ERR_INVALID, "scnet: conv_kernel 3 only");
   SESA_REQUIRE(c.num_dplayer >= 0 && c.num_dplayer % 2 == 0 && c.expand >= 1, SESA_ERR_INVALID,
                "scnet: num_dplayer must be even (rfft/irfft pairs)");
-  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16, SESA_ERR_INVALID, "scnet: precision");
+  SESA_REQUIRE(c.precision == SESA_PREC_BF16X3 || c.precision == SESA_PREC_BF16 || c.precision == SESA_PREC_F16MIX,
+               SESA_ERR_INVALID, "scnet: precision");
   sesa_scnet* m = new sesa_scnet();
   m->cfg = c;
   m->dims.assign(c.dims, c.dims + c.n_dims);
@@ -1614,6 +1615,9 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
   }
   std::vector<uint16_t> blob;
   std::vector<float> bias;
+  // fp16mix: the token GEMMs (3x3 convs, LSTM input projections, dual-path Linears) as fp16 weight images for
+  // the fp16 single-pass kernels; W_hh (the recurrence) stays bf16 hi / lo
+  const bool f16w = m->cfg.precision == SESA_PREC_F16MIX;
   // globalconv / FusionLayer 3x3 convs for the token GEMM's conv mode: K = 9 taps x C (tap = 3 df + dt,
   // channel-minor); FusionLayer: repeat(1, 2) folded, GLU pairs interleaved (column 2j = a_j, 2j + 1 = gate_j)
   for (int i = 0; i < m->nl; ++i) {
@@ -1623,7 +1627,7 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
     const auto& Bg = P(m, "encoder." + S(i) + ".globalconv.bias");
     TokGroup g = pack_group(
         C, 9 * C, [&](int n, int k) { const int tap = k / C, ci = k - tap * C; return Wg[((size_t)n * C + ci) * 9 + tap]; },
-        true, [&](int n) { return Bg[n]; }, blob, bias);
+        true, [&](int n) { return Bg[n]; }, blob, bias, f16w);
     g.x_off = g.o_off = 0;
     L.gc_gm.groups = {g};
     const std::string dpfx = "decoder." + S(m->nl - 1 - i);
@@ -1636,7 +1640,7 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
           const int co = (n & 1) ? C + (n >> 1) : (n >> 1), tap = k / C, ci = k - tap * C;
           return Wf[((size_t)co * C2 + ci) * 9 + tap] + Wf[((size_t)co * C2 + ci + C) * 9 + tap];
         },
-        true, [&](int n) { return Bf[(n & 1) ? C + (n >> 1) : (n >> 1)]; }, blob, bias);
+        true, [&](int n) { return Bf[(n & 1) ? C + (n >> 1) : (n >> 1)]; }, blob, bias, f16w);
     g.x_off = g.o_off = 0;
     L.fu_gm.groups = {g};
   }
@@ -1655,13 +1659,13 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
       TokGroup g = pack_group(
           8 * H, d,
           [&](int n, int k) { return n < 4 * H ? Wf[(int64_t)n * d + k] : Wr[(int64_t)(n - 4 * H) * d + k]; }, true,
-          [&](int n) { return n < 4 * H ? bif[n] + bhf[n] : bir[n - 4 * H] + bhr[n - 4 * H]; }, blob, bias);
+          [&](int n) { return n < 4 * H ? bif[n] + bhf[n] : bir[n - 4 * H] + bhr[n - 4 * H]; }, blob, bias, f16w);
       g.x_off = g.o_off = 0;
       L.ih[l].groups = {g};
       const auto& Wl = P(m, p + ".linear_layers." + S(l) + ".weight");
       const auto& bl = P(m, p + ".linear_layers." + S(l) + ".bias");
       g = pack_group(d, 2 * H, [&](int n, int k) { return Wl[(int64_t)n * 2 * H + k]; }, true,
-                     [&](int n) { return bl[n]; }, blob, bias);
+                     [&](int n) { return bl[n]; }, blob, bias, f16w);
       g.x_off = g.o_off = 0;
       L.lin[l].groups = {g};
       std::vector<float> wt((size_t)2 * H * 4 * H);  // W_hh [4H][H] -> [dir][k][4H]
@@ -1770,7 +1774,9 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
   auto F32 = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
   const float* Wb = m->d_f32;
   const int T = m->T, K = m->K, F0 = m->F0, ach = c.audio_channels;
-  const int x3 = c.precision == SESA_PREC_BF16X3 ? 1 : 0;
+  const bool f16mix = c.precision == SESA_PREC_F16MIX;
+  const int x3 = c.precision == SESA_PREC_BF16X3 || f16mix ? 1 : 0;   // the LSTM recurrence: bf16x3 in fp16mix
+  const int gx = f16mix ? 2 : x3;   // token GEMMs (3x3 convs, input projections, Linears): fp16 single pass
   ScnTables tb;
   int rc = get_tables(&tb);
   if (rc) return rc;
@@ -1806,7 +1812,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
       a.bn64 = 1;
       a.n_tiles_n = (gm.groups[0].N + 63) / 64;
     }
-    return launch_tok_gemm(a, x3, st);
+    return launch_tok_gemm(a, gx, st);
   };
 
   // 1. STFT (scnet.py:335-348)
@@ -1954,7 +1960,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         a.M = (int)rows;
         a.act = TOK_ACT_NONE;
         void* t0 = profile_begin(st);
-        rc = launch_tok_gemm(a, x3, st);
+        rc = launch_tok_gemm(a, gx, st);
         profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(L.ih[path], rows));
         if (rc) return rc;
       }
@@ -2004,7 +2010,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         a.M = (int)rows;
         a.act = TOK_ACT_NONE;
         void* t0 = profile_begin(st);
-        rc = launch_tok_gemm(a, x3, st);
+        rc = launch_tok_gemm(a, gx, st);
         profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(L.lin[path], rows));
         if (rc) return rc;
       }

@@ -20,6 +20,9 @@ class SCNet(NativeModule):
     """Reference-compatible SCNet module (torch.nn.Module) backed by the native HIP forward."""
 
     _prefix = "scnet"
+    # fp16mix: the token GEMMs (3x3 convs, LSTM input projections, dual-path Linears) on one fp16 MFMA pass;
+    # the LSTM recurrence bf16x3, the VALU kernels fp32
+    _precisions = ("bf16x3", "bf16", "fp16mix")
 
     def __init__(self, sources=("drums", "bass", "other", "vocals"), audio_channels=2, dims=(4, 32, 64, 128),
                  nfft=4096, hop_size=1024, win_size=4096, normalized=True, band_SR=(0.175, 0.392, 0.433),
@@ -96,7 +99,8 @@ class SCNet(NativeModule):
             band_stride=(ctypes.c_int * 3)(*k["band_stride"]), band_kernel=(ctypes.c_int * 3)(*k["band_kernel"]),
             conv_depths=(ctypes.c_int * 3)(*k["conv_depths"]), compress=int(k["compress"]),
             conv_kernel=k["conv_kernel"], num_dplayer=k["num_dplayer"], expand=k["expand"],
-            precision=N.SESA_PREC_BF16X3 if self.precision == "bf16x3" else N.SESA_PREC_BF16)
+            precision={"bf16x3": N.SESA_PREC_BF16X3, "bf16": N.SESA_PREC_BF16,
+                       "fp16mix": N.SESA_PREC_F16MIX}[self.precision])
 
     def _out_shape(self, B, ch, L):
         if ch != self.audio_channels:

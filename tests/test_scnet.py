@@ -108,12 +108,13 @@ def dev():
 
 
 @pytest.mark.gpu
-def test_forward_small_matches_reference(golden, dev):
+@pytest.mark.parametrize("precision", ["bf16x3", "fp16mix"])
+def test_forward_small_matches_reference(golden, dev, precision):
     g = golden("scnet_small.npz")
-    m, _ = _model("config_scnet_small.yaml", str(g["affine"]))
+    m, _ = _model("config_scnet_small.yaml", str(g["affine"]), precision)
     y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
     err = rms(y, g["y"])
-    print(f"scnet small rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    print(f"scnet small {precision} rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
     assert y.shape == g["y"].shape and err <= RMS_GATE
 
 
@@ -143,12 +144,14 @@ def test_forward_small_bf16_reports_deviation(golden, dev):
 
 
 @pytest.mark.gpu
-def test_forward_full_chunk_matches_reference(golden, dev):
+@pytest.mark.parametrize("precision", ["bf16x3", "fp16mix"])
+def test_forward_full_chunk_matches_reference(golden, dev, precision):
+    """fp16mix: the token GEMMs (3x3 convs, LSTM input projections, dual-path Linears) on one fp16 pass."""
     g = golden("scnet_full_chunk.npz")
-    m, _ = _model("config_musdb18_scnet.yaml", str(g["affine"]))
+    m, _ = _model("config_musdb18_scnet.yaml", str(g["affine"]), precision)
     y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
     err = rms(y, g["y"])
-    print(f"scnet musdb full chunk rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
+    print(f"scnet musdb full chunk {precision} rms {err:.3e} (ref rms {rms(g['y'], 0):.3e})")
     assert err <= RMS_GATE
 
 

@@ -12,6 +12,8 @@ timeout -k 10 240 ./tools/tokgemm_bench 198648 f16 > $O/tokgemm_f16.txt 2>&1
 echo "[r04f] $(date +%T) parity"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_htdemucs.py -v --timeout 300 \
   --timeout-method thread -k "levels or matrix or config0 or small_matches or full_segment" > $O/parity.txt 2>&1 || rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_scnet.py -v --timeout 300 --timeout-method thread \
+  -k "small_matches or full_chunk_matches" > $O/parity_scnet.txt 2>&1 || rc=$?
 if [ "${rc:-0}" != 0 ]; then echo "[r04f] parity rc=$rc"; [ "$rc" = 1 ] || exit "$rc"; fi
 run() {
   echo "[r04f] $(date +%T) $1"
@@ -25,4 +27,6 @@ run bsr_d4 SESA_TOKGEMM_DEPTH=4 "--model bs_roformer --steps 2 --warmup 1"
 run bsr_d3 SESA_TOKGEMM_DEPTH=3 "--model bs_roformer --steps 2 --warmup 1"
 run htd_fp16mix fp=1 "--model htdemucs --precision fp16mix --steps 1 --warmup 1"
 run htd_bf16x3 fp=1 "--model htdemucs --precision bf16x3 --steps 1 --warmup 1"
+run scn_fp16mix fp=1 "--model scnet --precision fp16mix --steps 2 --warmup 1"
+run scn_bf16x3 fp=1 "--model scnet --precision bf16x3 --steps 2 --warmup 1"
 echo "[r04f] $(date +%T) done"
