@@ -143,9 +143,11 @@ def default_precision(model):
     (bf16x3), the rest bf16x3: every MDX23C full-chunk golden (0.1-RMS noise, §8(d) sines, 0.3-RMS noise, a
     second weight draw) within 5.3e-5 of the reference; plain fp16 sits at 9.75e-5 on the 0.3-RMS fixture, no
     margin -- also for the MDX23C member of the ensemble; BS-Roformer: its QKV / out / FF Linears
-    and attention on one fp16 pass (SESA_PREC_F16); SCNet / HTDemucs (and those ensemble members, build_model)
-    bf16x3.  The line carries the measured parity of every fixture."""
-    return {"mdx23c": "fp16mix", "ensemble": "fp16mix", "bs_roformer": "fp16"}.get(model, "bf16x3")
+    and attention on one fp16 pass (SESA_PREC_F16); HTDemucs fp16mix: attention, implicit-GEMM convs and 1x1
+    rewrites fp16, Linears bf16x3 (5.9e-6 full segment); SCNet fp16mix: token GEMMs fp16, LSTM recurrence
+    bf16x3 (9.7e-6 full chunk) -- the ensemble's SCNet member too.  The line carries the measured parity."""
+    return {"mdx23c": "fp16mix", "ensemble": "fp16mix", "bs_roformer": "fp16", "htdemucs": "fp16mix",
+            "scnet": "fp16mix"}.get(model, "bf16x3")
 
 
 # kernel classes whose kernels run in the MDX23C precision mode; every other class is bf16x3 in the fp16 modes
@@ -165,6 +167,8 @@ def class_precision(kclass, precision, model="mdx23c"):
         return "fp16"         # HTDemucs fp16mix: attention and implicit-GEMM convs fp16, Linears bf16x3
     if kclass == "tokgemm" and model == "scnet" and precision == "fp16mix":
         return "fp16"         # SCNet fp16mix: token GEMMs fp16, the LSTM recurrence bf16x3
+    if kclass == "tokgemm" and model == "htdemucs":
+        return "bf16x3"
     return "bf16x3"
 
 

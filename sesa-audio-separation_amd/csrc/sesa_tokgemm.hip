@@ -446,9 +446,14 @@ __device__ __forceinline__ uint32_t dpp_xor1u(uint32_t x) {
 // DEPTH > 2 (EP_F16 only): compact fp16 stages (A hi plane + the two 128-column hi images, 32 KiB)
 // in a DEPTH-slot ring over the same LDS, DEPTH - 1 chunks in flight instead of one, one barrier per
 // chunk (counted vmcnt waits); the epilogue is unchanged.
-template <int EP, bool M16 = false, int DEPTH = 2>
-__global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
-  constexpr int NT = 512, BM = 256, BK = kTokBK, WN = 4;
+// HT (half tile; fp16 ring only): 256 threads, 256 tokens x 128 columns (4 waves of 128 x 64), a 24 KiB ring
+// slot, two workgroups per CU -- one workgroup's epilogue runs beside the other's main loop instead of
+// idling the MFMA pipe (the epilogues of the fp16 Linears cost as much as their main loops).
+template <int EP, bool M16 = false, int DEPTH = 2, bool HT = false>
+__global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kernel(TokGemmArgs a) {
+  constexpr int NT = HT ? 256 : 512, BM = 256, BK = kTokBK, WN = HT ? 2 : 4;
+  constexpr int NW = NT / 64;                              // waves
+  constexpr int TN = HT ? 128 : 256;                       // tile columns
   constexpr int BLK = M16 ? 16 : 32;                       // MFMA block edge
   constexpr int MI = 128 / BLK, NI = 64 / BLK;             // blocks per 128 x 64 wave tile
   constexpr int RPB = BLK * BLK / 64;                      // accumulator registers per block
@@ -464,16 +469,21 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   constexpr int APW = A_PIECES / (NT / 64);                 // of which A pieces (4)
   static_assert((A_PIECES + W_PIECES) % (NT / 64) == 0 && A_PIECES % (NT / 64) == 0, "piece split");
   static_assert(2 * STAGE >= 128 * 1024, "epilogue staging reuses the two stages");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * BM * 4];
-  float* rs = reinterpret_cast<float*>(smem + 2 * STAGE);
+  constexpr bool CMP = (EP & EP_F16) != 0 && DEPTH > 2;   // compact fp16 ring
+  constexpr int SSZ = CMP ? A_BYTES + (HT ? 1 : 2) * W_PLANE : STAGE;  // bytes per ring slot
+  static_assert(!HT || CMP, "half tile: the fp16 ring only");
+  // LDS: the two bf16x3 stages, or (HT) the ring, at least the 64 KiB the epilogue staging takes
+  constexpr int RING = HT ? (DEPTH * SSZ > 65536 ? DEPTH * SSZ : 65536) : 2 * STAGE;
+  __shared__ __attribute__((aligned(16))) char smem[RING + 2 * BM * 4];
+  float* rs = reinterpret_cast<float*>(smem + RING);
   int* rpos = reinterpret_cast<int*>(rs + BM);
 
   const TokGroup g = a.groups[blockIdx.y];
-  const int n_tiles2 = (a.n_tiles_n + 1) >> 1;             // 256-column tiles
+  const int n_tiles2 = HT ? a.n_tiles_n : (a.n_tiles_n + 1) >> 1;   // TN-column tiles
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const int n_tile2 = tile % n_tiles2;
   const int m_tile = tile / n_tiles2;
-  const int n0 = n_tile2 * 256;
+  const int n0 = n_tile2 * TN;
   if (n0 >= g.N) return;
   const int m0 = m_tile * BM;
   const int tid = threadIdx.x;
@@ -481,9 +491,7 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int l32 = lane & 31, h = lane >> 5;
   const int n_chunks = (g.K + BK - 1) / BK;
-  constexpr bool CMP = (EP & EP_F16) != 0 && DEPTH > 2;   // compact fp16 ring
-  constexpr int SSZ = CMP ? A_BYTES + 2 * W_PLANE : STAGE;  // bytes per ring slot
-  static_assert(!CMP || DEPTH * SSZ <= 2 * STAGE, "ring fits the two bf16x3 stages");
+  static_assert(!CMP || DEPTH * SSZ <= RING, "ring fits the LDS");
   static_assert(DEPTH == 2 || ((EP & EP_F16) != 0 && M16), "deep ring: the fp16 16x16x32 kernel only");
 
   for (int r = tid; r < BM; r += NT) {                      // ordinary loads, before any DMA is in flight
@@ -493,22 +501,42 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   }
 
   // this lane's A pieces: piece p (per plane) covers tile rows 16 p .. 16 p + 15, 4 lanes a row
-  constexpr int AP1 = A_BYTES / 1024 / (NT / 64);           // pieces per plane per wave (2)
+  constexpr int AP1 = A_BYTES / 1024 / NW;                  // pieces per plane per wave (2; HT 4)
   constexpr bool F16 = (EP & EP_F16) != 0;                  // fp16 A planes x fp16 weight images, one pass
   int64_t asrc[AP1];
   int aslot8[AP1];
 #pragma unroll
   for (int i = 0; i < AP1; ++i) {
-    const int row = 16 * (wave + 8 * i) + (lane >> 2);
+    const int row = 16 * (wave + NW * i) + (lane >> 2);
     asrc[i] = (int64_t)min(m0 + row, a.M - 1) * a.a_ld + g.x_off;
     aslot8[i] = 8 * ((lane & 3) ^ ((row >> 2) & 3));
   }
   const int64_t wimg = W_IMG / 2;                           // uint16 per packed chunk image (hi + lo)
-  const uint16_t* wblk0 = a.w + g.w_off + (int64_t)(2 * n_tile2) * n_chunks * wimg;
+  const uint16_t* wblk0 = a.w + g.w_off + (int64_t)((HT ? 1 : 2) * n_tile2) * n_chunks * wimg;
   // the second 128-column tile; past the group's last tile a harmless repeat (its columns are >= N)
   const uint16_t* wblk1 = n0 + kTokBN < g.N ? wblk0 + (int64_t)n_chunks * wimg : wblk0;
 
+  // compact fp16 ring: per wave and chunk AP1 A pieces + WPW hi-image pieces (the lo planes are never read)
+  constexpr int WPW = (HT ? 8 : 16) / NW;
+  constexpr int PPC = AP1 + WPW;                            // DMA pieces per wave per chunk
   auto issue = [&](int kc, char* stg) {
+    if constexpr (CMP) {
+#pragma unroll
+      for (int i = 0; i < AP1; ++i) {                       // A piece wave + NW i: tile rows 16 p .. 16 p + 15
+        const int k = kc * BK + aslot8[i];
+        const uint16_t* src = a.a_hi + asrc[i] + (k < g.K ? k : 0);
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stg + (wave + NW * i) * 1024),
+                                         16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < WPW; ++i) {                       // hi piece q of the (one or two) 128-column images
+        const int q = wave + NW * i, half = q >> 3, qq = q & 7;
+        const uint16_t* src = (half ? wblk1 : wblk0) + (int64_t)kc * wimg + qq * 512 + lane * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stg + A_BYTES + q * 1024), 16,
+                                         0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       // EP_F16: the lo planes are never read -- skip their pieces (A plane 1; the odd W pieces of this
@@ -526,9 +554,8 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
         const int q = wave + 8 * (i - APW);
         const int half = q / W_HALF, qq = q - half * W_HALF;
         const uint16_t* src = (half ? wblk1 : wblk0) + (int64_t)kc * wimg + qq * 512 + lane * 8;
-        // compact ring: hi image half h at A_BYTES + h W_PLANE (qq < 8: the hi pieces)
-        char* dst = CMP ? stg + A_BYTES + half * W_PLANE + qq * 1024 : stg + A_REG + q * 1024;
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stg + A_REG + q * 1024), 16,
+                                         0, 0);
       }
     }
   };
@@ -595,15 +622,16 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   // 8 gate columns after q / k / v) skip their MFMAs (wave-uniform); they still issue their DMA pieces
   const bool busy = n0 + wn * 64 < g.N;
   if constexpr (CMP) {
-    // 4 DMA pieces per wave per chunk (2 A, 2 W): chunk kc has landed for this wave when at most
-    // 4 min(DEPTH - 2, n_chunks - 1 - kc) of its pieces are still outstanding
+    // PPC DMA pieces per wave per chunk: chunk kc has landed for this wave when at most
+    // PPC min(DEPTH - 2, n_chunks - 1 - kc) of its pieces are still outstanding
+    static_assert(DEPTH <= 4 && 2 * PPC <= 63, "counted waits");
 #pragma unroll
     for (int s = 0; s < DEPTH - 1; ++s)
       if (s < n_chunks) issue(s, smem + s * SSZ);
     for (int kc = 0; kc < n_chunks; ++kc) {
       const int pend = min(DEPTH - 2, n_chunks - 1 - kc);
-      if (pend >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (pend == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (pend >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPC) : "memory");
+      else if (pend == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPC) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // every wave's pieces of chunk kc landed, and every wave's reads of slot (kc - 1) % DEPTH retired
       // (lgkmcnt(0) below) -- that slot takes chunk kc + DEPTH - 1
@@ -660,8 +688,8 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
   const float2* lrope = reinterpret_cast<const float2*>(smem);
   if constexpr ((EP & EP_ROPE) != 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {                          // piece q: tile rows 4 q .. 4 q + 3 (256 B each)
-      const int q = wave + 8 * i;
+    for (int i = 0; i < 64 / NW; ++i) {                    // piece q: tile rows 4 q .. 4 q + 3 (256 B each)
+      const int q = wave + NW * i;
       const int row = 4 * q + (lane >> 4);
       const float2* src = a.rope + (int64_t)rpos[row] * 32 + (lane & 15) * 2;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + q * 1024), 16, 0, 0);
@@ -670,7 +698,7 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
-  const bool full = m0 + BM <= a.M && n0 + 256 <= g.N;
+  const bool full = m0 + BM <= a.M && n0 + TN <= g.N;
   float bias[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -716,7 +744,7 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
           const float y = (d & 1) ? fmaf(x, cs.x, partner * cs.y) : fmaf(x, cs.x, -partner * cs.y);
           x = rot ? y : x;
         }
-        if constexpr ((EP & EP_RES) != 0) x += lres[(ml - p * 64 - wm * 64) * 256 + nl];
+        if constexpr ((EP & EP_RES) != 0) x += lres[(ml - p * 64 - wm * 64) * TN + nl];
         v[r] = x;
       }
     }
@@ -772,15 +800,19 @@ __global__ void __launch_bounds__(512, 1) tok_gemm_glds_kernel(TokGemmArgs a) {
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
         }
+        // 128 local rows of TN fp32 (1 KiB piece = 1024 / (4 TN) rows); local row rl <-> tile row (half p of
+        // each wm)
+        constexpr int RPP = 256 / TN, LPR = 64 / RPP;      // rows per piece, lanes per row
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {                     // local row rl <-> tile row (half p of each wm)
-          const int rl = wave + 8 * i;
+        for (int i = 0; i < 128 / RPP / NW; ++i) {
+          const int pc = wave + NW * i;
+          const int rl = pc * RPP + lane / LPR;
           const int row = rl < 64 ? p * 64 + rl : 128 + p * 64 + (rl - 64);
           const int m = min(m0 + row, a.M - 1);
-          int col = n0 + lane * 4;
+          int col = n0 + (lane % LPR) * 4;
           if (col + 4 > g.N) col = n0;                     // columns >= N are never used
           const float* src = a.residual + (int64_t)m * a.o_ld + g.o_off + col;
-          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + rl * 1024), 16, 0,
+          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0,
                                            0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1355,6 +1387,9 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
       if (a.bn64)
         hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 1, false, true, false, 64, true>), grid, dim3(256), 0,
                            st, a);
+      else if (hv == 1)
+        hipLaunchKernelGGL((tok_gemm_kernel<false, 512, 256, 2, 2, 2, true, true, false, 128, true>),
+                           dim3((unsigned)(((a.M + 255) / 256) * a.n_tiles_n)), dim3(512), 0, st, a);
       else
         hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true, false, 128, true>), grid, dim3(256),
                            0, st, a);
@@ -1392,13 +1427,19 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
 #define SESA_GLDS(EPV)                                                                                 \
   if (m16) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true>), gbig, dim3(512), 0, st, a);            \
   else hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, false>), gbig, dim3(512), 0, st, a);
-    // fp16: the compact-stage ring, DEPTH - 1 chunks in flight (SESA_TOKGEMM_DEPTH = 2 | 3 | 4; 16x16x32 only)
+    // fp16: the compact-stage ring, DEPTH - 1 chunks in flight (SESA_TOKGEMM_DEPTH = 2 | 3 | 4; 16x16x32 only).
+    // Depth 3 by default: same box, BS-Roformer 189.2x (2) -> 194.0x (3), 192.2x (4); outputs bit-identical
+    // (profiles/r04_tokgemm_bench_f16.txt, r04_bsr_depth_*.json)
     static const int depth = [] {
-      const int d = getenv("SESA_TOKGEMM_DEPTH") ? atoi(getenv("SESA_TOKGEMM_DEPTH")) : 2;
+      const int d = getenv("SESA_TOKGEMM_DEPTH") ? atoi(getenv("SESA_TOKGEMM_DEPTH")) : 3;
       return d == 3 || d == 4 ? d : 2;
     }();
+    // SESA_TOKGEMM_HT=1: the half tile (256 x 128, 256 threads, two workgroups per CU) on a depth-3 ring
+    static const bool ht = getenv("SESA_TOKGEMM_HT") && std::string(getenv("SESA_TOKGEMM_HT")) == "1";
+    const dim3 ght((unsigned)(((a.M + 255) / 256) * a.n_tiles_n), (unsigned)a.n_groups);
 #define SESA_GLDS16(EPV)                                                                                   \
-  if (m16 && depth == 4) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 4>), gbig, dim3(512), 0, st, a); \
+  if (m16 && ht) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 3, true>), ght, dim3(256), 0, st, a);    \
+  else if (m16 && depth == 4) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 4>), gbig, dim3(512), 0, st, a); \
   else if (m16 && depth == 3) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 3>), gbig, dim3(512), 0, st, a); \
   else SESA_GLDS(EPV)
     switch (ep) {

@@ -114,8 +114,14 @@ def main():
     if what == "modes":
         fixtures = sys.argv[2:] or FIXTURES
         modes = os.environ.get("MODES", "fp32,fp16,fp16w2").split(",")
-        # TDF=lo-hi: those TDF stacks' Linears in fp16 too (the fp16mix default: stacks 5-10)
-        tdf = set(range(*(int(v) + i for i, v in enumerate(os.environ["TDF"].split("-"))))) if os.environ.get("TDF") else None
+        # TDF=...: those TDF stacks' Linears in fp16 too (the fp16mix default: stacks 5-10)
+        # (comma-separated stacks or lo-hi ranges, e.g. 0,4-10)
+        tdf = None
+        if os.environ.get("TDF"):
+            tdf = set()
+            for part in os.environ["TDF"].split(","):
+                lo, _, hi = part.partition("-")
+                tdf |= set(range(int(lo), int(hi or lo) + 1))
         for fx in fixtures:
             for m in modes:
                 pc = NAMED.get(m, plan_to_convs(m[5:]) if m.startswith("plan:") else m)

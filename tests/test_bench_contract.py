@@ -20,8 +20,14 @@ def test_default_precision():
     assert bench.default_precision("mdx23c") == bench.default_precision("ensemble") == "fp16mix"
     assert bench.default_precision("bs_roformer") == "fp16"
     for m in ("htdemucs", "scnet"):
-        assert bench.default_precision(m) == "bf16x3"
-    # PMC stamps: only the MDX23C classes run in the fp16 mode
+        assert bench.default_precision(m) == "fp16mix"
+    # PMC stamps: the classes each model's fp16 mode puts on fp16 MFMA
+    assert bench.class_precision("hconv", "fp16mix", "htdemucs") == "fp16"
+    assert bench.class_precision("attn", "fp16mix", "htdemucs") == "fp16"
+    assert bench.class_precision("tokgemm", "fp16mix", "htdemucs") == "bf16x3"
+    assert bench.class_precision("tokgemm", "fp16mix", "scnet") == "fp16"
+    assert bench.class_precision("lstm", "fp16mix", "scnet") == "bf16x3"
+    assert bench.class_precision("simt", "fp16mix", "scnet") == "bf16x3"
     assert bench.class_precision("conv3x3", "fp16") == "fp16"
     assert bench.class_precision("tokgemm", "fp16") == "bf16x3"
     assert bench.class_precision("tokgemm", "fp16", "bs_roformer") == "fp16"

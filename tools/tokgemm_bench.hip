@@ -64,6 +64,12 @@ template <int EP, int D>
 void launch_f16(const TokGemmArgs& a, dim3 g) {
   hipLaunchKernelGGL((tok_gemm_glds_kernel<EP, true, D>), g, dim3(512), 0, 0, a);
 }
+// half tile: 256 x 128 per 256-thread workgroup, two workgroups per CU
+template <int EP>
+void launch_ht(const TokGemmArgs& a) {
+  const dim3 g((unsigned)(((a.M + 255) / 256) * a.n_tiles_n));
+  hipLaunchKernelGGL((tok_gemm_glds_kernel<EP, true, 3, true>), g, dim3(256), 0, 0, a);
+}
 template <int EP>
 void f16_shape(const char* name, int M, int N, int K, TokGemmArgs a, dim3 g, size_t n_out, bool planes) {
   const double flop = 2.0 * M * (double)N * K;
@@ -71,6 +77,8 @@ void f16_shape(const char* name, int M, int N, int K, TokGemmArgs a, dim3 g, siz
   rep("f16 depth 2", time_ms([&] { launch_f16<EP, 2>(a, g); }));
   rep("f16 depth 3", time_ms([&] { launch_f16<EP, 3>(a, g); }));
   rep("f16 depth 4", time_ms([&] { launch_f16<EP, 4>(a, g); }));
+  rep("f16 half tile (2 WG / CU)", time_ms([&] { launch_ht<EP>(a); }));
+  rep("f16 half tile no epilogue", time_ms([&] { launch_ht<EP_F16 | EP_NONE>(a); }));
   rep("f16 depth 2 no epilogue", time_ms([&] { launch_f16<EP_F16 | EP_NONE, 2>(a, g); }));
   rep("f16 depth 4 no epilogue", time_ms([&] { launch_f16<EP_F16 | EP_NONE, 4>(a, g); }));
   if constexpr ((EP & EP_GELU) != 0)
@@ -86,8 +94,9 @@ void f16_shape(const char* name, int M, int N, int K, TokGemmArgs a, dim3 g, siz
   const auto r2 = get([&] { launch_f16<EP, 2>(a, g); });
   const auto r3 = get([&] { launch_f16<EP, 3>(a, g); });
   const auto r4 = get([&] { launch_f16<EP, 4>(a, g); });
-  printf("     depth 3 %s depth 2, depth 4 %s depth 2\n", r3 == r2 ? "IDENTICAL to" : "DIFFERS from",
-         r4 == r2 ? "IDENTICAL to" : "DIFFERS from");
+  const auto rh = get([&] { launch_ht<EP>(a); });
+  printf("     depth 3 %s depth 2, depth 4 %s depth 2, half tile %s depth 2\n", r3 == r2 ? "IDENTICAL to" : "DIFFERS from",
+         r4 == r2 ? "IDENTICAL to" : "DIFFERS from", rh == r2 ? "IDENTICAL to" : "DIFFERS from");
 }
 
 void run_f16(int M) {
