@@ -80,8 +80,8 @@ __global__ void __launch_bounds__(kT) htd_stft_kernel(const float* __restrict__ 
                                                       float* __restrict__ X) {
   __shared__ float2 bufA[kFft2048];
   __shared__ float2 bufB[kFft2048];
-  const int t = blockIdx.x;
-  const int sig = blockIdx.y;
+  const int t = blockIdx.y;      // signal-major grid: the ach channels of one frame write one 16-B group per bin
+  const int sig = blockIdx.x;
   const int b = sig / ach, c = sig - b * ach;
   const float* xs = x + (int64_t)sig * L;
   const int64_t j0 = (int64_t)t * kHop - kPadSpec;
@@ -494,8 +494,10 @@ __global__ void __launch_bounds__(kT) htd_istft_frames_kernel(const float* __res
                                                               float* __restrict__ fw) {
   __shared__ float2 bufA[kFft2048];
   __shared__ float2 bufB[kFft2048 + 1];
-  const int t = blockIdx.x;
-  const int sig = blockIdx.y;
+  // signal-major grid: the nsrc * ach workgroups of one (item, frame) run back to back, so the 64-B channel
+  // groups of Z[b][k][t][:] each fetches (one 128-B line per bin, shared by all of them) hit L2 after the first
+  const int t = blockIdx.y;
+  const int sig = blockIdx.x;
   const int b = sig / (nsrc * ach), rem = sig - b * nsrc * ach;
   const int s = rem / ach, c = rem - s * ach;
   float mean, sd;
@@ -1221,6 +1223,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   const int St = c.stride, Kk = c.kernel_size, pad = Kk / 4;
   SESA_REQUIRE((int64_t)B * std::max<int64_t>((int64_t)m->fq[0].Fin * T, (int64_t)L) < (1ll << 31) / 4,
                SESA_ERR_INVALID, "htdemucs forward: batch too large");
+  SESA_REQUIRE(T < 65536, SESA_ERR_INVALID, "htdemucs forward: %d STFT frames per item (grid y < 65536)", T);
   Fft2048Tables tb;
   int rc = get_fft2048_tables(&tb);
   if (rc) return rc;
@@ -1236,7 +1239,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   SESA_CHECK_HIP(hipMemsetAsync(stats, 0, (size_t)B * 8 * sizeof(double), st));
   {
     void* tok = profile_begin(st);
-    hipLaunchKernelGGL(htd_stft_kernel, dim3(T, B * ach), dim3(kT), 0, st, x, ach, L, T, win, tb, X0);
+    hipLaunchKernelGGL(htd_stft_kernel, dim3(B * ach, T), dim3(kT), 0, st, x, ach, L, T, win, tb, X0);
     SESA_CHECK_LAUNCH();
     profile_end(tok, st, SESA_KCLASS_STFT, 4.0 * B * ach * ((double)L + (double)T * kF0 * 2));
   }
@@ -1701,7 +1704,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     void* tok = profile_begin(st);
     float* FR = F32(pl.frames);
     const int nsig = B * m->nsrc * ach;
-    hipLaunchKernelGGL(htd_istft_frames_kernel, dim3(T, nsig), dim3(kT), 0, st, cur_f, T, m->fq[0].Cdec, ach, m->nsrc,
+    hipLaunchKernelGGL(htd_istft_frames_kernel, dim3(nsig, T), dim3(kT), 0, st, cur_f, T, m->fq[0].Cdec, ach, m->nsrc,
                        st_f, (int64_t)kF0 * T * 2 * ach, win, tb, FR);
     SESA_CHECK_LAUNCH();
     hipLaunchKernelGGL(htd_istft_ola_kernel, dim3((L + kT - 1) / kT, nsig), dim3(kT), 0, st, FR, T, L, ach, m->nsrc, win,

@@ -699,6 +699,9 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
     asm volatile("" ::: "memory");
   }
   const bool full = m0 + BM <= a.M && n0 + TN <= g.N;
+  // fp16 split output staged through LDS (the ring is free after the main loop) and stored as full lines
+  // (not beside the rotary table, which occupies the same LDS during the epilogue)
+  const bool stage16 = (EP & EP_SPLIT) != 0 && (EP & EP_ROPE) == 0 && F16 && a.o_ld % 8 == 0 && g.o_off % 8 == 0;
   float bias[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -756,7 +759,13 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
         const uint32_t hb = __builtin_bit_cast(uint16_t, (_Float16)v[r]);
         const int64_t o = (int64_t)m * a.o_ld + g.o_off + n;
         const uint32_t hn = dpp_xor1u(hb);  // uniform control flow
-        if (FULL) {
+        if (FULL && stage16) {
+          // into the LDS tile image (row stride 2 TN bytes, 32-B groups XOR-permuted by (row >> 2) & 3: the
+          // four row groups of one store land in different banks); written out in full lines below
+          const int ml = row_of(i, r);
+          if (!(l32 & 1))
+            *reinterpret_cast<uint32_t*>(smem + ml * (2 * TN) + ((2 * nl) ^ (((ml >> 2) & 3) << 5))) = hb | (hn << 16);
+        } else if (FULL) {
           if (!(l32 & 1)) *reinterpret_cast<uint32_t*>(a.out_hi + o) = hb | (hn << 16);
         } else if (m < a.M && n < g.N) {
           a.out_hi[o] = (uint16_t)hb;
@@ -826,6 +835,23 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
   };
   if (full) run(std::true_type{});
   else run(std::false_type{});
+  if constexpr ((EP & EP_SPLIT) != 0 && F16) {
+    if (full && stage16) {
+      // the fp16 tile from LDS as full rows: 16 B per lane, 2 TN bytes contiguous per row
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      constexpr int C16 = 2 * TN / 16;                     // 16-B groups per row
+#pragma unroll 4
+      for (int it = 0; it < BM * C16 / NT; ++it) {
+        const int e = tid + it * NT;
+        const int row = e / C16, c16 = e % C16;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(smem + row * (2 * TN) + ((16 * c16) ^ (((row >> 2) & 3) << 5)));
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(a.out_hi + (int64_t)(m0 + row) * a.o_ld + g.o_off + n0 +
+                                                                8 * c16));
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
