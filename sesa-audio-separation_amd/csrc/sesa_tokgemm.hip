@@ -76,10 +76,13 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 // implicit-GEMM convs of HTDemucs: N = 24 / 32 / 48 / 64 fill a 128-column tile to 19-50 %).
 // F16 (X3 = false): the A operand rounded once to fp16 and the fp16 weight image (pack_group(..., f16)), one
 // v_mfma_f32_32x32x16_f16 pass -- the implicit-GEMM convs of HTDemucs' fp16mix precision.
+// PD (single-stage form): register sets for PD chunks, so chunk kc + PD is loading while chunk kc is staged and
+// computed (PD = 1: the next chunk only -- its gather latency, not the MFMAs, bounded the narrow HTDemucs convs).
 template <bool X3, int NT, int BM, int WN, int MI, int NI, bool DB, bool CONV, bool PRE, int BN = kTokBN,
-          bool F16 = false>
+          bool F16 = false, int PD = 1>
 __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a) {
   static_assert(!F16 || (!X3 && !PRE), "fp16: one pass on fp32 rows / conv gathers");
+  static_assert(PD >= 1 && (PD == 1 || !DB), "register prefetch depth: single-stage form");
   constexpr int BK = kTokBK;
   static_assert(BN == kTokBN || BN == kTokBN / 2, "tile width");
   static_assert((NT / 64) == (BM / (32 * MI)) * WN && BN == WN * NI * 32, "tile");
@@ -119,16 +122,16 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
   constexpr int AI = BM * 8 / NT;
   constexpr int RS = NT / 8;
   const int arow0 = tid >> 3, akq = (tid & 7) * 4;
-  f32x4 areg[AI];
-  f32x4 a2reg[CONV ? AI : 1];
-  uint2 ahreg[PRE ? AI : 1], alreg[PRE && X3 ? AI : 1];  // pre-split quads (4 bf16 each)
+  f32x4 areg[PD][AI];
+  f32x4 a2reg[PD][CONV ? AI : 1];
+  uint2 ahreg[PD][PRE ? AI : 1], alreg[PD][PRE && X3 ? AI : 1];  // pre-split quads (4 bf16 each)
   float ss[AI];
   const float* xrow[AI];
   int64_t prow[PRE ? AI : 1];                             // plane element offset of the row
   bool rok[AI];
   // CONV: per-row input grid origin (b Q1, i1 s1, i2 s2) and per-chunk validity
   int rb1[CONV ? AI : 1], ri1[CONV ? AI : 1], ri2[CONV ? AI : 1];
-  bool aval[CONV ? AI : 1];
+  bool aval[PD][CONV ? AI : 1];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     ss[i] = 0.f;
@@ -143,30 +146,31 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
       rb1[i] = b * a.geo.Q1;
       ri1[i] = i1 * a.geo.s1;
       ri2[i] = i2 * a.geo.s2;
-      aval[i] = false;
+      for (int s = 0; s < PD; ++s) aval[s][i] = false;
     }
   }
-  bool kok = true;
+  bool kok[PD];
   constexpr int W16 = (X3 ? 2 : 1) * W_BYTES / 16;
   constexpr int W_ITEMS = (W16 + NT - 1) / NT;
-  u32x4 wreg[W_ITEMS];
+  u32x4 wreg[PD][W_ITEMS];
   // packed per 128-column block: [block][chunk][hi 128 x 32][lo 128 x 32]; a 64-column tile takes rows
   // 64 half .. 64 half + 63 of both planes (the row swizzle depends on row & 15 only, so it carries over)
   constexpr int IMG128 = kTokBN * BK;                       // uint16 per plane of a packed chunk image
   const uint16_t* wblk = a.w + g.w_off + (int64_t)(BN == kTokBN ? n_tile : n_tile >> 1) * n_chunks * (2 * IMG128) +
                          (BN == kTokBN ? 0 : (n_tile & 1) * (BN * BK));
 
-  auto load_chunk = [&](int kc) {
+  auto load_chunk = [&](auto S, int kc) {
+    constexpr int s = decltype(S)::value;
     const uint16_t* wc = wblk + (int64_t)kc * (2 * IMG128);
     Unroll<0, W_ITEMS>::run([&](auto I) {
       const int e = min(tid + I * NT, W16 - 1);
       constexpr int PL16 = W_BYTES / 16;                    // u32x4 per plane of this tile
       const int pl = e >= PL16 ? 1 : 0, ee = e - pl * PL16;
-      wreg[I] = reinterpret_cast<const u32x4*>(wc + pl * IMG128)[ee];
+      wreg[s][I] = reinterpret_cast<const u32x4*>(wc + pl * IMG128)[ee];
     });
     const int k = kc * BK + akq;
-    kok = k < g.K;  // K % 4 == 0 (host check): a quad is wholly in or out
-    const int kc_ = kok ? k : 0;
+    kok[s] = k < g.K;  // K % 4 == 0 (host check): a quad is wholly in or out
+    const int kc_ = kok[s] ? k : 0;
     if constexpr (CONV) {
       // Cin % 4 == 0 (host check): a quad lies inside one tap
       const int tap = kc_ / a.geo.Cin, c = kc_ - tap * a.geo.Cin;
@@ -174,61 +178,62 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const int j1 = ri1[i] + d1, j2 = ri2[i] + d2;
-        aval[i] = rok[i] && kok && j1 >= 0 && j1 < a.geo.Q1 && j2 >= 0 && j2 < a.geo.Q2;
-        const int64_t off = aval[i] ? ((int64_t)(rb1[i] + j1) * a.geo.Q2 + j2) * a.x_ld + g.x_off + c : 0;
-        areg[i] = *reinterpret_cast<const f32x4*>(a.x + off);
-        if (a.geo.x2) a2reg[i] = *reinterpret_cast<const f32x4*>(a.geo.x2 + off);
+        aval[s][i] = rok[i] && kok[s] && j1 >= 0 && j1 < a.geo.Q1 && j2 >= 0 && j2 < a.geo.Q2;
+        const int64_t off = aval[s][i] ? ((int64_t)(rb1[i] + j1) * a.geo.Q2 + j2) * a.x_ld + g.x_off + c : 0;
+        areg[s][i] = *reinterpret_cast<const f32x4*>(a.x + off);
+        if (a.geo.x2) a2reg[s][i] = *reinterpret_cast<const f32x4*>(a.geo.x2 + off);
       }
     } else if constexpr (PRE) {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
-        ahreg[i] = *reinterpret_cast<const uint2*>(a.a_hi + prow[i] + kc_);
-        if constexpr (X3) alreg[i] = *reinterpret_cast<const uint2*>(a.a_lo + prow[i] + kc_);
+        ahreg[s][i] = *reinterpret_cast<const uint2*>(a.a_hi + prow[i] + kc_);
+        if constexpr (X3) alreg[s][i] = *reinterpret_cast<const uint2*>(a.a_lo + prow[i] + kc_);
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < AI; ++i) areg[i] = *reinterpret_cast<const f32x4*>(xrow[i] + kc_);
+      for (int i = 0; i < AI; ++i) areg[s][i] = *reinterpret_cast<const f32x4*>(xrow[i] + kc_);
     }
   };
   // count: 1 when this store is a real chunk (0 for the clamped repeat past the end: no RMS sum)
-  auto store_chunk = [&](char* stg, float count) {
+  auto store_chunk = [&](auto S, char* stg, float count) {
+    constexpr int s = decltype(S)::value;
     char* Ahi = stg;
     char* Alo = stg + A_BYTES;
     u32x4* d4 = reinterpret_cast<u32x4*>(stg + 2 * A_BYTES);
     Unroll<0, W_ITEMS>::run([&](auto I) {
       const int e = min(tid + I * NT, W16 - 1);  // duplicates write identical values
-      d4[e] = wreg[I];
+      d4[e] = wreg[s][I];
     });
     if constexpr (PRE) {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const int row = arow0 + RS * i;
-        const bool ok = rok[i] && kok;
+        const bool ok = rok[i] && kok[s];
         const int off = row * ROWB + ((((akq >> 3) ^ ((row >> 2) & 3))) << 4) + ((akq & 4) << 1);
-        *reinterpret_cast<uint2*>(Ahi + off) = ok ? ahreg[i] : make_uint2(0u, 0u);
-        if (X3) *reinterpret_cast<uint2*>(Alo + off) = ok ? alreg[i] : make_uint2(0u, 0u);
+        *reinterpret_cast<uint2*>(Ahi + off) = ok ? ahreg[s][i] : make_uint2(0u, 0u);
+        if (X3) *reinterpret_cast<uint2*>(Alo + off) = ok ? alreg[s][i] : make_uint2(0u, 0u);
       }
       return;
     }
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int row = arow0 + RS * i;
-      bool ok = rok[i] && kok;
-      if constexpr (CONV) ok = aval[i];
+      bool ok = rok[i] && kok[s];
+      if constexpr (CONV) ok = aval[s][i];
       __bf16 hi[4], lo[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float v = ok ? areg[i][q] : 0.f;
+        float v = ok ? areg[s][i][q] : 0.f;
         if constexpr (CONV) {
-          if (a.geo.x2 && ok) v += a2reg[i][q];
+          if (a.geo.x2 && ok) v += a2reg[s][i][q];
         }
         ss[i] = fmaf(v * count, v, ss[i]);
-        if constexpr (F16) areg[i][q] = v;   // (the fp16 pack below reads the final values)
+        if constexpr (F16) areg[s][i][q] = v;   // (the fp16 pack below reads the final values)
         else split_bf16(v, hi[q], lo[q]);
       }
       const int off = row * ROWB + ((((akq >> 3) ^ ((row >> 2) & 3))) << 4) + ((akq & 4) << 1);
       if constexpr (F16) {
-        const f32x4 v = areg[i];
+        const f32x4 v = areg[s][i];
         const uint32_t m = ok ? 0xffffffffu : 0u;
         const auto h2 = [](float x, float y) {
           return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x) |
@@ -276,31 +281,49 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
       }
   };
 
-  if (DB) {
-    load_chunk(0);
-    store_chunk(smem, 1.f);
-    load_chunk(min(1, n_chunks - 1));
+  using S0 = std::integral_constant<int, 0>;
+  if constexpr (DB) {
+    load_chunk(S0{}, 0);
+    store_chunk(S0{}, smem, 1.f);
+    load_chunk(S0{}, min(1, n_chunks - 1));
     __syncthreads();
     for (int kc = 0; kc < n_chunks; ++kc) {
       const char* cur = smem + (kc & 1) * STAGE;
       char* nxt = smem + ((kc + 1) & 1) * STAGE;
       kstep(cur, 0);
-      store_chunk(nxt, kc + 1 < n_chunks ? 1.f : 0.f);
-      load_chunk(min(kc + 2, n_chunks - 1));
+      store_chunk(S0{}, nxt, kc + 1 < n_chunks ? 1.f : 0.f);
+      load_chunk(S0{}, min(kc + 2, n_chunks - 1));
       kstep(cur, 1);
       __syncthreads();
     }
-  } else {
+  } else if constexpr (PD == 1) {
     // single stage, two barriers per chunk, register prefetch of the next chunk under the MFMAs;
     // two workgroups per CU overlap one's staging / epilogue with the other's MFMAs
-    load_chunk(0);
+    load_chunk(S0{}, 0);
     for (int kc = 0; kc < n_chunks; ++kc) {
       __syncthreads();
-      store_chunk(smem, 1.f);
+      store_chunk(S0{}, smem, 1.f);
       __syncthreads();
-      load_chunk(min(kc + 1, n_chunks - 1));
+      load_chunk(S0{}, min(kc + 1, n_chunks - 1));
       kstep(smem, 0);
       kstep(smem, 1);
+    }
+  } else {
+    // PD register sets: the loop is unrolled by PD so every set is addressed at compile time; chunk kc's set
+    // is refilled with chunk kc + PD right after it is staged (past the end: clamped repeats, never staged)
+    Unroll<0, PD>::run([&](auto S) { load_chunk(S, min((int)decltype(S)::value, n_chunks - 1)); });
+    for (int kc0 = 0; kc0 < n_chunks; kc0 += PD) {
+      Unroll<0, PD>::run([&](auto S) {
+        const int kc = kc0 + decltype(S)::value;
+        if (kc < n_chunks) {
+          __syncthreads();
+          store_chunk(S, smem, 1.f);
+          __syncthreads();
+          load_chunk(S, min(kc + PD, n_chunks - 1));
+          kstep(smem, 0);
+          kstep(smem, 1);
+        }
+      });
     }
   }
 
@@ -1408,7 +1431,23 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
     SESA_REQUIRE(!a.a_hi, SESA_ERR_INVALID, "tok_gemm conv: pre-split A is for token rows");
     // SESA_HCONV_VARIANT=1: the double-buffered 512-thread 256 x 128 tile for the implicit-GEMM convs (A/B)
     static const int hv = getenv("SESA_HCONV_VARIANT") ? atoi(getenv("SESA_HCONV_VARIANT")) : 0;
-    if (x3 == 2) {
+    // SESA_HCONV_PD = 1 | 2 | 3: register prefetch depth of the fp16 conv gathers (A/B)
+    static const int pd = getenv("SESA_HCONV_PD") ? atoi(getenv("SESA_HCONV_PD")) : 1;
+    if (x3 == 2 && pd == 2) {
+      if (a.bn64)
+        hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 1, false, true, false, 64, true, 2>), grid, dim3(256),
+                           0, st, a);
+      else
+        hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true, false, 128, true, 2>), grid,
+                           dim3(256), 0, st, a);
+    } else if (x3 == 2 && pd == 3) {
+      if (a.bn64)
+        hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 1, false, true, false, 64, true, 3>), grid, dim3(256),
+                           0, st, a);
+      else
+        hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true, false, 128, true, 3>), grid,
+                           dim3(256), 0, st, a);
+    } else if (x3 == 2) {
       // fp16 single pass (fp16 weight images): 64- or 128-column tiles
       if (a.bn64)
         hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 1, false, true, false, 64, true>), grid, dim3(256), 0,
@@ -1460,8 +1499,10 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
       const int d = getenv("SESA_TOKGEMM_DEPTH") ? atoi(getenv("SESA_TOKGEMM_DEPTH")) : 3;
       return d == 3 || d == 4 ? d : 2;
     }();
-    // SESA_TOKGEMM_HT=1: the half tile (256 x 128, 256 threads, two workgroups per CU) on a depth-3 ring
-    static const bool ht = getenv("SESA_TOKGEMM_HT") && std::string(getenv("SESA_TOKGEMM_HT")) == "1";
+    // the half tile (256 x 128, 256 threads, two workgroups per CU) on a depth-3 ring, by default: same box,
+    // BS-Roformer 193.0 / 193.0x -> 195.3 / 194.8x, and 190.3 / 190.3x -> 195.0 / 195.7x with the LDS-staged FF1
+    // output (profiles/r04_bsr_halftile_ab_*.json, r04_bsr_ff1stage_ab_*.json); SESA_TOKGEMM_HT=0: 256 x 256
+    static const bool ht = !(getenv("SESA_TOKGEMM_HT") && std::string(getenv("SESA_TOKGEMM_HT")) == "0");
     const dim3 ght((unsigned)(((a.M + 255) / 256) * a.n_tiles_n), (unsigned)a.n_groups);
 #define SESA_GLDS16(EPV)                                                                                   \
   if (m16 && ht) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 3, true>), ght, dim3(256), 0, st, a);    \
