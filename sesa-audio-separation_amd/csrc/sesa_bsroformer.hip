@@ -755,6 +755,10 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
   const bool qp = qkv_planes && !f16 && m->qkv_ld % 8 == 0 && c.dim_head % 8 == 0;
   uint16_t* QKVhi = reinterpret_cast<uint16_t*>(QKV);
   uint16_t* QKVlo = x3 ? QKVhi + (int64_t)M * m->qkv_ld : nullptr;
+  // fp16: the QKV epilogue writes q / k / v / gate logits as one fp16 plane (the rounding the fp16 attention
+  // applies on load, at half the bytes written and read); SESA_BSR_QKV16=0: fp32 rows (A/B)
+  static const bool qkv16_on = !(getenv("SESA_BSR_QKV16") && std::string(getenv("SESA_BSR_QKV16")) == "0");
+  const bool q16 = f16 && qkv16_on && m->qkv_ld % 4 == 0 && c.dim_head % 8 == 0 && m->inner % 4 == 0;
   for (size_t li = 0; li < m->layers.size(); ++li) {
     const Layer& L = m->layers[li];
     // attention: QKV + gates (RMSNorm, rotary on q/k)
@@ -772,6 +776,7 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
         a.out_hi = QKVhi;
         a.out_lo = QKVlo;
       }
+      if (q16) a.out_hi = QKVhi;   // one fp16 plane (EP_F16 | EP_ROPE | EP_SPLIT)
       gemm(a, L.qkv, M, f16);
     }
     if (rc) return rc;
@@ -791,6 +796,7 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
         a.qkv_hi = QKVhi;
         a.qkv_lo = QKVlo;
       }
+      if (q16) a.qkv16 = QKVhi;
       a.heads = c.heads;
       if (L.time) {  // sequences (b, band) over t
         a.L = T;

@@ -438,9 +438,11 @@ __global__ void __launch_bounds__(kT) htd_layernorm_kernel(const float* __restri
                                                            int64_t rows, int D, const float* __restrict__ g,
                                                            const float* __restrict__ be,
                                                            const float* __restrict__ tab, int n_tok,
-                                                           uint16_t* __restrict__ ohi, uint16_t* __restrict__ olo) {
+                                                           uint16_t* __restrict__ ohi, uint16_t* __restrict__ olo,
+                                                           int f16 = 0) {
   // ohi (nullable): write the normalised rows as bf16 hi / lo planes [rows][D] instead of fp32 `out` --
-  // the pre-split A operand of the following token GEMM (tok_gemm_glds_kernel); olo null for bf16
+  // the pre-split A operand of the following token GEMM (tok_gemm_glds_kernel); olo null for bf16;
+  // f16: one fp16 plane (the fp16 Linears of fp16mix)
   const int64_t r = (int64_t)blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int lane = threadIdx.x & 63;
@@ -461,7 +463,9 @@ __global__ void __launch_bounds__(kT) htd_layernorm_kernel(const float* __restri
   for (int i = lane; i < D; i += 64) {
     float o = (x[i] - mean) * rstd * g[i] + be[i];
     if (tr) o += tr[i];
-    if (ohi) {
+    if (ohi && f16) {
+      ohi[r * D + i] = __builtin_bit_cast(uint16_t, (_Float16)o);
+    } else if (ohi) {
       __bf16 hi, lo;
       split_bf16(o, hi, lo);
       ohi[r * D + i] = __builtin_bit_cast(uint16_t, hi);
@@ -929,8 +933,8 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
   std::vector<uint16_t> blob;
   std::vector<float> bias;
   auto single = [&](Gemm& gm, const TokGroup& g) { gm.groups = {g}; };
-  // fp16mix: the conv-family weights (encoder / transposed / DConv / rewrite convs) as fp16 images for the
-  // fp16 single-pass implicit GEMMs; the transformer Linears stay bf16 hi / lo
+  // fp16mix: every GEMM weight (encoder / transposed / DConv / rewrite convs, transformer and channel Linears)
+  // as fp16 images for the fp16 single-pass kernels
   const bool f16w = c.precision == SESA_PREC_F16MIX;
   std::vector<double> f64;
   auto pack_dconv = [&](std::vector<DcLayer>& out, const std::string& p, int C, int h) {
@@ -1066,7 +1070,7 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                      const float w = W[(size_t)(row0 + n) * K_ + k];
                      return scale ? (*scale)[n] * w : w;
                    },
-                   true, [&](int n) { return scale ? (*scale)[n] * Bv[row0 + n] : Bv[row0 + n]; }, blob, bias));
+                   true, [&](int n) { return scale ? (*scale)[n] * Bv[row0 + n] : Bv[row0 + n]; }, blob, bias, f16w));
   };
   const int D = m->D, hid = (int)(m->D * c.t_hidden_scale);
   if (c.bottom_channels) {
@@ -1214,9 +1218,10 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   const float* Wb = m->d_f32;
   const int T = m->T, L = c.chunk_size, ach = m->ach, D = m->D;
   const int hid = (int)(m->D * c.t_hidden_scale);
-  // SESA_PREC_F16MIX: the cross-transformer attention (QK^T, PV) on one fp16 MFMA pass with fp32 softmax
-  // statistics (attn_f16_kernel) and the implicit-GEMM convs + 1x1 rewrites on one fp16 pass (operand rounded
-  // once to fp16, fp16 weight images); the transformer / channel Linears bf16x3
+  // SESA_PREC_F16MIX: every contraction on one fp16 MFMA pass with fp32 accumulation -- the cross-transformer
+  // attention (QK^T, PV; fp32 softmax statistics, attn_f16_kernel), the implicit-GEMM convs + 1x1 rewrites
+  // (operand rounded once to fp16 in the staging) and the transformer / channel Linears (fp16 operand planes from
+  // LayerNorm, the attention and the FF1 epilogue); fp16 weight images throughout
   const bool att16 = c.precision == SESA_PREC_F16MIX;
   const int x3 = c.precision == SESA_PREC_BF16X3 || att16 ? 1 : 0;
   const int cx = att16 ? 2 : x3;   // the implicit-GEMM convs and the 1x1 rewrite: fp16 single pass in fp16mix
@@ -1333,7 +1338,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     a.M = (int)M;
     a.act = act;
     void* t0 = profile_begin(st);
-    rc = launch_tok_gemm(a, x3, st);
+    rc = launch_tok_gemm(a, cx, st);   // (fp16mix: fp32 rows rounded to fp16 in the staging)
     profile_end(t0, st, kclass, gemm_flops(gm, M));
   };
   // 1x1 rewrite + GLU (:114-118 of HEncLayer): the plain token GEMM (2 % faster end to end than the
@@ -1507,13 +1512,15 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     // per N tile.  SESA_HTD_PRESPLIT=0: the fp32 path (A/B).
     static const bool presplit = !(getenv("SESA_HTD_PRESPLIT") && std::string(getenv("SESA_HTD_PRESPLIT")) == "0");
     const bool ps = presplit && x3 && D % 8 == 0 && hid % 8 == 0;
+    const bool l16 = ps && att16;   // fp16 operand planes (one plane, no lo) for the fp16 Linears
     auto hi_of = [&](float* buf) { return reinterpret_cast<uint16_t*>(buf); };
     auto lo_of = [&](float* buf, int64_t n) { return reinterpret_cast<uint16_t*>(buf) + n; };
     // LayerNorm -> planes of `o` (rows x D)
     auto lnp = [&](const float* in, float* o, int64_t rows, int64_t g, int64_t b) {
       if (!ps) return ln(in, o, rows, g, b, nullptr, 1);
       hipLaunchKernelGGL(htd_layernorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(kT), 0, st, in, o, rows, D,
-                         Wb + g, Wb + b, (const float*)nullptr, 1, hi_of(o), lo_of(o, rows * D));
+                         Wb + g, Wb + b, (const float*)nullptr, 1, hi_of(o), l16 ? nullptr : lo_of(o, rows * D),
+                         (int)l16);
     };
     // Linear with a pre-split A (planes of `xin`, rows x K = x_ld); optional split output (planes of o)
     auto plin = [&](const Gemm& gm, float* xin, int64_t x_ld, float* o, int64_t o_ld, int64_t M, int act,
@@ -1523,11 +1530,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       TokGemmArgs a{};
       a.x = nullptr;
       a.a_hi = hi_of(xin);
-      a.a_lo = lo_of(xin, M * x_ld);
+      a.a_lo = l16 ? nullptr : lo_of(xin, M * x_ld);
       a.a_ld = x_ld;
       a.out = split_out ? nullptr : o;
       a.out_hi = split_out ? hi_of(o) : nullptr;
-      a.out_lo = split_out ? lo_of(o, M * o_ld) : nullptr;
+      a.out_lo = split_out && !l16 ? lo_of(o, M * o_ld) : nullptr;
       a.o_ld = o_ld;
       a.residual = residual;
       a.w = m->d_w;
@@ -1540,7 +1547,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       a.M = (int)M;
       a.act = act;
       void* t0 = profile_begin(st);
-      rc = launch_tok_gemm(a, x3, st);
+      rc = launch_tok_gemm(a, l16 ? 2 : x3, st);
       profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(gm, M));
     };
     {
@@ -1576,7 +1583,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       a.dh = dh;
       if (ps) {                // planes for the following out-projection's pre-split A
         a.out_hi = hi_of(o);
-        a.out_lo = lo_of(o, (int64_t)B * Lq * D);
+        a.out_lo = l16 ? nullptr : lo_of(o, (int64_t)B * Lq * D);
+        a.out_f16 = l16;       // fp16mix: one fp16 plane, the fp16 out-projection's A
       }
       if (ps && !att16) {      // q / k / v from the planes the projection GEMMs wrote (plin split_out)
         a.qkv_hi = hi_of(const_cast<float*>(q));

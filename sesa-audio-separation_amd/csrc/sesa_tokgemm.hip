@@ -1177,7 +1177,9 @@ __device__ __forceinline__ uint32_t pack2h_(float a, float b) {
 
 // NW: waves per workgroup (32 queries each): 4 (128 queries) for long sequences, 2 (64 queries) where L <= 64
 // (BS-Roformer's band attention, L = 62: a 128-query tile would compute half of its MFMAs on padding).
-template <int NW>
+// H16: q / k / v / gates from the fp16 plane a.qkv16 (the rounding the fp32 path does here, done by the QKV
+// epilogue; the gate logit is the fp16-rounded one)
+template <int NW, bool H16 = false>
 __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
   constexpr int NTH = NW * 64, QB = NW * 32, NIT = kKB * 16 / NTH;   // staging items per thread
   constexpr int IMG = kKB * kHD * 2;                      // one fp16 [64 key][64 d] image
@@ -1199,7 +1201,24 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
   const bool q_ok = q_pos < a.L;
 
   bf16x8 qf[4];   // fp16 bits: Q[q][16 ks + 8 hl + j] / sqrt(dh)
-  {
+  if constexpr (H16) {
+    const uint16_t* qp = a.qkv16 + token(q_ok ? q_pos : 0) * a.ld + head * dh;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int d0 = 16 * ks + 8 * hl;
+      u32x4 w = {0u, 0u, 0u, 0u};
+      if (q_ok && d0 < dh) {
+        const u32x4 raw = *reinterpret_cast<const u32x4*>(qp + d0);   // dh % 8 == 0 (host check)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw[e] & 0xffffu));
+          const float hi = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw[e] >> 16));
+          w[e] = pack2h_(lo * qscale, hi * qscale);
+        }
+      }
+      qf[ks] = __builtin_bit_cast(bf16x8, w);
+    }
+  } else {
     const float* qp = a.qkv + token(q_ok ? q_pos : 0) * a.ld + head * dh;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -1218,7 +1237,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
     for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  f32x4 kreg[NIT], vreg[NIT];
+  f32x4 kreg[H16 ? 1 : NIT], vreg[H16 ? 1 : NIT];
+  uint2 kreg16[H16 ? NIT : 1], vreg16[H16 ? NIT : 1];   // H16: 4 fp16 per item, stored as loaded
   auto load_block = [&](int kb) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
@@ -1226,9 +1246,15 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
       const int key = e >> 4, dq = (e & 15) * 4;
       const int p = kb * kKB + key;
       const bool ok = p < Lk && dq < dh;
-      const float* row = kvb + ktoken(ok ? p : 0) * kv_ld + head * dh + (ok ? dq : 0);
-      kreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.k_off) : f32x4{0.f, 0.f, 0.f, 0.f};
-      vreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.v_off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (H16) {
+        const uint16_t* row = a.qkv16 + token(ok ? p : 0) * a.ld + head * dh + (ok ? dq : 0);
+        kreg16[i] = ok ? *reinterpret_cast<const uint2*>(row + a.k_off) : make_uint2(0u, 0u);
+        vreg16[i] = ok ? *reinterpret_cast<const uint2*>(row + a.v_off) : make_uint2(0u, 0u);
+      } else {
+        const float* row = kvb + ktoken(ok ? p : 0) * kv_ld + head * dh + (ok ? dq : 0);
+        kreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.k_off) : f32x4{0.f, 0.f, 0.f, 0.f};
+        vreg[i] = ok ? *reinterpret_cast<const f32x4*>(row + a.v_off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   };
   auto store_block = [&](char* stg) {
@@ -1237,10 +1263,15 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
       const int e = tid + i * NTH;
       const int key = e >> 4, dq = (e & 15) * 4;
       const int off = swz(key, dq >> 3) + ((dq & 4) << 1);
-      *reinterpret_cast<uint2*>(stg + off) =
-          make_uint2(pack2h_(kreg[i][0], kreg[i][1]), pack2h_(kreg[i][2], kreg[i][3]));
-      *reinterpret_cast<uint2*>(stg + IMG + off) =
-          make_uint2(pack2h_(vreg[i][0], vreg[i][1]), pack2h_(vreg[i][2], vreg[i][3]));
+      if constexpr (H16) {
+        *reinterpret_cast<uint2*>(stg + off) = kreg16[i];
+        *reinterpret_cast<uint2*>(stg + IMG + off) = vreg16[i];
+      } else {
+        *reinterpret_cast<uint2*>(stg + off) =
+            make_uint2(pack2h_(kreg[i][0], kreg[i][1]), pack2h_(kreg[i][2], kreg[i][3]));
+        *reinterpret_cast<uint2*>(stg + IMG + off) =
+            make_uint2(pack2h_(vreg[i][0], vreg[i][1]), pack2h_(vreg[i][2], vreg[i][3]));
+      }
     }
   };
   const int tg = lane >> 4, ti = lane & 15;
@@ -1325,7 +1356,10 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
 
   if (!q_ok) return;
   const int64_t tq = token(q_pos);
-  const float gate = a.g_off >= 0 ? sigmoidf_(a.qkv[tq * a.ld + a.g_off + head]) : 1.f;
+  const float glogit = a.g_off < 0 ? 0.f
+                       : H16 ? (float)__builtin_bit_cast(_Float16, a.qkv16[tq * a.ld + a.g_off + head])
+                             : a.qkv[tq * a.ld + a.g_off + head];
+  const float gate = a.g_off >= 0 ? sigmoidf_(glogit) : 1.f;
   const float scale = gate / l_run;
   const int64_t obase = tq * a.o_ld + head * dh;
 #pragma unroll
@@ -1431,7 +1465,8 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
     SESA_REQUIRE(!a.a_hi, SESA_ERR_INVALID, "tok_gemm conv: pre-split A is for token rows");
     // SESA_HCONV_VARIANT=1: the double-buffered 512-thread 256 x 128 tile for the implicit-GEMM convs (A/B)
     static const int hv = getenv("SESA_HCONV_VARIANT") ? atoi(getenv("SESA_HCONV_VARIANT")) : 0;
-    // SESA_HCONV_PD = 1 | 2 | 3: register prefetch depth of the fp16 conv gathers (A/B)
+    // SESA_HCONV_PD = 1 | 2 | 3: register prefetch depth of the fp16 conv gathers (A/B).  Deeper is slower: same
+    // box, HTDemucs hconv 804 / 802 ms per step (PD 1) -> 938 (2) -> 1052 (3) (profiles/r04_hconv_pd_ab_*.json)
     static const int pd = getenv("SESA_HCONV_PD") ? atoi(getenv("SESA_HCONV_PD")) : 1;
     if (x3 == 2 && pd == 2) {
       if (a.bn64)
@@ -1520,6 +1555,8 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
       case EP_F16 | EP_GELU | EP_SPLIT: SESA_GLDS16(EP_F16 | EP_GELU | EP_SPLIT) break;  // FF1 (A pre-scaled)
       case EP_F16 | EP_RES: SESA_GLDS16(EP_F16 | EP_RES) break;                                         // FF2
       case EP_F16 | EP_ROPE: SESA_GLDS16(EP_F16 | EP_ROPE) break;                       // QKV (A pre-scaled)
+      case EP_F16 | EP_ROPE | EP_SPLIT: SESA_GLDS16(EP_F16 | EP_ROPE | EP_SPLIT) break;   // QKV -> fp16 plane
+      case EP_F16: SESA_GLDS16(EP_F16) break;                                   // HTDemucs q / kv projections
       default: ep = -1;
     }
     SESA_REQUIRE(!f16 || ep >= 0, SESA_ERR_INVALID, "tok_gemm: no fp16 kernel for this epilogue / shape");
@@ -1585,11 +1622,19 @@ int launch_attention(const AttnArgs& a, int x3, hipStream_t st) {
   // x3 == 2: QK^T and PV on one fp16 pass (fp32 QKV rows; SESA_PREC_F16 of BS- / Mel-Band-Roformer)
   SESA_REQUIRE(x3 != 2 || !pre, SESA_ERR_INVALID, "attention: the fp16 kernel reads fp32 q / k / v rows");
   SESA_REQUIRE(!a.out_f16 || (a.out_hi && x3 == 2), SESA_ERR_INVALID, "attention: fp16 output plane from the fp16 kernel");
+  SESA_REQUIRE(!a.qkv16 || (x3 == 2 && !a.kv && (a.dh == 0 || a.dh % 8 == 0) && a.ld % 4 == 0 && a.k_off % 4 == 0 &&
+                            a.v_off % 4 == 0),
+               SESA_ERR_INVALID, "attention: the fp16 q / k / v plane is for fp16 self attention, dh %% 8, 8-B aligned");
   if (x3 == 2) {
-    if (a.L <= 64)
-      hipLaunchKernelGGL(attn_f16_kernel<2>, dim3((unsigned)((a.L + 63) / 64), (unsigned)a.heads, (unsigned)a.n_seq),
-                         dim3(128), 0, st, a);
-    else hipLaunchKernelGGL(attn_f16_kernel<4>, grid, dim3(kThreads), 0, st, a);
+    const dim3 g64((unsigned)((a.L + 63) / 64), (unsigned)a.heads, (unsigned)a.n_seq);
+    if (a.qkv16) {
+      if (a.L <= 64) hipLaunchKernelGGL((attn_f16_kernel<2, true>), g64, dim3(128), 0, st, a);
+      else hipLaunchKernelGGL((attn_f16_kernel<4, true>), grid, dim3(kThreads), 0, st, a);
+    } else if (a.L <= 64) {
+      hipLaunchKernelGGL(attn_f16_kernel<2>, g64, dim3(128), 0, st, a);
+    } else {
+      hipLaunchKernelGGL(attn_f16_kernel<4>, grid, dim3(kThreads), 0, st, a);
+    }
   } else if (pre) {
     if (x3) hipLaunchKernelGGL((attn_kernel<true, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((attn_kernel<false, true>), grid, dim3(kThreads), 0, st, a);

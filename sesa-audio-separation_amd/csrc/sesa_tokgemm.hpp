@@ -117,6 +117,10 @@ struct AttnArgs {
   const uint16_t* kv_hi;
   const uint16_t* kv_lo;
   int out_f16;                // with out_hi: one fp16 plane (the fp16 kernel, x3 == 2; the fp16 out-projection's A)
+  // nullable (fp16 kernel, self attention): q / k / v / gate logits as ONE fp16 plane written by the fp16 QKV
+  // GEMM's split epilogue (same stride and column offsets as qkv): the values the kernel would round to fp16
+  // itself, at half the bytes
+  const uint16_t* qkv16;
 };
 
 
