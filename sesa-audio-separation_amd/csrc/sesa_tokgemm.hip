@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
   __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE];
   __shared__ float rs[BM];
   __shared__ int orow_base[CONV ? BM : 1], orow_i1[CONV ? BM : 1];  // transposed-conv output rows
+  __shared__ int tap_d1[CONV ? kMaxTaps : 1], tap_d2[CONV ? kMaxTaps : 1];   // CONV: tap offsets (LDS copy)
 
   const TokGroup g = a.groups[blockIdx.y];
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
@@ -129,8 +130,8 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
   const float* xrow[AI];
   int64_t prow[PRE ? AI : 1];                             // plane element offset of the row
   bool rok[AI];
-  // CONV: per-row input grid origin (b Q1, i1 s1, i2 s2) and per-chunk validity
-  int rb1[CONV ? AI : 1], ri1[CONV ? AI : 1], ri2[CONV ? AI : 1];
+  // CONV: per-row input grid origin (b Q1, i1 s1, i2 s2), its input position index, and per-chunk validity
+  int rb1[CONV ? AI : 1], ri1[CONV ? AI : 1], ri2[CONV ? AI : 1], rpos0[CONV ? AI : 1];
   bool aval[PD][CONV ? AI : 1];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
@@ -146,10 +147,22 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
       rb1[i] = b * a.geo.Q1;
       ri1[i] = i1 * a.geo.s1;
       ri2[i] = i2 * a.geo.s2;
+      rpos0[i] = (rb1[i] + ri1[i]) * a.geo.Q2 + ri2[i];   // input position of tap offset (0, 0)
       for (int s = 0; s < PD; ++s) aval[s][i] = false;
     }
   }
   bool kok[PD];
+  // CONV: this thread's k quad as (tap, channel), advanced incrementally (no division per chunk); the tap
+  // offsets come from an LDS copy of the geometry (a per-lane index into the kernel arguments is a memory
+  // round trip per chunk)
+  int k_cur = 0, tap_s = 0, c_s = 0;
+  if constexpr (CONV) {
+    for (int t = tid; t < a.geo.n_taps; t += NT) {
+      tap_d1[t] = a.geo.d1[t];
+      tap_d2[t] = a.geo.d2[t];
+    }
+    __syncthreads();
+  }
   constexpr int W16 = (X3 ? 2 : 1) * W_BYTES / 16;
   constexpr int W_ITEMS = (W16 + NT - 1) / NT;
   u32x4 wreg[PD][W_ITEMS];
@@ -172,14 +185,22 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
     kok[s] = k < g.K;  // K % 4 == 0 (host check): a quad is wholly in or out
     const int kc_ = kok[s] ? k : 0;
     if constexpr (CONV) {
-      // Cin % 4 == 0 (host check): a quad lies inside one tap
-      const int tap = kc_ / a.geo.Cin, c = kc_ - tap * a.geo.Cin;
-      const int d1 = a.geo.d1[tap], d2 = a.geo.d2[tap];
+      // Cin % 4 == 0 (host check): a quad lies inside one tap.  k advances monotonically (0, 32, 64, ... plus
+      // clamped repeats of the last chunk)
+      c_s += k - k_cur;
+      k_cur = k;
+      while (c_s >= a.geo.Cin) {
+        c_s -= a.geo.Cin;
+        ++tap_s;
+      }
+      const int tap = min(tap_s, a.geo.n_taps - 1), c = c_s;
+      const int d1 = tap_d1[tap], d2 = tap_d2[tap];
+      const int dpos = d1 * a.geo.Q2 + d2;
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const int j1 = ri1[i] + d1, j2 = ri2[i] + d2;
-        aval[s][i] = rok[i] && kok[s] && j1 >= 0 && j1 < a.geo.Q1 && j2 >= 0 && j2 < a.geo.Q2;
-        const int64_t off = aval[s][i] ? ((int64_t)(rb1[i] + j1) * a.geo.Q2 + j2) * a.x_ld + g.x_off + c : 0;
+        aval[s][i] = rok[i] && kok[s] && (unsigned)j1 < (unsigned)a.geo.Q1 && (unsigned)j2 < (unsigned)a.geo.Q2;
+        const int64_t off = aval[s][i] ? (int64_t)(rpos0[i] + dpos) * a.x_ld + g.x_off + c : 0;
         areg[s][i] = *reinterpret_cast<const f32x4*>(a.x + off);
         if (a.geo.x2) a2reg[s][i] = *reinterpret_cast<const f32x4*>(a.geo.x2 + off);
       }
@@ -227,7 +248,7 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
         if constexpr (CONV) {
           if (a.geo.x2 && ok) v += a2reg[s][i][q];
         }
-        ss[i] = fmaf(v * count, v, ss[i]);
+        if constexpr (!CONV) ss[i] = fmaf(v * count, v, ss[i]);
         if constexpr (F16) areg[s][i][q] = v;   // (the fp16 pack below reads the final values)
         else split_bf16(v, hi[q], lo[q]);
       }
@@ -1507,7 +1528,7 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
       hipLaunchKernelGGL((tok_gemm_kernel<false, 256, 128, 2, 2, 2, false, true, false>), grid, dim3(256), 0, st, a);
     }
   } else if (a.a_hi) {
-    SESA_REQUIRE(a.a_ld % 4 == 0 && (!x3 || a.a_lo) && (!a.rownorm || a.row_scale), SESA_ERR_INVALID,
+    SESA_REQUIRE(a.a_ld % 4 == 0 && (x3 != 1 || a.a_lo) && (!a.rownorm || a.row_scale), SESA_ERR_INVALID,
                  "tok_gemm: pre-split A needs a_ld %% 4 == 0, the lo plane for bf16x3, row_scale for rownorm");
     // LDS-DMA kernel for the bf16x3 transformer Linears (every group's K % 8 == 0, epilogue one of
     // the specialised forms); SESA_TOKGEMM_GLDS=0 selects the register-staged kernel for A/B runs
