@@ -27,6 +27,7 @@ from oracle.weights import synth_state_dict  # noqa: E402
 
 torch.set_num_threads(os.cpu_count())
 CFG = yaml.safe_load(open(REPO + "/sesa-audio-separation_amd/sesa/configs/config_vocals_mdx23c.yaml"))
+OTHER = set(filter(None, os.environ.get("OTHER", "").split(",")))
 FIXTURES = ["mdx23c_full_chunk.npz", "mdx23c_full_sines.npz", "mdx23c_full_loud.npz", "mdx23c_full_wseed2.npz"]
 
 
@@ -56,6 +57,14 @@ def make(per_conv, tdf=None):
     ns.linear = linear
 
     def conv2d(inp, w, *a, **k):
+        # OTHER (env, comma list): also round these operands to fp16 -- down (2x2 s2 downscale), sc (fused 1x1
+        # shortcuts, every level), c33 (3x3 convs of the T < 32 levels)
+        if w.shape[-1] == 2 and "down" in OTHER:
+            return F.conv2d(f16(inp), f16(w), *a, **k)
+        if w.shape[-1] == 1 and w.shape[0] != w.shape[1] and "sc" in OTHER and inp.shape[1] > 4:
+            return F.conv2d(f16(inp), f16(w), *a, **k)
+        if w.shape[-1] == 3 and inp.shape[2] < 32 and "c33" in OTHER:
+            return F.conv2d(f16(inp), f16(w), *a, **k)
         if w.shape[-1] == 3 and inp.shape[2] >= 32:
             m = per_conv[idx[0]]
             idx[0] += 1
@@ -68,6 +77,13 @@ def make(per_conv, tdf=None):
         return F.conv2d(inp, w, *a, **k)
 
     ns.conv2d = conv2d
+
+    def conv_transpose2d(inp, w, *a, **k):
+        if "up" in OTHER:
+            return F.conv_transpose2d(f16(inp), f16(w), *a, **k)
+        return F.conv_transpose2d(inp, w, *a, **k)
+
+    ns.conv_transpose2d = conv_transpose2d
     return ns, idx
 
 
