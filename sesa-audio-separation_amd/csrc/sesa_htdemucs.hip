@@ -1586,6 +1586,10 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         a.out_lo = l16 ? nullptr : lo_of(o, (int64_t)B * Lq * D);
         a.out_f16 = l16;       // fp16mix: one fp16 plane, the fp16 out-projection's A
       }
+      if (l16) {               // fp16mix: q / k / v as the fp16 planes the projection GEMMs wrote
+        a.qkv16 = hi_of(const_cast<float*>(q));
+        if (kv) a.kv16 = hi_of(const_cast<float*>(kv));
+      }
       if (ps && !att16) {      // q / k / v from the planes the projection GEMMs wrote (plin split_out)
         a.qkv_hi = hi_of(const_cast<float*>(q));
         a.qkv_lo = lo_of(const_cast<float*>(q), (int64_t)B * Lq * q_ld);
@@ -1629,8 +1633,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       if (!Lx.cross) {  // MyTransformerEncoderLayer (norm_first): x += g1 SA(n1(x)); x += g2 FF(n2(x)); norm_out
         lnp(X, Hx, Mx, Lx.n1g, Lx.n1b);
         lnp(XT, Ht, Mt, Lt.n1g, Lt.n1b);
-        plin(Lx.qkv, Hx, D, Qx, 3 * D, Mx, TOK_ACT_NONE, nullptr, !att16);
-        plin(Lt.qkv, Ht, D, Qt, 3 * D, Mt, TOK_ACT_NONE, nullptr, !att16);
+        plin(Lx.qkv, Hx, D, Qx, 3 * D, Mx, TOK_ACT_NONE, nullptr, !att16 || l16);
+        plin(Lt.qkv, Ht, D, Qt, 3 * D, Mt, TOK_ACT_NONE, nullptr, !att16 || l16);
         attn(Qx, 3 * D, nullptr, 0, D, 2 * D, Ax, m->Nx, m->Nx);
         attn(Qt, 3 * D, nullptr, 0, D, 2 * D, At, m->Nt, m->Nt);
         plin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, false);
@@ -1644,10 +1648,10 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         lnp(X, Hx2, Mx, Lt.n2g, Lt.n2b);     // keys / values of xt's layer (from old x)
         float* KVt = Qx + (size_t)Mx * D;    // [Mx][2D]: xt-layer keys / values (from x)
         float* KVx = Qt + (size_t)Mt * D;    // [Mt][2D]: x-layer keys / values (from xt)
-        plin(Lx.q, Hx, D, Qx, D, Mx, TOK_ACT_NONE, nullptr, !att16);
-        plin(Lx.kv, Ht2, D, KVx, 2 * D, Mt, TOK_ACT_NONE, nullptr, !att16);
-        plin(Lt.q, Ht, D, Qt, D, Mt, TOK_ACT_NONE, nullptr, !att16);
-        plin(Lt.kv, Hx2, D, KVt, 2 * D, Mx, TOK_ACT_NONE, nullptr, !att16);
+        plin(Lx.q, Hx, D, Qx, D, Mx, TOK_ACT_NONE, nullptr, !att16 || l16);
+        plin(Lx.kv, Ht2, D, KVx, 2 * D, Mt, TOK_ACT_NONE, nullptr, !att16 || l16);
+        plin(Lt.q, Ht, D, Qt, D, Mt, TOK_ACT_NONE, nullptr, !att16 || l16);
+        plin(Lt.kv, Hx2, D, KVt, 2 * D, Mx, TOK_ACT_NONE, nullptr, !att16 || l16);
         attn(Qx, D, KVx, 2 * D, 0, D, Ax, m->Nx, m->Nt);
         attn(Qt, D, KVt, 2 * D, 0, D, At, m->Nt, m->Nx);
         plin(Lx.out, Ax, D, X, D, Mx, TOK_ACT_NONE, X, false);

@@ -1268,7 +1268,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
       const int p = kb * kKB + key;
       const bool ok = p < Lk && dq < dh;
       if constexpr (H16) {
-        const uint16_t* row = a.qkv16 + token(ok ? p : 0) * a.ld + head * dh + (ok ? dq : 0);
+        const uint16_t* row = (a.kv16 ? a.kv16 + ktoken(ok ? p : 0) * kv_ld : a.qkv16 + token(ok ? p : 0) * a.ld) +
+                              head * dh + (ok ? dq : 0);
         kreg16[i] = ok ? *reinterpret_cast<const uint2*>(row + a.k_off) : make_uint2(0u, 0u);
         vreg16[i] = ok ? *reinterpret_cast<const uint2*>(row + a.v_off) : make_uint2(0u, 0u);
       } else {
@@ -1577,7 +1578,8 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
       case EP_F16 | EP_RES: SESA_GLDS16(EP_F16 | EP_RES) break;                                         // FF2
       case EP_F16 | EP_ROPE: SESA_GLDS16(EP_F16 | EP_ROPE) break;                       // QKV (A pre-scaled)
       case EP_F16 | EP_ROPE | EP_SPLIT: SESA_GLDS16(EP_F16 | EP_ROPE | EP_SPLIT) break;   // QKV -> fp16 plane
-      case EP_F16: SESA_GLDS16(EP_F16) break;                                   // HTDemucs q / kv projections
+      case EP_F16: SESA_GLDS16(EP_F16) break;                                   // fp32 rows out
+      case EP_F16 | EP_SPLIT: SESA_GLDS16(EP_F16 | EP_SPLIT) break;             // HTDemucs q / kv -> fp16 planes
       default: ep = -1;
     }
     SESA_REQUIRE(!f16 || ep >= 0, SESA_ERR_INVALID, "tok_gemm: no fp16 kernel for this epilogue / shape");
@@ -1643,9 +1645,10 @@ int launch_attention(const AttnArgs& a, int x3, hipStream_t st) {
   // x3 == 2: QK^T and PV on one fp16 pass (fp32 QKV rows; SESA_PREC_F16 of BS- / Mel-Band-Roformer)
   SESA_REQUIRE(x3 != 2 || !pre, SESA_ERR_INVALID, "attention: the fp16 kernel reads fp32 q / k / v rows");
   SESA_REQUIRE(!a.out_f16 || (a.out_hi && x3 == 2), SESA_ERR_INVALID, "attention: fp16 output plane from the fp16 kernel");
-  SESA_REQUIRE(!a.qkv16 || (x3 == 2 && !a.kv && (a.dh == 0 || a.dh % 8 == 0) && a.ld % 4 == 0 && a.k_off % 4 == 0 &&
-                            a.v_off % 4 == 0),
-               SESA_ERR_INVALID, "attention: the fp16 q / k / v plane is for fp16 self attention, dh %% 8, 8-B aligned");
+  SESA_REQUIRE(!a.qkv16 || (x3 == 2 && (!a.kv || (a.kv16 && a.kv_ld % 4 == 0)) && (a.dh == 0 || a.dh % 8 == 0) &&
+                            a.ld % 4 == 0 && a.k_off % 4 == 0 && a.v_off % 4 == 0),
+               SESA_ERR_INVALID, "attention: fp16 q / k / v planes (fp16 kernel; cross attention needs kv16), dh %% 8, "
+               "8-B aligned");
   if (x3 == 2) {
     const dim3 g64((unsigned)((a.L + 63) / 64), (unsigned)a.heads, (unsigned)a.n_seq);
     if (a.qkv16) {

@@ -121,6 +121,7 @@ struct AttnArgs {
   // GEMM's split epilogue (same stride and column offsets as qkv): the values the kernel would round to fp16
   // itself, at half the bytes
   const uint16_t* qkv16;
+  const uint16_t* kv16;       // nullable (cross attention with qkv16): k / v as one fp16 plane (kv's layout)
 };
 
 

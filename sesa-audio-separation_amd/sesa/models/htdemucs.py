@@ -36,6 +36,7 @@ class HTDemucs(NativeModule):
     # fp16mix: the cross-transformer attention (fp32 softmax statistics), the implicit-GEMM convs and the 1x1
     # rewrites on one fp16 MFMA pass; the transformer / channel Linears bf16x3
     _precisions = ("bf16x3", "bf16", "fp16mix")
+    _amp_precision = "fp16mix"  # --enable_amp (the reference's AMP is fp16 autocast): 5.9e-6 full segment
 
     def __init__(self, sources, audio_channels=2, samplerate=44100, segment=10, precision="bf16x3", **kw):
         super().__init__(precision)

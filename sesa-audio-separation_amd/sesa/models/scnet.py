@@ -23,6 +23,7 @@ class SCNet(NativeModule):
     # fp16mix: the token GEMMs (3x3 convs, LSTM input projections, dual-path Linears) on one fp16 MFMA pass;
     # the LSTM recurrence bf16x3, the VALU kernels fp32
     _precisions = ("bf16x3", "bf16", "fp16mix")
+    _amp_precision = "fp16mix"  # --enable_amp (the reference's AMP is fp16 autocast): 9.7e-6 full chunk
 
     def __init__(self, sources=("drums", "bass", "other", "vocals"), audio_channels=2, dims=(4, 32, 64, 128),
                  nfft=4096, hop_size=1024, win_size=4096, normalized=True, band_SR=(0.175, 0.392, 0.433),
