@@ -349,9 +349,10 @@ char g_f16_plan[17] = {0};
 
 // The TDF Linears' plan for SESA_PREC_F16MIX, same layout, digits '1' (fp16) / '3' (bf16x3); only Linears the
 // LDS-DMA kernel takes (tdf_dma_eligible) go fp16.  Default from the emulation's per-stack scan on the 0.3-RMS
-// golden with the conv plan above: the decoder stacks in fp16 add 2.7e-6 (5.235 -> 5.262e-5), the encoder
-// level-1 stack alone 6.1e-5.
-constexpr char kTdfPlanDefault[17] = "3333311111111111";
+// golden with the conv plan above: the decoder stacks in fp16 add 2.7e-6 (5.235 -> 5.262e-5), encoder level 0
+// 1.05e-5, levels 1 / 2 / 3 6.1 / 3.0 / 1.8e-5 (kept bf16x3).  Measured: encoder level 0 in fp16 too, worst
+// fixture 5.25 -> 5.50e-5, same box 267.2 / 267.1x -> 270.6 / 270.5x (profiles/r04_tdf0_ab_*.json).
+constexpr char kTdfPlanDefault[17] = "1333111111111111";
 char g_tdf_plan[17] = {0};
 
 bool tdf_plan_f16(int precision, bool enc, int level) {
@@ -646,7 +647,9 @@ struct Fwd {
       Tensor upt{buf((int64_t)B * L.T * L.F * L.c), stats(L.c), L.c};
       // Upscale: GEMM over the level-(l+1) positions, N = 4*c_l, scattered to 2x2 outputs
       const size_t mark = off;
-      conv(m->up[i], act(xt, Tensor{}, &m->up_norm[i], L1.T, L1.F), L1.T, L1.F, L1.T, L1.F, upt.p, nullptr, upt.st, 0);
+      conv(m->up[i],
+           m->up[i].f16 ? act16(xt, Tensor{}, &m->up_norm[i], L1.T, L1.F) : act(xt, Tensor{}, &m->up_norm[i], L1.T, L1.F),
+           L1.T, L1.F, L1.T, L1.F, upt.p, nullptr, upt.st, 0);
       off = mark;
       xt = stack(m->dec[i], upt, skips[l], L);
     }
@@ -806,7 +809,12 @@ extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
     pack_norm(m, m->down_norm[i], aff);
   }
   pstack(m->bottleneck, true, (int)m->enc.size());
+  // fp16mix: the transposed 2x2 up-convs on one fp16 pass too (emulated on the 0.3-RMS fixture: 5.26 ->
+  // 5.30e-5); SESA_MDX_UP16=0 keeps them bf16x3 (A/B)
+  static const bool up16 = !(getenv("SESA_MDX_UP16") && std::string(getenv("SESA_MDX_UP16")) == "0");
   for (size_t i = 0; i < m->dec.size(); ++i) {
+    m->up[i].f16 = up16 && m->cfg.precision == SESA_PREC_F16MIX;
+    m->up[i].f16c = 3;
     pc(m->up[i]);
     pack_norm(m, m->up_norm[i], aff);
     pstack(m->dec[i], false, (int)(m->dec.size() - 1 - i));

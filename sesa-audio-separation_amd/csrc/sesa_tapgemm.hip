@@ -126,8 +126,12 @@ __device__ __forceinline__ void transform4(float (&v)[4], int mode, const float*
 // all KH*KW taps, then x_chunks chunks of an optional RAW extra input over the centre tap only --
 // the 1x1 shortcut of TFC_TDF (mdx23c_tfc_tdf_v3.py:126, :132, :137) fused into tfc2's conv as
 // extra K, so `s` never round-trips through HBM.
-template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool X3, bool UPS, bool XTRA, bool PRE>
+// F16 (PRE, no XTRA, X3 = false): the fp16 plane of act_f16 against the fp16 weight image, one
+// v_mfma_f32_32x32x16_f16 pass (the transposed up-convs of MDX23C's fp16mix)
+template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool X3, bool UPS, bool XTRA, bool PRE,
+          bool F16 = false>
 __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
+  static_assert(!F16 || (PRE && !XTRA && !X3), "fp16: a pre-activated fp16 plane, no shortcut");
   constexpr int WN = 4 / WM;
   constexpr int MI = TM / WM;                 // 32-position MFMA row blocks per wave
   constexpr int NI = BN / WN / 32;            // 32-channel MFMA column blocks per wave
@@ -245,7 +249,7 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
         if (ok) {
           const int64_t idx = (((int64_t)b * a.T_in + ti) * a.F_in + fi) * src.C + cl0 + 8 * hf;
           areg[2 * i] = *reinterpret_cast<const f32x4*>(src.hi + idx);
-          areg[2 * i + 1] = *reinterpret_cast<const f32x4*>(src.lo + idx);
+          if constexpr (!F16) areg[2 * i + 1] = *reinterpret_cast<const f32x4*>(src.lo + idx);
         } else {
           areg[2 * i] = f32x4{0.f, 0.f, 0.f, 0.f};
           areg[2 * i + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -345,7 +349,8 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
           acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
           acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
         }
-        acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+        if constexpr (F16) acc[i][j] = mfma32h(ah[i], bh[j], acc[i][j]);
+        else acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
       }
   };
 
@@ -2796,13 +2801,23 @@ __global__ void __launch_bounds__(kThreads) act_split_kernel(GemmIn in, int64_t 
 
 template <int KH, int KW, int S, int PAD, int TM, int BN, int WM, bool UPS, bool XTRA, bool PRE>
 int launch_conv_t(int x3, const ConvArgs& a, int batch, hipStream_t st) {
-  // PRE kernels read only the bf16 planes of the main input
-  SESA_REQUIRE(!PRE || (a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && a.in.src[0].lo && a.in.C_split == a.in.C_in),
+  // PRE kernels read only the bf16 planes of the main input (x3 == 3: the one fp16 plane of act_f16)
+  SESA_REQUIRE(!PRE || (a.in.src[0].mode == SRC_PRE && a.in.src[0].hi && (x3 == 3 || a.in.src[0].lo) &&
+                        a.in.C_split == a.in.C_in),
                SESA_ERR_INVALID, "conv: this kernel needs a single pre-activated (act_split) input");
+  SESA_REQUIRE(x3 != 3 || (PRE && !XTRA), SESA_ERR_INVALID, "conv: fp16 tap kernel takes a pre-activated plane only");
   SESA_REQUIRE(PRE || (a.in.src[0].mode != SRC_PRE && a.in.src[1].mode != SRC_PRE), SESA_ERR_INVALID,
                "conv: pre-activated input given to a transforming kernel");
   dim3 grid((unsigned)(((a.T_out + TM - 1) / TM) * (a.F_out / kTF) * ((a.n_cols + BN - 1) / BN)), 1u,
             (unsigned)batch);
+  if constexpr (PRE && !XTRA) {
+    if (x3 == 3) {
+      hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, false, UPS, XTRA, PRE, true>), grid,
+                         dim3(kThreads), 0, st, a);
+      SESA_CHECK_LAUNCH();
+      return SESA_OK;
+    }
+  }
   if (x3)
     hipLaunchKernelGGL((tap_gemm_kernel<KH, KW, S, PAD, TM, BN, WM, true, UPS, XTRA, PRE>), grid, dim3(kThreads), 0, st, a);
   else
@@ -2932,8 +2947,8 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
   x3 = x3 != 0 ? 1 : 0;
   const bool db3 = kind == CONV3X3 && a.in.src[0].mode != SRC_ACT32 && a.T_out >= 32 && a.out.residual == nullptr &&
                    a.out.gelu == 0 && !conv3x3_m16_selected(a.T_out, a.in.C_in, a.out.C_out, a.x_chunks > 0 ? a.xin.C_in : 0);
-  SESA_REQUIRE(xmode >= 0 && xmode <= 3 && (xmode < 2 || db3), SESA_ERR_INVALID,
-               "conv: fp16 mode %d only for the direct 3x3 kernel", xmode);
+  SESA_REQUIRE(xmode >= 0 && xmode <= 3 && (xmode < 2 || db3 || (xmode == 3 && kind == DECONV2X2S2)), SESA_ERR_INVALID,
+               "conv: fp16 mode %d only for the direct 3x3 kernel and the transposed up-convs", xmode);
   SESA_REQUIRE(a.in.C_in % kConvBK == 0 && a.in.C_split % kConvBK == 0 && a.in.C_in <= kMaxCin, SESA_ERR_INVALID,
                "conv: C_in %d / split %d must be multiples of %d (<= %d)", a.in.C_in, a.in.C_split, kConvBK,
                kMaxCin);
@@ -3058,9 +3073,9 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
     case CONV2X2S2:
       if (bn == 128) return launch_conv_t<2, 2, 2, 0, 4, 128, 4, false, false, true>(x3, a, batch, st);
       return launch_conv_t<2, 2, 2, 0, 4, 64, 4, false, false, true>(x3, a, batch, st);
-    case DECONV2X2S2:
-      if (bn == 128) return launch_conv_t<1, 1, 1, 0, 8, 128, 4, true, false, true>(x3, a, batch, st);
-      return launch_conv_t<1, 1, 1, 0, 8, 64, 4, true, false, true>(x3, a, batch, st);
+    case DECONV2X2S2:   // (xmode 3: the fp16 plane x fp16 image kernel)
+      if (bn == 128) return launch_conv_t<1, 1, 1, 0, 8, 128, 4, true, false, true>(xmode == 3 ? 3 : x3, a, batch, st);
+      return launch_conv_t<1, 1, 1, 0, 8, 64, 4, true, false, true>(xmode == 3 ? 3 : x3, a, batch, st);
   }
   set_error("conv: unknown kind %d", kind);
   return SESA_ERR_INVALID;
