@@ -177,13 +177,21 @@ __global__ void htd_norm_time_kernel(const float* __restrict__ x, int ach, int L
 }
 
 // x[b][f][t][c] += tab[f][c]  (freq_emb after encoder layer 0, :611-616)
+// grid (ceil(T C / 4 / 256), F, B): one float4 per thread along a (b, f) row of T C contiguous floats (C % 4 == 0),
+// 32-bit index math only (the per-element 64-bit div / mod form ran at 2.7 TB/s)
 __global__ void htd_add_rows_kernel(float* __restrict__ X, int F, int T, int C, const float* __restrict__ tab,
                                     int64_t total) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int c = (int)(i % C);
-  const int f = (int)((i / ((int64_t)T * C)) % F);
-  X[i] += tab[(int64_t)f * C + c];
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;   // quad inside the row
+  const int row_quads = T * C / 4;
+  if (q >= row_quads) return;
+  const int f = blockIdx.y;
+  const int c = (4 * q) % C;
+  f32x4* x4 = reinterpret_cast<f32x4*>(X + ((int64_t)blockIdx.z * F + f) * T * C) + q;
+  const f32x4 t4 = *reinterpret_cast<const f32x4*>(tab + (int64_t)f * C + c);
+  f32x4 v = *x4;
+  v += t4;
+  *x4 = v;
+  (void)total;
 }
 
 // ---- DConv (demucs.demucs.DConv restated: per layer x += LayerScale(GLU(GN(conv1x1(GELU(GN(
@@ -409,10 +417,17 @@ __global__ void __launch_bounds__(kT) htd_dc_apply_kernel(DcArgs a) {
     const float ga = a.g2[c] * r2, gg = a.g2[C + c] * r2;   // (v - mean) * (rstd * gamma) + beta
     const float oa = a.be2[c], og = a.be2[C + c];
     const float sc = a.scale[c];
-    for (int q = 0; q < kDcP / 4; ++q) {
+    // the residual rows of all kDcP / 4 positions are loaded up front: X is read and written in place, so
+    // with a load -> store per position the compiler cannot hoist the next position's load above the store
+    // and every position paid a full memory round trip
+    constexpr int NQ = kDcP / 4;
+    float* xrow = a.X + ((int64_t)row * T + t0 + wv) * C + c;
+    float xv[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) xv[q] = t0 + wv + 4 * q < T ? xrow[(int64_t)4 * q * C] : 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
       const int p = wv + 4 * q;
-      const int t = t0 + p;
-      if (t >= T) break;
       float va = ba, vg = bg;
 #pragma unroll
       for (int j4 = 0; j4 < HM; j4 += 4) {
@@ -426,9 +441,11 @@ __global__ void __launch_bounds__(kT) htd_dc_apply_kernel(DcArgs a) {
         va = fmaf(wa[j4 + 3], g.w, va);
         vg = fmaf(wg[j4 + 3], g.w, vg);
       }
-      float* xp = a.X + ((int64_t)row * T + t) * C + c;
-      *xp = *xp + sc * (fmaf(va - m2, ga, oa) * sigm(fmaf(vg - m2, gg, og)));
+      xv[q] = xv[q] + sc * (fmaf(va - m2, ga, oa) * sigm(fmaf(vg - m2, gg, og)));
     }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      if (t0 + wv + 4 * q < T) xrow[(int64_t)4 * q * C] = xv[q];
   }
 }
 
@@ -493,16 +510,24 @@ __global__ void htd_gn_apply_kernel(float* __restrict__ X, int64_t n_item, int D
 // [B][2048][T][Cz] output, channel s * 2 ach + 2 c + (re, im), de-normalised (x * std + mean, :670),
 // Nyquist bin zero (:451); normalized inverse (c2r by_root_n) times the Hann window.
 __global__ void __launch_bounds__(kT) htd_istft_frames_kernel(const float* __restrict__ Z, int T, int Cz, int ach,
-                                                              int nsrc, const double* __restrict__ stats, int64_t n_item,
+                                                              int nsrc, int n_items, const double* __restrict__ stats,
+                                                              int64_t n_item,
                                                               const float* __restrict__ win, Fft2048Tables tb,
                                                               float* __restrict__ fw) {
   __shared__ float2 bufA[kFft2048];
   __shared__ float2 bufB[kFft2048 + 1];
-  // signal-major grid: the nsrc * ach workgroups of one (item, frame) run back to back, so the 64-B channel
-  // groups of Z[b][k][t][:] each fetches (one 128-B line per bin, shared by all of them) hit L2 after the first
-  const int t = blockIdx.y;
-  const int sig = blockIdx.x;
-  const int b = sig / (nsrc * ach), rem = sig - b * nsrc * ach;
+  // XCD-grouped 1-D grid: a 128-B line of Z[b][k][t][:] holds bin k of frames t, t + 1 for all Cz channels,
+  // i.e. of all 2 nsrc ach workgroups of a frame pair; the dispatcher deals ids round-robin over the 8 XCDs, so
+  // those workgroups get ids 8 apart (same XCD, same L2, consecutive in time) and each line is fetched once
+  // per XCD instead of once per workgroup (measured 25 GB of fetch per launch for ~1.5 GB of spectrum).
+  const int nper = nsrc * ach, gsz = 2 * nper;
+  const int Tp = (T + 1) >> 1;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int gi = xcd + 8 * (slot / gsz), j = slot % gsz;
+  const int b = gi / Tp, t = 2 * (gi - b * Tp) + j / nper;
+  if (b >= n_items || t >= T) return;   // (whole workgroup: padding of the grid)
+  const int sig = b * nper + j % nper;
+  const int rem = sig - b * nper;
   const int s = rem / ach, c = rem - s * ach;
   float mean, sd;
   mean_std(stats + 2 * b, n_item, mean, sd);
@@ -1469,7 +1494,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     rewrite_glu(f.rewrite, E, skf, (int64_t)B * f.Fout * T, f.Cout);
     if (i == 0 && c.freq_emb != 0.0 && !rc) {
       const int64_t n = (int64_t)B * f.Fout * T * f.Cout;
-      hipLaunchKernelGGL(htd_add_rows_kernel, blocks(n), dim3(kT), 0, st, skf, f.Fout, T, f.Cout, Wb + m->emb_tab, n);
+      SESA_REQUIRE(f.Cout % 4 == 0 && (int64_t)T * f.Cout < (1ll << 31) && f.Fout < 65536 && B < 65536,
+                   SESA_ERR_INVALID, "htdemucs: frequency embedding rows");
+      hipLaunchKernelGGL(htd_add_rows_kernel,
+                         dim3((unsigned)((T * f.Cout / 4 + kT - 1) / kT), (unsigned)f.Fout, (unsigned)B),
+                         dim3(kT), 0, st, skf, f.Fout, T, f.Cout, Wb + m->emb_tab, n);
       SESA_CHECK_LAUNCH();
     }
     xf = skf;
@@ -1716,8 +1745,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     void* tok = profile_begin(st);
     float* FR = F32(pl.frames);
     const int nsig = B * m->nsrc * ach;
-    hipLaunchKernelGGL(htd_istft_frames_kernel, dim3(nsig, T), dim3(kT), 0, st, cur_f, T, m->fq[0].Cdec, ach, m->nsrc,
-                       st_f, (int64_t)kF0 * T * 2 * ach, win, tb, FR);
+    const int64_t n_groups = (int64_t)B * ((T + 1) / 2);
+    const int64_t n_ids = 8 * (int64_t)(2 * m->nsrc * ach) * ((n_groups + 7) / 8);
+    SESA_REQUIRE(n_ids < (1ll << 31), SESA_ERR_INVALID, "htdemucs forward: iSTFT grid too large");
+    hipLaunchKernelGGL(htd_istft_frames_kernel, dim3((unsigned)n_ids), dim3(kT), 0, st, cur_f, T, m->fq[0].Cdec, ach,
+                       m->nsrc, B, st_f, (int64_t)kF0 * T * 2 * ach, win, tb, FR);
     SESA_CHECK_LAUNCH();
     hipLaunchKernelGGL(htd_istft_ola_kernel, dim3((L + kT - 1) / kT, nsig), dim3(kT), 0, st, FR, T, L, ach, m->nsrc, win,
                        cur_t, st_t, out);
