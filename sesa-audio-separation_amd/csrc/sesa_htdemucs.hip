@@ -417,17 +417,10 @@ __global__ void __launch_bounds__(kT) htd_dc_apply_kernel(DcArgs a) {
     const float ga = a.g2[c] * r2, gg = a.g2[C + c] * r2;   // (v - mean) * (rstd * gamma) + beta
     const float oa = a.be2[c], og = a.be2[C + c];
     const float sc = a.scale[c];
-    // the residual rows of all kDcP / 4 positions are loaded up front: X is read and written in place, so
-    // with a load -> store per position the compiler cannot hoist the next position's load above the store
-    // and every position paid a full memory round trip
-    constexpr int NQ = kDcP / 4;
-    float* xrow = a.X + ((int64_t)row * T + t0 + wv) * C + c;
-    float xv[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) xv[q] = t0 + wv + 4 * q < T ? xrow[(int64_t)4 * q * C] : 0.f;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
+    for (int q = 0; q < kDcP / 4; ++q) {
       const int p = wv + 4 * q;
+      const int t = t0 + p;
+      if (t >= T) break;
       float va = ba, vg = bg;
 #pragma unroll
       for (int j4 = 0; j4 < HM; j4 += 4) {
@@ -441,11 +434,11 @@ __global__ void __launch_bounds__(kT) htd_dc_apply_kernel(DcArgs a) {
         va = fmaf(wa[j4 + 3], g.w, va);
         vg = fmaf(wg[j4 + 3], g.w, vg);
       }
-      xv[q] = xv[q] + sc * (fmaf(va - m2, ga, oa) * sigm(fmaf(vg - m2, gg, og)));
+      // (batching the kDcP / 4 residual loads ahead of the stores measured 1.5-14x slower: register
+      // pressure at HM = 32 / 64 and no gain at HM = 8 -- profiles/r04_htd_dcapply_batched_experiment.json)
+      float* xp = a.X + ((int64_t)row * T + t) * C + c;
+      *xp = *xp + sc * (fmaf(va - m2, ga, oa) * sigm(fmaf(vg - m2, gg, og)));
     }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      if (t0 + wv + 4 * q < T) xrow[(int64_t)4 * q * C] = xv[q];
   }
 }
 
