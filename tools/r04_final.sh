@@ -3,26 +3,30 @@
 #   GPU parity suite, smoke, sha-stamped HBM-traffic PMC summaries (separate FETCH_SIZE / WRITE_SIZE passes)
 #   for every dominant class + the streaming classes, one bench line per BASELINE config, rocprofv3 kernel
 #   stats.  Every GPU step has its own time limit; the script stops at the first failure.
-#   PART=a|b|c splits it over calls (a: tests + PMC, b: bench lines, c: rocprof + MFMA-busy passes).
+#   PART=t|p|b|c splits it over calls (t: GPU tests + smoke, p: PMC passes, b: bench lines, c: rocprof +
+#   MFMA-busy passes).
 set -e
 O=gpurun_out/final4
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 step() { echo "[final] $(date +%T) $*"; }
-PART=${PART:-abc}
-if [[ $PART == *a* ]]; then
+PART=${PART:-tpbc}
+if [[ $PART == *t* ]]; then
 step tests
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gputest.log 2>&1
 step smoke
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+fi
+if [[ $PART == *p* ]]; then
 step pmc mdx23c
-timeout -k 10 700 bash tools/pmc_refresh.sh mdx23c "conv3x3=conv3x3_db_kernel|tap_gemm_kernel<3, 3" \
+timeout -k 10 700 bash tools/pmc_refresh.sh mdx23c \
+  "conv3x3=conv3x3_db_kernel<true, true, 0, false, 1, true|conv3x3_db_kernel<true, false, 0, false, 1, true" \
   "tdf=tdf_dma_kernel|tdf_kernel|tdf_u_split" "act=act_split_kernel|act_f16" > $O/pmc_mdx23c.log 2>&1
 timeout -k 10 120 python3 tools/pmc_stream.py gpurun_out/pmc_mdx23c_f gpurun_out/pmc_mdx23c_w mdx23c \
   "$(python3 -c 'import bench; print(bench.default_precision("mdx23c"))')" gpurun_out > $O/pmc_stream.log 2>&1
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step pmc htdemucs
-timeout -k 10 700 bash tools/pmc_refresh.sh htdemucs "hconv=tok_gemm_kernel<|htd_dc_conv_valu" \
+timeout -k 10 700 bash tools/pmc_refresh.sh htdemucs "hconv=2, false, true, false|1, false, true, false|htd_dc_conv_valu" \
   "attn=attn_kernel|attn_f16_kernel" > $O/pmc_htdemucs.log 2>&1
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step pmc bs_roformer
