@@ -1335,24 +1335,33 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
       store_block(smem + ((kb + 1) & 1) * 2 * IMG);
       if (kb + 2 < n_blocks) load_block(kb + 2);
     }
+    // keys past Lk exist only in the last block (uniform branch: the full blocks skip 32 compare / selects)
+    if ((kb + 1) * kKB > Lk) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb * kKB + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= Lk) s[rb][r] = -INFINITY;
+        }
+    }
     float bmax = -INFINITY;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb * kKB + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        if (key >= Lk) s[rb][r] = -INFINITY;
-        bmax = fmaxf(bmax, s[rb][r]);
-      }
+      for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[rb][r]);
     bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
     const float m_new = fmaxf(m_run, bmax);
-    const float alpha = __expf(m_run - m_new);
+    // exp(x - m) as exp2(x log2e - m log2e): one fma per element feeding v_exp_f32 (exp2)
+    constexpr float kLog2e = 1.4426950408889634f;
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kLog2e);
+    const float ml = m_new * kLog2e;
     float psum = 0.f;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = __expf(s[rb][r] - m_new);
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[rb][r], kLog2e, -ml));
         s[rb][r] = p;
         psum += p;
       }

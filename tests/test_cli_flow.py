@@ -107,19 +107,19 @@ def test_cli_flow_matches_reference(tmp_path, idx):
 
 @pytest.mark.gpu
 def test_raw_model_keeps_session_precision():
-    """utils.apply_tta / demix on the raw model after an --enable_amp session (MDX23C: the fp16 TFC-conv
-    precision): the precision the session set must stay (inference_pytorch.py:229 passes the raw model)."""
+    """utils.apply_tta / demix on the raw model after an --enable_amp session (MDX23C: the fp16mix precision):
+    the precision the session set must stay (inference_pytorch.py:229 passes the raw model)."""
     from sesa.backend import create_inference_session
     from sesa.utils import apply_tta, demix, get_model_from_config
     from sesa.weights import synth_state_dict
     model, cfg = get_model_from_config("mdx23c", os.path.join(CONFIGS, "config_mdx23c_small.yaml"))
     model.load_state_dict(synth_state_dict(model, affine="random"))
     create_inference_session(model, device="cuda:0", enable_amp=True)
-    assert model.precision == "fp16"
+    assert model.precision == "fp16mix" == model._amp_precision
     mix = _mix(3, 40000)
     w = demix(cfg, model, mix, "cuda:0", model_type="mdx23c")
     apply_tta(cfg, model, mix, w, "cuda:0", "mdx23c")
-    assert model.precision == "fp16"
+    assert model.precision == "fp16mix" == model._amp_precision
 
 
 def test_flac_codec_roundtrip(tmp_path):

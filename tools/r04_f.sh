@@ -27,6 +27,7 @@ run bsr_d4 SESA_TOKGEMM_DEPTH=4 "--model bs_roformer --steps 2 --warmup 1"
 run bsr_d3 SESA_TOKGEMM_DEPTH=3 "--model bs_roformer --steps 2 --warmup 1"
 run htd_fp16mix fp=1 "--model htdemucs --precision fp16mix --steps 1 --warmup 1"
 run htd_bf16x3 fp=1 "--model htdemucs --precision bf16x3 --steps 1 --warmup 1"
+run htd_fp16mix_db SESA_HCONV_VARIANT=1 "--model htdemucs --precision fp16mix --steps 1 --warmup 1"
 run scn_fp16mix fp=1 "--model scnet --precision fp16mix --steps 2 --warmup 1"
 run scn_bf16x3 fp=1 "--model scnet --precision bf16x3 --steps 2 --warmup 1"
 echo "[r04f] $(date +%T) done"
