@@ -85,11 +85,11 @@ FULL_MEMBERS = (("mdx23c", "config_vocals_mdx23c.yaml"), ("bs_roformer", "config
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precisions", [("bf16x3", "bf16x3", "bf16x3"), ("fp16mix", "fp16", "bf16x3")],
+@pytest.mark.parametrize("precisions", [("bf16x3", "bf16x3", "bf16x3"), ("fp16mix", "fp16", "fp16mix")],
                          ids=["bf16x3", "bench"])
 def test_full_width_ensemble_matches_reference(golden, precisions):
     """BASELINE configs[4] at full width: the three full-size members (the bench line's precisions: MDX23C
-    fp16mix, BS-Roformer fp16 Linears, SCNet bf16x3 -- and all bf16x3) on a 3 s mix, each stem and the
+    fp16mix, BS-Roformer fp16, SCNet fp16mix -- and all bf16x3) on a 3 s mix, each stem and the
     avg_wave (weighted) / median_fft blends against the REAL reference composition
     (tests/golden/make_golden_ensemble_full.py: reference demix_pytorch_optimized per member, reference
     AudioEnsembleEngine blend).  Gate: per-sample RMS <= 1e-4."""
