@@ -357,8 +357,11 @@ def cpu_baseline(model_name, cfg_path, n_chunks_track, track_seconds, sample_chu
     with torch.inference_mode():
         fwd(params, cfg, x)                       # warm-up (allocator, oneDNN primitives)
         t0 = time.time()
-        for _ in range(sample_chunks):
+        for i in range(sample_chunks):
             fwd(params, cfg, x)
+            # a progress line per chunk (stderr): a silent multi-minute CPU leg reads as a hung run
+            print(f"[bench] cpu_baseline {model_name}: chunk {i + 1}/{sample_chunks} "
+                  f"({time.time() - t0:.1f} s)", file=sys.stderr, flush=True)
     per_chunk = (time.time() - t0) / sample_chunks
     return {"value": round(track_seconds / (per_chunk * n_chunks_track), 4), "unit": "separated-audio sec/sec",
             "cores": threads, "kind": "port",
