@@ -654,8 +654,14 @@ def main():
                 gbs = kbytes / (kms * 1e-3) / 1e9
                 hbm[kc] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / 8000.0, 4), "launches": kn,
                            "avg_launch_ms": round(kms / kn, 4), "bytes_per_launch": round(kbytes / kn)}
-                # rocprofv3 counter bytes of one step of this workload (profiles/pmc_<class>.json, tools/pmc_stream.py)
-                cb, src = stream_counter_bytes(kc, args.model, args.precision)
+                # rocprofv3 counter bytes of one step of this workload (profiles/pmc_<class>.json, tools/pmc_stream.py);
+                # act: the per-launch summary of tools/pmc_traffic.py (same sha / precision rules)
+                if kc == "act":   # (measured on MDX23C's act_split / act_f16 launches: that model only)
+                    bpl, src = (pmc_traffic("act", class_precision("act", args.precision, args.model))
+                                if args.model == "mdx23c" else (None, "act counters: measured for mdx23c only"))
+                    cb = bpl * kn / args.steps if bpl else None
+                else:
+                    cb, src = stream_counter_bytes(kc, args.model, args.precision)
                 hbm[kc]["counter_source"] = src
                 if cb:
                     cgbs = cb * args.steps / (kms * 1e-3) / 1e9
