@@ -1351,11 +1351,22 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[rb][r]);
     bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
-    const float m_new = fmaxf(m_run, bmax);
-    // exp(x - m) as exp2(x log2e - m log2e): one fma per element feeding v_exp_f32 (exp2)
+    // lazy rescale: the running max m (and with it O and l) moves only when a block's max exceeds it by more than
+    // 8, so between rescales P = exp(s - m) <= e^8 ~ 2981 (well inside fp16) and most blocks skip the 32
+    // multiplies of O; O / l is unchanged (P and l carry the same factor).  The two lanes of a query row hold the
+    // same bmax and m, so they agree.
     constexpr float kLog2e = 1.4426950408889634f;
-    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kLog2e);
-    const float ml = m_new * kLog2e;
+    if (bmax > m_run + 8.f) {
+      const float alpha = __builtin_amdgcn_exp2f((m_run - bmax) * kLog2e);   // (0 on the first block)
+      l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+      m_run = bmax;
+    }
+    // exp(x - m) as exp2(x log2e - m log2e): one fma per element feeding v_exp_f32 (exp2)
+    const float ml = m_run * kLog2e;
     float psum = 0.f;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
@@ -1366,12 +1377,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
         psum += p;
       }
     psum += __shfl_xor(psum, 32);
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+    l_run += psum;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int r0 = 8 * (ks & 1);
