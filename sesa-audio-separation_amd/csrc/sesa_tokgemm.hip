@@ -1424,6 +1424,169 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_f16_kernel(AttnArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// attn_f16_band_kernel<HPW>: BS-Roformer's band attention (self attention over L <= 64 band tokens, dh = 64,
+// q / k / v / gates from the fp16 plane, fp16 output plane), HPW heads of one sequence per workgroup: the
+// sequence has a single key block, so the per-head work is one QK^T / PV block (16 MFMAs a wave) and the
+// one-head-per-workgroup form spent its time on setup and exposed load latency (4 % MFMA-busy).  Here head h + 1's
+// Q / K / V are loaded into registers under head h's MFMAs and staged into the other LDS buffer, one barrier
+// per head.  Same arithmetic as attn_f16_kernel<2, true> on its single block (bit-identical output).
+template <int HPW>
+__global__ void __launch_bounds__(128, 2) attn_f16_band_kernel(AttnArgs a) {
+  constexpr int NTH = 128, NIT = kKB * 16 / NTH;   // 8 staging items (4 fp16 of K and of V) per thread
+  constexpr int IMG = kKB * kHD * 2;                // one fp16 [64 key][64 d] image
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];   // [buffer][K, V]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hl = lane >> 5;
+  const int head0 = blockIdx.y * HPW;
+  const int seq = blockIdx.z;
+  const int64_t sbase = (int64_t)(seq / a.sdiv) * a.smul_a + (int64_t)(seq % a.sdiv) * a.smul_b;
+  auto token = [&](int p) -> int64_t { return sbase + (int64_t)p * a.pstride; };
+  const int L = a.L;
+  const int q_pos = wave * 32 + l32;
+  const bool q_ok = q_pos < L;
+  const uint16_t* qrow = a.qkv16 + token(q_ok ? q_pos : 0) * a.ld;
+
+  u32x4 qraw[4];
+  uint2 kr[NIT], vr[NIT];
+  auto load = [&](int head) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      qraw[ks] = q_ok ? *reinterpret_cast<const u32x4*>(qrow + head * kHD + 16 * ks + 8 * hl) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + i * NTH;
+      const int key = e >> 4, dq = (e & 15) * 4;
+      const bool ok = key < L;
+      const uint16_t* row = a.qkv16 + token(ok ? key : 0) * a.ld + head * kHD + dq;
+      kr[i] = ok ? *reinterpret_cast<const uint2*>(row + a.k_off) : make_uint2(0u, 0u);
+      vr[i] = ok ? *reinterpret_cast<const uint2*>(row + a.v_off) : make_uint2(0u, 0u);
+    }
+  };
+  auto store = [&](char* stg) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = tid + i * NTH;
+      const int key = e >> 4, dq = (e & 15) * 4;
+      const int off = swz(key, dq >> 3) + ((dq & 4) << 1);
+      *reinterpret_cast<uint2*>(stg + off) = kr[i];
+      *reinterpret_cast<uint2*>(stg + IMG + off) = vr[i];
+    }
+  };
+  bf16x8 qf[4];   // Q / 8 (exact: dh = 64), fp16 bits
+  auto q_convert = [&]() {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      u32x4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = (float)__builtin_bit_cast(_Float16, (uint16_t)(qraw[ks][e] & 0xffffu));
+        const float hi = (float)__builtin_bit_cast(_Float16, (uint16_t)(qraw[ks][e] >> 16));
+        w[e] = pack2h_(lo * 0.125f, hi * 0.125f);
+      }
+      qf[ks] = __builtin_bit_cast(bf16x8, w);
+    }
+  };
+  const int tg = lane >> 4, ti = lane & 15;
+  const int tr_q = ti >> 2, tp = ti & 3, th = tg >> 1;
+  auto vt_frag = [&](const char* V, int ks, int db) -> bf16x8 {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const int d = db * 32 + 16 * (tg & 1) + 4 * tp;
+    const int key0 = 32 * (ks >> 1) + 16 * (ks & 1) + 4 * th + tr_q;
+    const bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) bf16x4*)(V + swz(key0, d >> 3) + ((d & 7) << 1)));
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) bf16x4*)(V + swz(key0 + 8, d >> 3) + ((d & 7) << 1)));
+    return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  load(head0);
+  store(smem);
+  q_convert();
+  __syncthreads();
+  for (int hi_ = 0; hi_ < HPW; ++hi_) {
+    const int head = head0 + hi_;
+    const bf16x8 q0 = qf[0], q1 = qf[1], q2 = qf[2], q3 = qf[3];
+    if (hi_ + 1 < HPW) load(head + 1);   // registers only: lands under this head's MFMAs
+    const char* K = smem + (hi_ & 1) * 2 * IMG;
+    const char* V = K + IMG;
+    f32x16 s[2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[rb][r] = 0.f;
+      s[rb] = mfma32h_(*reinterpret_cast<const bf16x8*>(K + swz(rb * 32 + l32, 0 + hl)), q0, s[rb]);
+      s[rb] = mfma32h_(*reinterpret_cast<const bf16x8*>(K + swz(rb * 32 + l32, 2 + hl)), q1, s[rb]);
+      s[rb] = mfma32h_(*reinterpret_cast<const bf16x8*>(K + swz(rb * 32 + l32, 4 + hl)), q2, s[rb]);
+      s[rb] = mfma32h_(*reinterpret_cast<const bf16x8*>(K + swz(rb * 32 + l32, 6 + hl)), q3, s[rb]);
+    }
+    if (L < kKB) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= L) s[rb][r] = -INFINITY;
+        }
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m = fmaxf(m, s[rb][r]);
+    m = fmaxf(m, __shfl_xor(m, 32));
+    constexpr float kLog2e = 1.4426950408889634f;
+    const float ml = m * kLog2e;
+    float l = 0.f;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[rb][r], kLog2e, -ml));
+        s[rb][r] = p;
+        l += p;
+      }
+    l += __shfl_xor(l, 32);
+    f32x16 o[2];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int r0 = 8 * (ks & 1);
+      const f32x16& sv = s[ks >> 1];
+      const u32x4 w = {pack2h_(sv[r0], sv[r0 + 1]), pack2h_(sv[r0 + 2], sv[r0 + 3]), pack2h_(sv[r0 + 4], sv[r0 + 5]),
+                       pack2h_(sv[r0 + 6], sv[r0 + 7])};
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, w);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) o[db] = mfma32h_(vt_frag(V, ks, db), pf, o[db]);
+    }
+    if (q_ok) {
+      const int64_t tq = token(q_pos);
+      const float gate =
+          a.g_off >= 0 ? sigmoidf_((float)__builtin_bit_cast(_Float16, a.qkv16[tq * a.ld + a.g_off + head])) : 1.f;
+      const float scale = gate / l;
+      const int64_t obase = tq * a.o_ld + head * kHD;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = db * 32 + 8 * g4 + 4 * hl;
+          *reinterpret_cast<uint2*>(a.out_hi + obase + d) =
+              make_uint2(pack2h_(o[db][4 * g4] * scale, o[db][4 * g4 + 1] * scale),
+                         pack2h_(o[db][4 * g4 + 2] * scale, o[db][4 * g4 + 3] * scale));
+        }
+    }
+    if (hi_ + 1 < HPW) {
+      store(smem + ((hi_ + 1) & 1) * 2 * IMG);   // that buffer's last reads were head hi_ - 1's, before the barrier
+      q_convert();
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // fp32 rows -> bf16 hi / lo planes (+ RMSNorm row scale): one wave per row, f32x4 per lane-step.
 // F16: one fp16 plane (round to nearest even) -- the A operand of the fp16 single-pass Linears.  With a
 // row_scale output the fp16 plane holds x * row_scale (the RMS-normalised row, |value| <= sqrt(K)), not the raw
@@ -1666,7 +1829,18 @@ int launch_attention(const AttnArgs& a, int x3, hipStream_t st) {
                "8-B aligned");
   if (x3 == 2) {
     const dim3 g64((unsigned)((a.L + 63) / 64), (unsigned)a.heads, (unsigned)a.n_seq);
-    if (a.qkv16) {
+    // band attention (single key block): heads looped per workgroup, SESA_ATTN_BAND_HPW = 1 (off) | 2 | 4 | 8
+    static const int hpw = [] {
+      const int v = getenv("SESA_ATTN_BAND_HPW") ? atoi(getenv("SESA_ATTN_BAND_HPW")) : 4;
+      return v == 2 || v == 4 || v == 8 ? v : 1;
+    }();
+    if (hpw > 1 && a.qkv16 && !a.kv && a.L <= kKB && (a.Lk == 0 || a.Lk == a.L) && (a.dh == 0 || a.dh == kHD) &&
+        a.out_hi && a.out_f16 && a.heads % hpw == 0) {
+      const dim3 gb(1u, (unsigned)(a.heads / hpw), (unsigned)a.n_seq);
+      if (hpw == 2) hipLaunchKernelGGL(attn_f16_band_kernel<2>, gb, dim3(128), 0, st, a);
+      else if (hpw == 4) hipLaunchKernelGGL(attn_f16_band_kernel<4>, gb, dim3(128), 0, st, a);
+      else hipLaunchKernelGGL(attn_f16_band_kernel<8>, gb, dim3(128), 0, st, a);
+    } else if (a.qkv16) {
       if (a.L <= 64) hipLaunchKernelGGL((attn_f16_kernel<2, true>), g64, dim3(128), 0, st, a);
       else hipLaunchKernelGGL((attn_f16_kernel<4, true>), grid, dim3(kThreads), 0, st, a);
     } else if (a.L <= 64) {
