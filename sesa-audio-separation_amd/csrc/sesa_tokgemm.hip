@@ -1829,9 +1829,11 @@ int launch_attention(const AttnArgs& a, int x3, hipStream_t st) {
                "8-B aligned");
   if (x3 == 2) {
     const dim3 g64((unsigned)((a.L + 63) / 64), (unsigned)a.heads, (unsigned)a.n_seq);
-    // band attention (single key block): heads looped per workgroup, SESA_ATTN_BAND_HPW = 1 (off) | 2 | 4 | 8
+    // band attention (single key block): heads looped per workgroup, SESA_ATTN_BAND_HPW = 1 (off) | 2 | 4 | 8.
+    // Same box, attention class 171.1 (1) -> 165.9 (2) / 167.2-168.3 (4) / 169.6 (8) ms per step, output
+    // bit-identical (profiles/r04_attn_band_hpw*.json)
     static const int hpw = [] {
-      const int v = getenv("SESA_ATTN_BAND_HPW") ? atoi(getenv("SESA_ATTN_BAND_HPW")) : 4;
+      const int v = getenv("SESA_ATTN_BAND_HPW") ? atoi(getenv("SESA_ATTN_BAND_HPW")) : 2;
       return v == 2 || v == 4 || v == 8 ? v : 1;
     }();
     if (hpw > 1 && a.qkv16 && !a.kv && a.L <= kKB && (a.Lk == 0 || a.Lk == a.L) && (a.dh == 0 || a.dh == kHD) &&
