@@ -78,6 +78,7 @@ TRACK_SECONDS = {"htdemucs": 1800.0}
 # rank's last forward is not a small remainder (169 chunks at N=1 -> 3 forwards of 57; 22 per rank at
 # N=8 -> one forward of 22)
 BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md chip table (dense, no sparsity)
+HBM_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E peak
 FP32_VECTOR_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table (fp32 vector)
 KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "tokgemm": "tok_gemm_glds_kernel + tok_gemm_kernel (token-major Linear layers, bf16x3 "
@@ -85,14 +86,16 @@ KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, bf16x3 v_mfm
          "lstm": "scn_lstm_mfma_kernel (bi-LSTM recurrence, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "hconv": "tok_gemm_kernel<conv> (HTDemucs implicit-GEMM convolutions, v_mfma_f32_32x32x16_bf16)",
          "attn": "attn_kernel (flash attention, S^T = K Q^T, bf16x3 v_mfma_f32_32x32x16_bf16)",
-         "simt": "SCNet fp32 VALU kernels (scn_cm_in / scn_cm_out ConvolutionModule, scn_sdconv / scn_convtr band "
-                 "convs, scn_rfft / scn_irfft feature conversion)"}
+         "simt": "fp32 VALU kernels (SCNet: scn_cm_in / scn_cm_out ConvolutionModule, scn_sdconv / scn_convtr band "
+                 "convs, scn_rfft / scn_irfft feature conversion; HTDemucs: htd_dc_conv_valu / htd_dc_gram / htd_dc_apply "
+                 "DConv, norms)"}
 
 
 def kdesc(kclass, precision, model):
     """KDESC with the MFMA instruction of the precision the class's launches run in (class_precision)."""
     cp = class_precision(kclass, precision, model)
     if kclass == "conv3x3":
+        cp = member_precision("mdx23c", precision, model)
         return {"bf16x3": KDESC["conv3x3"],
                 "bf16": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, single-pass v_mfma_f32_32x32x16_bf16)",
                 "fp16": "conv3x3_db_kernel<F16, MI4> (TFC conv3x3 T >= 32: one v_mfma_f32_32x32x16_f16 pass, "
@@ -107,7 +110,7 @@ def kdesc(kclass, precision, model):
                 "fp32 softmax statistics, double-buffered K / V)")
     if kclass == "hconv" and cp == "fp16":
         return ("tok_gemm_kernel<conv, F16> (HTDemucs implicit-GEMM convolutions and 1x1 rewrites, operand rounded "
-                "once to fp16 in the staging, one v_mfma_f32_32x32x16_f16 pass) + htd_dc_conv_valu (fp32 VALU)")
+                "once to fp16 in the staging, one v_mfma_f32_32x32x16_f16 pass)")
     if kclass == "tokgemm" and cp == "fp16":
         return ("tok_gemm_glds_kernel<EP_F16> (QKV / out-projection / FF Linears, one v_mfma_f32_16x16x32_f16 pass) + "
                 "bf16x3 token GEMMs (band split, mask MLPs: v_mfma_f32_32x32x16_bf16 / 16x16x32_bf16)")
@@ -142,35 +145,81 @@ def default_precision(model):
     """MDX23C: fp16mix -- the T >= 32 TFC 3x3 convs on one fp16 MFMA pass except the encoder level-1 ones
     (bf16x3), the decoder TDF Linears fp16, the rest bf16x3: every MDX23C full-chunk golden (0.1-RMS noise,
     §8(d) sines, 0.3-RMS noise, a second weight draw) within 5.3e-5 of the reference; plain fp16 sits at
-    9.75e-5 on the 0.3-RMS fixture, no
-    margin -- also for the MDX23C member of the ensemble; BS-Roformer: its QKV / out / FF Linears
-    and attention on one fp16 pass (SESA_PREC_F16); HTDemucs fp16mix: attention, implicit-GEMM convs and 1x1
-    rewrites fp16, Linears bf16x3 (5.9e-6 full segment); SCNet fp16mix: token GEMMs fp16, LSTM recurrence
-    bf16x3 (9.7e-6 full chunk) -- the ensemble's SCNet member too.  The line carries the measured parity."""
+    9.75e-5 on the 0.3-RMS fixture, no margin.  BS-Roformer fp16: its QKV / out / FF Linears
+    and attention on one fp16 pass.  HTDemucs fp16mix: attention, implicit-GEMM convs, 1x1 rewrites and the
+    transformer / channel Linears on one fp16 pass (5.9e-6 full segment).  SCNet fp16mix: token GEMMs fp16,
+    LSTM recurrence bf16x3 (9.7e-6 full chunk).  The ensemble's members run sesa.ensemble.ENSEMBLE_PRECISIONS
+    (chosen so every configs[4] blend holds 8e-5).  Every line carries its measured parity."""
     return {"mdx23c": "fp16mix", "ensemble": "fp16mix", "bs_roformer": "fp16", "htdemucs": "fp16mix",
             "scnet": "fp16mix"}.get(model, "bf16x3")
 
 
-# kernel classes whose kernels run in the MDX23C precision mode; every other class is bf16x3 in the fp16 modes
+# precision modes each native model accepts (sesa/models/*.py _precisions)
+MODEL_PRECISIONS = {"mdx23c": ("bf16x3", "bf16", "fp16w2", "fp16", "fp16mix"), "bs_roformer": ("bf16x3", "bf16", "fp16"),
+                    "scnet": ("bf16x3", "bf16", "fp16mix"), "htdemucs": ("bf16x3", "bf16", "fp16mix")}
+
+
+def member_precision(name, precision, model=None):
+    """The precision build_model gives member `name` of a `model` line run in `precision`: the ensemble's members
+    their sesa.ensemble.ENSEMBLE_PRECISIONS for its default precision; otherwise fp16mix -> fp16 where the model
+    has no fp16mix (BS-Roformer), and any mode the model lacks -> bf16x3 (e.g. fp16w2, MDX23C's only)."""
+    if model == "ensemble" and precision == default_precision("ensemble"):
+        from sesa.ensemble import ENSEMBLE_PRECISIONS
+        return ENSEMBLE_PRECISIONS[name]
+    if precision == "fp16mix" and precision not in MODEL_PRECISIONS[name]:
+        precision = "fp16"
+    return precision if precision in MODEL_PRECISIONS[name] else "bf16x3"
+
+
+# kernel classes whose kernels run in the MDX23C precision mode
 MDX_CLASSES = ("conv3x3", "conv3x3_x3", "conv1x1", "down", "up", "tdf", "act")
 
 
-def class_precision(kclass, precision, model="mdx23c"):
-    """The precision a kernel class's launches run in for a bench line of `model` in `precision` (the PMC
-    stamp bench.py compares): the MDX23C classes follow the MDX23C mode; the token GEMMs and the attention
-    follow BS-Roformer's fp16 mode (bs_roformer, ensemble); HTDemucs fp16mix runs its attention and convs fp16;
-    every other class is bf16x3 in the fp16 modes."""
-    if not precision.startswith("fp16") or kclass in MDX_CLASSES:
-        return precision
-    if kclass in ("tokgemm", "attn") and model in ("bs_roformer", "ensemble"):
-        return "fp16"
-    if kclass in ("hconv", "attn") and model == "htdemucs" and precision == "fp16mix":
-        return "fp16"         # HTDemucs fp16mix: attention and implicit-GEMM convs fp16, Linears bf16x3
-    if kclass == "tokgemm" and model == "scnet" and precision == "fp16mix":
-        return "fp16"         # SCNet fp16mix: token GEMMs fp16, the LSTM recurrence bf16x3
-    if kclass == "tokgemm" and model == "htdemucs":
+def class_precision(kclass, precision, model="mdx23c", members=None):
+    """The arithmetic the launches of a kernel class run in, for a `model` line in `precision` (the roofline's MFMA
+    pass count and the PMC stamp bench.py compares): ``members`` maps each member to the precision it actually built
+    with (default: member_precision).  MDX23C classes follow MDX23C's mode; token GEMMs run one fp16 pass for a
+    BS-Roformer fp16, SCNet fp16mix or HTDemucs fp16mix member (HTDemucs: unless SESA_HTD_PRESPLIT=0 keeps its
+    Linears bf16x3), else that member's mode (bf16 / bf16x3); attention fp16 for BS-Roformer fp16 / HTDemucs
+    fp16mix; HTDemucs' implicit-GEMM convs fp16 in fp16mix; the LSTM recurrence bf16x3 (bf16 in the bf16 mode);
+    simt is fp32 VALU."""
+    if members is None:
+        names = ("mdx23c", "bs_roformer", "scnet") if model == "ensemble" else (model,)
+        members = {n: member_precision(n, precision, model) for n in names}
+    if kclass in MDX_CLASSES:
+        p = members.get("mdx23c", precision)
+        if p not in ("fp16", "fp16w2", "fp16mix"):
+            return p
+        # the fp16 modes: conv3x3 = the one-pass (fp16w2: two-pass) fp16 direct convs; act = MDX23C's own mode
+        # (its PMC stamp); fp16mix's TDF Linears mix fp16 (decoder) and bf16x3 stacks, priced at the fp16 peak (the
+        # conservative choice); the opt-in fp16 up-convs (SESA_MDX_UP16=1); everything else stays bf16x3
+        if kclass == "conv3x3":
+            return "fp16w2" if p == "fp16w2" else "fp16"
+        if kclass == "act":
+            return p
+        if kclass == "tdf" and p == "fp16mix":
+            return "fp16"
+        if kclass == "up" and p == "fp16mix" and os.environ.get("SESA_MDX_UP16") == "1":
+            return "fp16"
         return "bf16x3"
-    return "bf16x3"
+    if kclass == "simt":
+        return "fp32"
+    if kclass == "lstm":
+        return "bf16" if members.get("scnet") == "bf16" else "bf16x3"
+    f16 = {"bs_roformer": "fp16", "scnet": "fp16mix", "htdemucs": "fp16mix"}
+    users = {"tokgemm": ("bs_roformer", "scnet", "htdemucs"), "attn": ("bs_roformer", "htdemucs"),
+             "hconv": ("htdemucs",)}.get(kclass, ())
+    modes = set()
+    for n in users:
+        if n not in members:
+            continue
+        p = members[n]
+        if p == f16[n] and not (n == "htdemucs" and kclass == "tokgemm" and os.environ.get("SESA_HTD_PRESPLIT") == "0"):
+            modes.add("fp16")
+        else:
+            modes.add("bf16" if p == "bf16" else "bf16x3")
+    # a class mixing one-pass fp16 and bf16x3 launches is priced at the one-pass peak (the conservative choice)
+    return "fp16" if "fp16" in modes else (modes.pop() if len(modes) == 1 else "bf16x3")
 
 
 def pmc_traffic(kclass, precision="bf16x3"):
@@ -439,17 +488,14 @@ def _forward_sizes(n_chunks, exec_batch, world):
     return [list(range(i, min(share, i + exec_batch))) for i in range(0, share, exec_batch)]
 
 
-def build_model(name, precision):
+def build_model(name, precision, line_model=None):
+    """Member `name` with name-keyed random-init weights, in member_precision(name, precision, line_model)."""
     from sesa.utils import get_model_from_config
     from sesa.weights import synth_state_dict
     cfg_path = os.path.join(CFG_DIR, MODELS[name][0])
     model, cfg = get_model_from_config(name, cfg_path)
     model.load_state_dict(synth_state_dict(model) if name == "mdx23c" else synth_weights(model), strict=True)
-    if precision == "fp16mix" and precision not in getattr(model, "_precisions", ()):
-        precision = "fp16"    # the ensemble's fp16 line: BS-Roformer's own fp16 mode
-    if precision not in getattr(model, "_precisions", ()):
-        precision = "bf16x3"  # (e.g. fp16w2 is MDX23C's only; SCNet / HTDemucs have no fp16 mode)
-    model.set_precision(precision)
+    model.set_precision(member_precision(name, precision, line_model))
     return model, cfg, cfg_path
 
 
@@ -472,6 +518,9 @@ def main():
     ap.add_argument("--no-parity", action="store_true", help="skip the parity forward (PMC passes: one workload only)")
     ap.add_argument("--streams", type=int, default=1, help="forwards in flight on separate HIP streams (> 1 is refused: "
                     "not bit-consistent, sesa/parallel.py)")
+    ap.add_argument("--rank-share", type=int, default=0, metavar="W",
+                    help="one-GPU rehearsal of rank 0's share of a W-rank run (its chunks, its exec batch, local OLA + "
+                         "finalise, no collective): value = the implied W-rank ceiling (track seconds / rank-0 time)")
     ap.add_argument("--cpu-chunks-only", action="store_true",
                     help="mdx23c: time --cpu-sample-chunks forwards instead of the configs[0] 10 s end-to-end run")
     args = ap.parse_args()
@@ -503,7 +552,8 @@ def main():
     from sesa.parallel import demix_sharded
 
     names = list(ENSEMBLE) if args.model == "ensemble" else [args.model]
-    members = [build_model(nm, args.precision) for nm in names]
+    members = [build_model(nm, args.precision, args.model) for nm in names]
+    member_prec = {nm: m.precision for nm, (m, _, _) in zip(names, members)}
     n = int(round(track_seconds * SR))
     rng = np.random.default_rng(0)
     mix_host = torch.from_numpy((0.1 * rng.standard_normal((2, n))).astype(np.float32)).pin_memory()
@@ -526,10 +576,12 @@ def main():
     def chunk_len(cfg, mode):
         return int(cfg.training.samplerate * cfg.training.segment) if mode == "demucs" else int(cfg.audio.chunk_size)
 
-    batches = [args.exec_batch or plan_exec_batch(m, c, chunk_len(cfg, md), dev, world=world, streams=args.streams)
+    sim = args.rank_share > 1 and world == 1      # rank 0's share of an args.rank_share-rank plan, on this GPU
+    pworld = args.rank_share if sim else world    # the world size the chunk plan is sharded for
+    batches = [args.exec_batch or plan_exec_batch(m, c, chunk_len(cfg, md), dev, world=pworld, streams=args.streams)
                for (m, cfg, _), c, md in zip(members, chunks, modes)]
     from sesa.parallel import shard_plan
-    shard_ranges = [shard_plan(cfg, n, world, md)["ranges"] for (_, cfg, _), md in zip(members, modes)]
+    shard_ranges = [shard_plan(cfg, n, pworld, md)["ranges"] for (_, cfg, _), md in zip(members, modes)]
     path_flop = sum(c * MODELS[nm][1] for c, nm in zip(chunks, names))
     stems_host = None
 
@@ -538,12 +590,12 @@ def main():
         mix_d = mix_host.to(dev, non_blocking=True)                          # H2D inside the timed region
         if args.model == "ensemble":
             est = ensemble_separate([(cfg, m) for m, cfg, _ in members], mix_d, "vocals", args.blend, rank=rank,
-                                    world=world, exec_batch=batches)[0]
+                                    world=pworld, exec_batch=batches, simulate=sim)[0]
         else:
             m, cfg, _ = members[0]
-            est = demix_sharded(cfg, m, mix_d, dev, rank=rank, world=world, exec_batch=batches[0], mode=modes[0],
-                                streams=args.streams)
-        if rank == 0:                                                         # stems D2H (one copy of the result)
+            est = demix_sharded(cfg, m, mix_d, dev, rank=rank, world=pworld, exec_batch=batches[0], mode=modes[0],
+                                streams=args.streams, simulate=sim)
+        if rank == 0:        # stems D2H (one copy of the result; the RCCL gather delivers it to rank 0 only)
             if stems_host is None or stems_host.shape != est.shape or stems_host.dtype != est.dtype:
                 stems_host = torch.empty(est.shape, dtype=est.dtype, pin_memory=True)
             stems_host.copy_(est, non_blocking=True)
@@ -569,53 +621,73 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    assert torch.isfinite(est).all().item()
+    assert (est is None) == (rank != 0)
     if rank == 0:
+        assert torch.isfinite(est).all().item()
         assert torch.isfinite(stems_host).all().item() and stems_host.shape == est.shape
 
+    # ---- rooflines of every kernel class, from libsesa's live hipEvent timing of the timed region ----
+    # Each launch records its algorithmic FLOPs and algorithmic HBM bytes (operands read once, results written once,
+    # in the storage types the launch reads / writes); a class's arithmetic intensity against the ridge of its own
+    # compute peak picks its bound, and floor_frac = (sum over its launches of max(FLOP / peak, bytes / 8 TB/s)) /
+    # its measured time -- the fraction of the roofline each launch's own intensity allows.
+    passes_of = {"bf16x3": 3, "bf16": 1, "fp16w2": 2, "fp16": 1}
+
+    def class_peak(kc):
+        """(compute peak TFLOP/s, compute-bound name, note) of kernel class kc in this line's precisions."""
+        cp = class_precision(kc, args.precision, args.model, member_prec)
+        if cp == "fp32":
+            return FP32_VECTOR_TFLOPS, "valu", "157.3 TF/s fp32 vector FMA peak (MI355X_MICROARCH.md; these kernels use no MFMA)"
+        p = passes_of[cp]
+        note = f"2.5 PF/s dense bf16/fp16 / {p} MFMA pass(es) per algorithmic FLOP ({cp})"
+        if kc == "conv3x3" and member_prec.get("mdx23c") == "fp16mix":
+            note += (f"; in fp16mix (plan {f16_plan()}) the conv3x3 class holds only the one-pass fp16 launches, the "
+                     f"plan's bf16x3 levels are the conv3x3_x3 class")
+        return BF16_DENSE_TFLOPS / p, "mfma", note
+
+    def class_roof(kc):
+        ms, n, work, nbytes = _native.profile_read2(kc)
+        if not n or ms <= 0:
+            return None
+        peak_c, cbound, note = class_peak(kc)
+        floor = _native.profile_floor(kc, peak_c, HBM_GBS)
+        ridge = peak_c * 1e12 / (HBM_GBS * 1e9)                     # FLOP per byte
+        ai = work / nbytes if nbytes > 0 else None
+        hbm = ai is not None and ai < ridge
+        r = {"bound": "hbm" if hbm else cbound,
+             "achieved": round(nbytes / (ms * 1e-3) / 1e9, 1) if hbm else round(work / (ms * 1e-3) / 1e12, 2),
+             "peak": HBM_GBS if hbm else round(peak_c, 1), "unit": "GB/s" if hbm else "TFLOP/s",
+             "launches": n, "ms_per_step": round(ms / args.steps, 2), "avg_launch_ms": round(ms / n, 4),
+             "flop_per_launch": round(work / n), "algorithmic_bytes_per_launch": round(nbytes / n) if nbytes else None,
+             "flop_per_byte": round(ai, 1) if ai else None, "ridge_flop_per_byte": round(ridge, 1),
+             "achieved_tflops": round(work / (ms * 1e-3) / 1e12, 2),
+             "achieved_alg_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1) if nbytes else None,
+             "floor_ms_per_step": round(floor / args.steps, 2), "floor_frac": round(floor / ms, 4) if nbytes else None,
+             "peak_note": note + (f"; HBM-side: {ai:.0f} FLOP/B < ridge {ridge:.0f}" if hbm else "")}
+        r["frac"] = round(r["achieved"] / r["peak"], 4)
+        return r
+
+    compute_classes = ("conv3x3", "conv3x3_x3", "conv1x1", "down", "up", "tdf", "tokgemm", "attn", "lstm", "simt",
+                       "hconv")
+    roofs = {kc: rf for kc in compute_classes if (rf := class_roof(kc))}
     # dominant kernel class: the model's own, or the class with the most kernel time
-    kclass = MODELS[args.model][2]
-    if kclass is None:
-        kclass = max(("conv3x3", "tokgemm", "lstm", "hconv", "attn", "simt"), key=lambda k: _native.profile_read(k)[0])
-    ms, launches, work = _native.profile_read(kclass)
-    # MFMA passes per algorithmic FLOP of the dominant class (fp16 has the same dense peak as bf16); in the
-    # fp16 modes the conv3x3 class is the fp16 direct convs (the T < 32 tap_gemm 3x3s, ~2 % of its FLOPs,
-    # stay bf16x3)
-    # (by the class's own precision, class_precision; a class that mixes fp16 and bf16x3 launches -- BS-Roformer's
-    # token GEMMs: QKV / FF fp16, band split / out-projection / mask MLPs bf16x3 -- is priced at the fp16 peak,
-    # the conservative choice)
-    passes = {"bf16x3": 3, "bf16": 1, "fp16w2": 2, "fp16": 1, "fp16mix": 1}[class_precision(kclass, args.precision,
-                                                                                             args.model)]
-    achieved = work / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-    peak = BF16_DENSE_TFLOPS / passes
-    note = f"2.5 PF/s dense bf16/fp16 / {passes} MFMA pass(es) per algorithmic FLOP ({args.precision})"
-    if class_precision(kclass, args.precision, args.model) == "fp16mix":
-        note = (f"2.5 PF/s dense fp16, one MFMA pass: in fp16mix (plan {f16_plan()}) the conv3x3 class holds only "
-                f"the one-pass fp16 launches; the plan's bf16x3 levels are the conv3x3_x3 class")
-    if kclass == "lstm":  # the recurrence is bf16x3 on MFMA in either precision mode
-        peak, note = BF16_DENSE_TFLOPS / 3, "2.5 PF/s dense bf16 / 3 MFMA passes (the recurrence is always bf16x3)"
-    bound = "mfma"
-    if kclass == "simt":  # SCNet's fp32 VALU kernels (band convs, ConvolutionModule, feature-conversion DFTs)
-        peak, bound = FP32_VECTOR_TFLOPS, "valu"
-        note = "157.3 TF/s fp32 vector FMA peak (MI355X_MICROARCH.md chip table; these kernels use no MFMA)"
-    traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model))
-    alg_bytes = None
-    if kclass == "conv3x3":
-        m0, cfg0, _ = members[0]
-        per_fwd, l_fwd = 0.0, 0
-        for nb_ in [len(x) for x in _forward_sizes(chunks[0], batches[0], world)]:
-            b_, l_ = mdx23c_conv3x3_alg_bytes(cfg0, nb_, args.precision, f16_plan())
-            per_fwd += b_
-            l_fwd += l_
-        alg_bytes = round(per_fwd / max(l_fwd, 1))
+    kclass = MODELS[args.model][2] or max(roofs, key=lambda k: roofs[k]["ms_per_step"])
+    roof = dict(roofs[kclass])
+    traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model, member_prec))
     if isinstance(traffic_src, dict):   # one algorithmic figure: this run's (the PMC file's own is for its run)
         traffic_src.pop("algorithmic_bytes_per_launch", None)
-    roof = {"bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": kdesc(kclass, args.precision, args.model),
-            "launches": launches, "avg_launch_ms": round(ms / max(launches, 1), 4),
-            "flop_per_launch": round(work / max(launches, 1)), "peak_note": note, "traffic_source": traffic_src,
-            "algorithmic_bytes_per_launch": alg_bytes,
-            "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic and alg_bytes else None}
+    alg_bytes = roof["algorithmic_bytes_per_launch"]
+    if kclass == "conv3x3" and args.model == "mdx23c":
+        # independent host-side model of the same bytes (mdx23c_conv3x3_alg_bytes) as a cross-check of libsesa's figure
+        per_fwd, l_fwd = 0.0, 0
+        for nb_ in [len(x) for x in _forward_sizes(chunks[0], batches[0], pworld)]:
+            b_, l_ = mdx23c_conv3x3_alg_bytes(members[0][1], nb_, member_prec["mdx23c"], f16_plan())
+            per_fwd += b_
+            l_fwd += l_
+        roof["algorithmic_bytes_host_model"] = round(per_fwd / max(l_fwd, 1))
+    roof.update(traffic=traffic, traffic_source=traffic_src, kernel=kdesc(kclass, args.precision, args.model),
+                traffic_over_algorithmic=round(traffic / alg_bytes, 3) if traffic and alg_bytes else None,
+                **{"class": kclass})
     path_tflops = path_flop * args.steps / elapsed / 1e12
 
     value = track_seconds * args.steps / elapsed
@@ -629,7 +701,7 @@ def main():
         if args.model == "ensemble":
             desc = [WORKLOAD["ensemble"] + f" [{args.blend}]: " + "; ".join(desc)]
         line = {
-            "metric": METRIC[args.model],
+            "metric": METRIC[args.model] + (f" -- rank-0 share of {pworld} ranks, one-GPU rehearsal" if sim else ""),
             "value": round(value, 3), "unit": "separated-audio sec/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
@@ -638,13 +710,23 @@ def main():
                                    f"host mix -> H2D -> separation -> stems D2H",
                        "model": args.model, "chunks": n_chunks,
                        "exec_batch": batches[0] if len(batches) == 1 else batches,
-                       "parallelism": f"chunk-shard x{world} + RCCL all_gather" if world > 1 else "1 GPU",
+                       "parallelism": (f"chunk-shard x{world} + RCCL gather to rank 0" if world > 1 else
+                                       f"1 GPU: rank 0's share of a {pworld}-rank chunk shard (rehearsal, no "
+                                       f"collective)" if sim else "1 GPU"),
                        "shard": {"world_size": dist.get_world_size() if world > 1 else 1,
                                  "backend": dist.get_backend() if world > 1 else None,
-                                 "chunk_ranges": shard_ranges[0] if len(shard_ranges) == 1 else shard_ranges},
+                                 "chunk_ranges": shard_ranges[0] if len(shard_ranges) == 1 else shard_ranges,
+                                 **({"rehearsal_world": pworld} if sim else {})},
                        "path_tflops_algorithmic": round(path_tflops, 2)},
             "roofline": roof,
         }
+        if sim:
+            line["rehearsal"] = {
+                "world": pworld, "rank0_chunks": shard_ranges[0][0][1] - shard_ranges[0][0][0] if len(names) == 1
+                else [r[0][1] - r[0][0] for r in shard_ranges],
+                "note": f"value = track seconds / rank 0's wall time for its share (gather -> forwards -> local OLA -> "
+                        f"assemble + finalise, no collective): the compute ceiling of a {pworld}-GPU run, which "
+                        f"adds the RCCL gather of the other ranks' spans to rank 0"}
         # north_star evidence: HBM GB/s of the streaming kernels (STFT / iSTFT / chunk gather + OLA),
         # algorithmic bytes / event-timed kernel time, against the 8 TB/s HBM3E peak
         hbm = {}
@@ -675,6 +757,11 @@ def main():
             kms, kn, kw = _native.profile_read(kc)
             if kn:
                 classes[kc] = {"ms_per_step": round(kms / args.steps, 2), "launches": kn}
+                if kc in roofs:   # the compute classes' own rooflines (bound by intensity, floor fraction)
+                    classes[kc].update({k: roofs[kc][k] for k in ("bound", "achieved", "unit", "frac", "flop_per_byte",
+                                                                   "floor_frac", "algorithmic_bytes_per_launch")})
+                elif kc in hbm:
+                    classes[kc].update(bound="hbm", achieved=hbm[kc]["achieved_gbs"], unit="GB/s", frac=hbm[kc]["frac"])
         line["kernel_classes"] = classes
         if "bs_roformer" in names or "htdemucs" in names:
             ams, alaunch, awork = _native.profile_read("attn")

@@ -323,13 +323,20 @@ int sesa_flac_encode(const float* in, int64_t frames, int channels, int sample_r
 #define SESA_KCLASS_TOKGEMM 8 /* token-major Linear layers (transformer models)           */
 #define SESA_KCLASS_ATTN 9    /* flash attention (work = 4 L^2 d FLOP per sequence-head)    */
 #define SESA_KCLASS_LSTM 10   /* SCNet bi-LSTM recurrence (work = h W_hh^T FLOP)            */
-#define SESA_KCLASS_SIMT 11   /* SCNet fp32 convolutions / feature-conversion DFTs          */
+#define SESA_KCLASS_SIMT 11   /* fp32 VALU kernels: SCNet convolutions / feature-conversion DFTs, HTDemucs DConv */
 #define SESA_KCLASS_OLA 12    /* chunk gather / overlap-add / finalize (work = HBM bytes)     */
 #define SESA_KCLASS_HCONV 13  /* HTDemucs implicit-GEMM convolutions (tok_gemm conv mode)    */
 #define SESA_KCLASS_CONV3X3_X3 14 /* MDX23C fp16 modes: the TFC 3x3 convs that stay bf16x3 (plan '3', T < 32) */
 #define SESA_KCLASS_COUNT 15
 int sesa_profile_enable(int enable);   /* 1: start recording (clears previous records), 0: stop */
 int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work);
+/* as sesa_profile_read, plus the class's ALGORITHMIC HBM bytes (each operand read once, each result written once,
+ * in the storage type the launch actually reads / writes) for the compute classes -- the bytes the roofline's
+ * HBM floor is priced on (0 for a launch that states none) */
+int sesa_profile_read2(int kclass, double* total_ms, int64_t* launches, double* total_work, double* total_bytes);
+/* sum over the class's launches of max(work / (peak_tflops 1e12), bytes / (peak_gbs 1e9)) in ms: the class's time at
+ * the roofline bound of each launch's own arithmetic intensity */
+int sesa_profile_floor(int kclass, double peak_tflops, double peak_gbs, double* floor_ms);
 
 #ifdef __cplusplus
 }

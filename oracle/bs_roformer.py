@@ -92,7 +92,7 @@ def param_names(cfg):
     return out
 
 
-def synth_params(cfg, affine="random"):
+def synth_params(cfg, affine="random", seed=0):
     """Name-keyed synthetic weights (oracle/weights.py scheme); rotary freqs are the real ones;
     Linear biases U(+-1/sqrt(fan_in)) of their weight (affine='random') or 0; gammas U(0.5,1.5) or 1."""
     from .weights import param_rng, synth_param
@@ -106,11 +106,11 @@ def synth_params(cfg, affine="random"):
         elif name.endswith(".bias") and (name[:-5] + ".weight") in shapes and affine == "random":
             fan_in = shapes[name[:-5] + ".weight"][1]
             b = 1.0 / math.sqrt(fan_in)
-            out[name] = param_rng(name).uniform(-b, b, size=shape).astype(np.float32)
+            out[name] = param_rng(name, seed).uniform(-b, b, size=shape).astype(np.float32)
         elif name.endswith(".bias"):
             out[name] = np.zeros(shape, np.float32)
         else:
-            out[name] = synth_param(name, shape, affine)
+            out[name] = synth_param(name, shape, affine, seed)
     return out
 
 

@@ -93,7 +93,7 @@ def param_names(cfg):
     return out
 
 
-def synth_params(cfg, affine="random"):
+def synth_params(cfg, affine="random", seed=0):
     """Name-keyed synthetic weights (oracle/weights.py scheme).  Conv/Linear/LSTM weights
     U(+-1/sqrt(prod(shape[1:]))); their biases U(+-1/sqrt(fan_in of the weight)) (affine='random')
     or 0; GroupNorm gamma U(0.5, 1.5) / beta U(-0.2, 0.2) (affine='random') or 1 / 0."""
@@ -107,11 +107,11 @@ def synth_params(cfg, affine="random"):
             fan_in = int(np.prod(shapes[wname][1:]))
             if affine == "random":
                 b = 1.0 / math.sqrt(fan_in)
-                out[name] = param_rng(name).uniform(-b, b, size=shape).astype(np.float32)
+                out[name] = param_rng(name, seed).uniform(-b, b, size=shape).astype(np.float32)
             else:
                 out[name] = np.zeros(shape, np.float32)
         else:
-            out[name] = synth_param(name, shape, affine)
+            out[name] = synth_param(name, shape, affine, seed)
     return out
 
 

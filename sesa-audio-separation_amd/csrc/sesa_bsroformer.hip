@@ -707,7 +707,7 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
     if (rc) return;
     void* t0 = profile_begin(st);
     rc = launch_tok_gemm(a, h16 ? 2 : x3, st);
-    profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(gm, rows));
+    profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(gm, rows), tok_gemm_bytes(a, gm, h16 ? 2 : x3));
   };
   const int64_t rowsBT = (int64_t)B * T;
   const float* bs_in = spec;
@@ -815,7 +815,8 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
       }
       void* t0 = profile_begin(st);
       rc = launch_attention(a, f16 ? 2 : x3, st);   // fp16: QK^T / PV on one fp16 pass
-      profile_end(t0, st, SESA_KCLASS_ATTN, 4.0 * (double)a.n_seq * c.heads * (double)a.L * a.L * c.dim_head);
+      profile_end(t0, st, SESA_KCLASS_ATTN, 4.0 * (double)a.n_seq * c.heads * (double)a.L * a.L * c.dim_head,
+                  attention_bytes(a, f16 ? 2 : x3));
     }
     {
       TokGemmArgs a = gemm_args(m, L.out, AO, m->inner, X, dim, M);

@@ -1281,7 +1281,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     hipLaunchKernelGGL(htd_norm_time_kernel, blocks((int64_t)B * L), dim3(kT), 0, st, x, ach, L, (int64_t)B * L, st_t,
                        XT0);
     SESA_CHECK_LAUNCH();
-    profile_end(tok, st, SESA_KCLASS_SIMT, 4.0 * B * (3.0 * nf + 3.0 * nt + 4.0 * L));
+    // branch normalisation: a few FLOPs per element; bytes: each branch input read twice (stats, apply), written once
+    profile_end(tok, st, SESA_KCLASS_SIMT, 4.0 * B * ((double)nf + nt), 4.0 * B * (3.0 * nf + 3.0 * nt + 4.0 * L));
   }
 
   // ---- GEMM helpers ----
@@ -1337,7 +1338,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
               gm.groups[0].N, gm.groups[0].K, g.n_taps, Cin, phases, glu, act, x2 != nullptr);
     void* t0 = profile_begin(st);
     rc = launch_tok_gemm(a, cx, st);
-    profile_end(t0, st, SESA_KCLASS_HCONV, gemm_flops(gm, a.M));
+    profile_end(t0, st, SESA_KCLASS_HCONV, gemm_flops(gm, a.M), tok_gemm_bytes(a, gm, cx));
   };
   auto lin = [&](const Gemm& gm, const float* xin, int64_t x_ld, float* o, int64_t o_ld, int64_t M, int act,
                  const float* residual, int kclass) {
@@ -1357,7 +1358,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     a.act = act;
     void* t0 = profile_begin(st);
     rc = launch_tok_gemm(a, cx, st);   // (fp16mix: fp32 rows rounded to fp16 in the staging)
-    profile_end(t0, st, kclass, gemm_flops(gm, M));
+    profile_end(t0, st, kclass, gemm_flops(gm, M), tok_gemm_bytes(a, gm, cx));
   };
   // 1x1 rewrite + GLU (:114-118 of HEncLayer): the plain token GEMM (2 % faster end to end than the
   // one-tap conv-mode GEMM, profiles/r03_htd_rw_*.json; SESA_HTD_REWRITE_CONV=1 selects the latter)
@@ -1382,7 +1383,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     a.glu = 1;
     void* t0 = profile_begin(st);
     rc = launch_tok_gemm(a, cx, st);
-    profile_end(t0, st, SESA_KCLASS_HCONV, gemm_flops(gm, M));
+    profile_end(t0, st, SESA_KCLASS_HCONV, gemm_flops(gm, M), tok_gemm_bytes(a, gm, cx));
   };
   auto dconv = [&](const std::vector<DcLayer>& layers, float* X, int rows, int Tn, int C, int h) {
     if (rc) return;
@@ -1413,7 +1414,9 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
           set_error("htdemucs: DConv conv launch failed");
           return;
         }
-        profile_end(t0, st, SESA_KCLASS_HCONV, 2.0 * rows * Tn * (double)h * 3.0 * C);
+        // fp32 VALU (no MFMA): the simt class, priced against the vector peak; X read once, U written once
+        profile_end(t0, st, SESA_KCLASS_SIMT, 2.0 * rows * Tn * (double)h * 3.0 * C,
+                    4.0 * rows * Tn * ((double)C + h) + 12.0 * C * h);
       } else {
         // dilated k3 conv over T (padding = dilation) -> U [rows][T][h] (+ bias), bf16x3 MFMA
         conv_gemm(Ly.conv, X, C, nullptr, U, h, P1, Tn, P1, Tn, 1, C, {0, 0, 0}, {-Ly.dil, 0, Ly.dil}, TOK_ACT_NONE,
@@ -1456,7 +1459,9 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         set_error("htdemucs: DConv launch failed");
         return;
       }
-      profile_end(tok, st, SESA_KCLASS_SIMT, 2.0 * rows * Tn * (2.0 * h * 2 * C + 0.5 * h * h));
+      // bytes: U read once, X read and written once (the residual update in place)
+      profile_end(tok, st, SESA_KCLASS_SIMT, 2.0 * rows * Tn * (2.0 * h * 2 * C + 0.5 * h * h),
+                  4.0 * rows * Tn * ((double)h + 2.0 * C));
     }
   };
 
@@ -1570,14 +1575,14 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       a.act = act;
       void* t0 = profile_begin(st);
       rc = launch_tok_gemm(a, l16 ? 2 : x3, st);
-      profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(gm, M));
+      profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(gm, M), tok_gemm_bytes(a, gm, l16 ? 2 : x3));
     };
     {
       void* tok = profile_begin(st);
       ln(X, X, Mx, m->nin_g, m->nin_b, Wb + m->pos_x, m->Nx);   // norm_in + pos_emb_2d (:203-204)
       ln(XT, XT, Mt, m->nint_g, m->nint_b, Wb + m->pos_t, m->Nt);
       SESA_CHECK_LAUNCH();
-      profile_end(tok, st, SESA_KCLASS_SIMT, 0.0);
+      profile_end(tok, st, SESA_KCLASS_SIMT, 8.0 * (double)(Mx + Mt) * D, 8.0 * (double)(Mx + Mt) * D);
     }
     const int heads = c.t_heads, dh = D / heads;
     auto attn = [&](const float* q, int64_t q_ld, const float* kv, int64_t kv_ld, int k_off, int v_off, float* o,
@@ -1622,7 +1627,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       }
       void* t0 = profile_begin(st);
       rc = launch_attention(a, att16 ? 2 : x3, st);
-      profile_end(t0, st, SESA_KCLASS_ATTN, 4.0 * (double)B * heads * (double)Lq * Lk * dh);
+      profile_end(t0, st, SESA_KCLASS_ATTN, 4.0 * (double)B * heads * (double)Lq * Lk * dh,
+                  attention_bytes(a, att16 ? 2 : x3));
     };
     auto gn_out = [&](float* Xs, int64_t ntok, int64_t g, int64_t b, double* sts) {
       if (rc) return;
@@ -1636,7 +1642,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
                          dim3(kT), 0, st, Xs, n_item, sts);
       hipLaunchKernelGGL(htd_gn_apply_kernel, blocks(B * n_item), dim3(kT), 0, st, Xs, n_item, D, sts, Wb + g, Wb + b,
                          (int64_t)B * n_item);
-      profile_end(tok, st, SESA_KCLASS_SIMT, 0.0);
+      profile_end(tok, st, SESA_KCLASS_SIMT, 8.0 * (double)B * n_item, 8.0 * (double)B * n_item);
     };
     const int act = c.t_gelu ? TOK_ACT_GELU : TOK_ACT_RELU;
     auto ff_block = [&](const TLayer& Ly, float* Xs, float* Hs, int64_t M, int64_t ng, int64_t nb) {

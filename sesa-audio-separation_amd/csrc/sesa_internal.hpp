@@ -18,5 +18,7 @@ namespace sesa {
 // launch timing hooks (sesa_profile.hip): token = profile_begin(st); <launch>; profile_end(token, ...)
 bool profiling();
 void* profile_begin(hipStream_t st);
-void profile_end(void* token, hipStream_t st, int kclass, double work);
+// work: algorithmic FLOPs (compute classes) or bytes (streaming classes); bytes: the algorithmic HBM bytes of a
+// compute-class launch (0: not stated)
+void profile_end(void* token, hipStream_t st, int kclass, double work, double bytes = 0.0);
 }  // namespace sesa

@@ -466,8 +466,29 @@ struct Fwd {
                        : w.kind == CONV2X2S2 ? SESA_KCLASS_DOWN : SESA_KCLASS_UP;
     void* tok = profile_begin(st);
     rc = launch_conv(w.kind, w.bn, w.f16 ? w.f16c : x3, a, B, st);
-    profile_end(tok, st, kclass,
-                2.0 * B * T_out * F_out * (double)w.n_cols * (w.C_in * taps + (xin ? xin->C_in : 0)));
+    if (tok) {
+      // algorithmic HBM bytes: every input element read once in the form the kernel reads it, the output
+      // (+ residual) once, the weight image once
+      const int64_t pin = (int64_t)B * T_in * F_in;
+      const bool one = w.f16 || x3 == 0;
+      double bytes = src_bytes(in.src[0], pin, in.C_split, one) + src_bytes(in.src[1], pin, in.C_in - in.C_split, one);
+      if (xin)
+        bytes += src_bytes(xin->src[0], pin, xin->C_split, x3 == 0) +
+                 src_bytes(xin->src[1], pin, xin->C_in - xin->C_split, x3 == 0);
+      bytes += (double)B * T_out * F_out * w.n_cols * 4.0 * (residual ? 2.0 : 1.0);
+      const double wb = w.f16 ? (w.f16c == 3 ? 2.0 : 4.0) : (x3 ? 4.0 : 2.0);
+      bytes += (double)w.n_cols * (w.C_in * taps * wb + (xin ? xin->C_in * (x3 ? 4.0 : 2.0) : 0.0));
+      profile_end(tok, st, kclass,
+                  2.0 * B * T_out * F_out * (double)w.n_cols * (w.C_in * taps + (xin ? xin->C_in : 0)), bytes);
+    }
+  }
+
+  // bytes of `ch` channels of one conv source over `pos` positions, read once: pre-split planes 2 B (one plane:
+  // fp16, or bf16 single pass) / 4 B (hi + lo), fp32 sources 4 B (+ 4 B for the SRC_MUL multiplier)
+  static double src_bytes(const Src& s, int64_t pos, int ch, bool one_plane) {
+    if (ch <= 0) return 0.0;
+    const double per = s.mode == SRC_PRE ? (s.lo && !one_plane ? 4.0 : 2.0) : s.mode == SRC_MUL ? 8.0 : 4.0;
+    return (double)pos * ch * per;
   }
 
   // transposed_io 0: first Linear (NHWC in, U^T [B][T][C][F/bn] out); 1: second Linear (U^T in, NHWC out)
@@ -485,7 +506,12 @@ struct Fwd {
     a.u_planes = u_planes;
     void* tok = profile_begin(st);
     rc = launch_tdf(w.f16 ? 2 : x3, a, B, st, transposed_io);
-    profile_end(tok, st, SESA_KCLASS_TDF, 2.0 * B * T * (double)w.M * w.K * C);
+    // algorithmic bytes: the fp32 input rows (K features) read once, the fp32 output rows (M features) + residual
+    // written / read once, the weight image once (fp16 2 B, bf16x3 4 B per coefficient)
+    const double rows = (double)B * T * C;
+    profile_end(tok, st, SESA_KCLASS_TDF, 2.0 * B * T * (double)w.M * w.K * C,
+                rows * w.K * 4.0 + rows * w.M * 4.0 * (residual ? 2.0 : 1.0) +
+                    (double)w.M * w.K * (w.f16 ? 2.0 : (x3 ? 4.0 : 2.0)));
   }
 
   // One act_split pass: GELU(InstanceNorm_affine(a [++ b])) -> bf16 hi/lo planes, returned as the

@@ -12,7 +12,8 @@ namespace sesa {
 namespace {
 struct Rec {
   int kclass;
-  double work;
+  double work;   // algorithmic FLOPs (MFMA / VALU classes) or bytes (streaming classes)
+  double bytes;  // algorithmic HBM bytes of a compute-class launch (its operands read once, results written once)
   hipEvent_t e0, e1;
 };
 std::mutex g_mu;
@@ -42,12 +43,12 @@ void* profile_begin(hipStream_t st) {
   return e;
 }
 
-void profile_end(void* token, hipStream_t st, int kclass, double work) {
+void profile_end(void* token, hipStream_t st, int kclass, double work, double bytes) {
   if (!token) return;
   std::lock_guard<std::mutex> lk(g_mu);
   hipEvent_t e1 = get_event();
   (void)hipEventRecord(e1, st);
-  g_recs.push_back(Rec{kclass, work, (hipEvent_t)token, e1});
+  g_recs.push_back(Rec{kclass, work, bytes, (hipEvent_t)token, e1});
 }
 
 }  // namespace sesa
@@ -68,9 +69,14 @@ extern "C" int sesa_profile_enable(int enable) {
 }
 
 extern "C" int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work) {
+  return sesa_profile_read2(kclass, total_ms, launches, total_work, nullptr);
+}
+
+extern "C" int sesa_profile_read2(int kclass, double* total_ms, int64_t* launches, double* total_work,
+                                  double* total_bytes) {
   clear_error();
   std::lock_guard<std::mutex> lk(g_mu);
-  double ms = 0, work = 0;
+  double ms = 0, work = 0, bytes = 0;
   int64_t n = 0;
   for (auto& r : g_recs) {
     if (r.kclass != kclass) continue;
@@ -79,10 +85,29 @@ extern "C" int sesa_profile_read(int kclass, double* total_ms, int64_t* launches
     SESA_CHECK_HIP(hipEventElapsedTime(&t, r.e0, r.e1));
     ms += t;
     work += r.work;
+    bytes += r.bytes;
     ++n;
   }
   if (total_ms) *total_ms = ms;
   if (launches) *launches = n;
   if (total_work) *total_work = work;
+  if (total_bytes) *total_bytes = bytes;
+  return SESA_OK;
+}
+
+// Sum over the class's launches of each launch's roofline floor, max(work / peak FLOP rate, bytes / peak HBM rate), in
+// ms: the time the class would take if every launch ran at the bound of its own arithmetic intensity (a class mixes
+// launches on both sides of the ridge, so this is tighter than the floor of the summed work and bytes).
+extern "C" int sesa_profile_floor(int kclass, double peak_tflops, double peak_gbs, double* floor_ms) {
+  clear_error();
+  SESA_REQUIRE(floor_ms && peak_tflops > 0 && peak_gbs > 0, SESA_ERR_INVALID, "sesa_profile_floor: bad arguments");
+  std::lock_guard<std::mutex> lk(g_mu);
+  double f = 0;
+  for (auto& r : g_recs) {
+    if (r.kclass != kclass) continue;
+    const double tc = r.work / (peak_tflops * 1e12), tm = r.bytes / (peak_gbs * 1e9);
+    f += (tc > tm ? tc : tm) * 1e3;
+  }
+  *floor_ms = f;
   return SESA_OK;
 }

@@ -1783,6 +1783,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
   auto blocks = [](int64_t n) { return dim3((unsigned)((n + kST - 1) / kST)); };
   // 3x3 conv over (F, T), padding 1, as an implicit GEMM (K = 9 taps x C): A = x (+ S on load), bias,
   // optional GLU over interleaved column pairs (FusionLayer)
+  double conv3_bytes = 0;   // algorithmic bytes of the last conv3_gemm launch (profiling)
   auto conv3_gemm = [&](const Gemm& gm, const float* xin, const float* S, int F, int C, float* o, int o_ld, int glu) {
     TokGemmArgs a{};
     a.x = xin;
@@ -1812,6 +1813,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
       a.bn64 = 1;
       a.n_tiles_n = (gm.groups[0].N + 63) / 64;
     }
+    conv3_bytes = tok_gemm_bytes(a, gm, gx);
     return launch_tok_gemm(a, gx, st);
   };
 
@@ -1835,6 +1837,9 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     float* skip = F32(pl.skip[i]);
     void* tok = profile_begin(st);
     double fl = 0;
+    // algorithmic bytes of the simt group: the level input read once and the band outputs written once, then
+    // every ConvolutionModule layer reads and writes its rows once
+    double by = 4.0 * B * T * ((double)L.Fin * L.Cin + (double)L.Fout * L.Cout);
     for (int b = 0; b < 3; ++b) {
       const BandConv& bc = L.sd[b];
       const int64_t total = (int64_t)B * bc.n_out * T * (L.Cout / 4);
@@ -1889,14 +1894,15 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
           SESA_CHECK_LAUNCH();
         }
         fl += 2.0 * rows * T * (6.0 * L.h * L.Cout + 3.0 * L.h + (double)L.h * L.Cout);
+        by += 8.0 * rows * T * L.Cout;
       }
     }
     if (scn_conv3_mfma()) {  // globalconv (3x3) -> bufA on the token GEMM's conv mode
-      profile_end(tok, st, SESA_KCLASS_SIMT, fl);
+      profile_end(tok, st, SESA_KCLASS_SIMT, fl, by);
       tok = profile_begin(st);
       rc = conv3_gemm(L.gc_gm, skip, nullptr, L.Fout, L.Cout, bufA, L.Cout, 0);
       if (rc) return rc;
-      profile_end(tok, st, SESA_KCLASS_TOKGEMM, 2.0 * B * L.Fout * T * L.Cout * L.Cout * 9);
+      profile_end(tok, st, SESA_KCLASS_TOKGEMM, 2.0 * B * L.Fout * T * L.Cout * L.Cout * 9, conv3_bytes);
       cur = bufA;
       continue;
     }
@@ -1916,8 +1922,9 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
       hipLaunchKernelGGL(scn_conv3x3_kernel, grid, dim3(kST), 0, st, a);
       SESA_CHECK_LAUNCH();
       fl += 2.0 * B * L.Fout * T * L.Cout * L.Cout * 9;
+      by += 8.0 * B * L.Fout * T * L.Cout;
     }
-    profile_end(tok, st, SESA_KCLASS_SIMT, fl);
+    profile_end(tok, st, SESA_KCLASS_SIMT, fl, by);
     cur = bufA;
   }
   // 3. separation net (separation.py:107-113): X in bufA, [B][Fn][T][d]
@@ -1961,7 +1968,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         a.act = TOK_ACT_NONE;
         void* t0 = profile_begin(st);
         rc = launch_tok_gemm(a, gx, st);
-        profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(L.ih[path], rows));
+        profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(L.ih[path], rows), tok_gemm_bytes(a, L.ih[path], gx));
         if (rc) return rc;
       }
       // recurrence: path 0 = frequency path, sequences (b, t) over f; path 1 = time path, (b, f) over t
@@ -1992,7 +1999,8 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         if (lstm_mfma_on(H)) launch_lstm_mfma(a, m->d_w + L.whh_frag[path], st);
         else launch_lstm(a, st);
         SESA_CHECK_LAUNCH();
-        profile_end(t0, st, SESA_KCLASS_LSTM, 2.0 * rows * 2 * 4 * H * (double)H);
+        // bytes: the input-projection gates read once, the hidden outputs written once (W_hh stays on chip)
+        profile_end(t0, st, SESA_KCLASS_LSTM, 2.0 * rows * 2 * 4 * H * (double)H, 4.0 * rows * (8.0 * H + 2.0 * H));
       }
       // Linear(2H -> d) + residual, in place
       {
@@ -2011,7 +2019,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         a.act = TOK_ACT_NONE;
         void* t0 = profile_begin(st);
         rc = launch_tok_gemm(a, gx, st);
-        profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(L.lin[path], rows));
+        profile_end(t0, st, SESA_KCLASS_TOKGEMM, gemm_flops(L.lin[path], rows), tok_gemm_bytes(a, L.lin[path], gx));
         if (rc) return rc;
       }
     }
@@ -2027,7 +2035,9 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
       hipLaunchKernelGGL(scn_irfft_kernel, grid, dim3(kST), 0, st, X, K, Ch, m->d_twT, scale, Y);
     }
     SESA_CHECK_LAUNCH();
-    profile_end(tok, st, SESA_KCLASS_SIMT, 4.0 * B * Fn * (double)K * T * (i % 2 ? d / 2 : d));
+    // bytes: the layer's activations read once and the converted ones written once
+    profile_end(tok, st, SESA_KCLASS_SIMT, 4.0 * B * Fn * (double)K * T * (i % 2 ? d / 2 : d),
+                4.0 * B * Fn * ((double)T * d + (double)K * d));
     std::swap(X, Y);
   }
   // 4. decoder (scnet.py:363-366): X [B][F_{i+1}][T][C_{i+1}] -> [B][F_i][T][Cdec_i]
@@ -2035,10 +2045,12 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     const Level& L = m->lv[m->nl - 1 - j];
     void* tok = profile_begin(st);
     double fl = 0;
+    // simt bytes: the band transposed convs read the fused level once and write the level output once
+    double by = 4.0 * B * T * ((double)L.Fout * L.Cout + (double)L.Fin * L.Cdec);
     if (scn_conv3_mfma()) {  // FusionLayer: x + skip on load, 3x3 C -> 2C, GLU
       rc = conv3_gemm(L.fu_gm, X, F32(pl.skip[m->nl - 1 - j]), L.Fout, L.Cout, Y, L.Cout, 1);
       if (rc) return rc;
-      profile_end(tok, st, SESA_KCLASS_TOKGEMM, 2.0 * B * L.Fout * T * 2.0 * L.Cout * L.Cout * 9);
+      profile_end(tok, st, SESA_KCLASS_TOKGEMM, 2.0 * B * L.Fout * T * 2.0 * L.Cout * L.Cout * 9, conv3_bytes);
       tok = profile_begin(st);
     } else {
     C3Args a{};
@@ -2058,6 +2070,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     hipLaunchKernelGGL(scn_conv3x3_kernel, grid, dim3(kST), 0, st, a);
     SESA_CHECK_LAUNCH();
     fl = 2.0 * B * L.Fout * T * 2.0 * L.Cout * 2.0 * L.Cout * 9;
+    by += 12.0 * B * L.Fout * T * L.Cout;
     }
     for (int b = 0; b < 3; ++b) {
       const BandConv& bc = L.su[b];
@@ -2067,7 +2080,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
       SESA_CHECK_LAUNCH();
       fl += 2.0 * total * 4 * L.Cout * ((bc.kern + bc.stride - 1) / bc.stride);
     }
-    profile_end(tok, st, SESA_KCLASS_SIMT, fl);
+    profile_end(tok, st, SESA_KCLASS_SIMT, fl, by);
   }
   // 5. iSTFT (scnet.py:367-373)
   {

@@ -210,4 +210,43 @@ inline int upload_groups(Gemm& gm) {
 int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st);
 int launch_attention(const AttnArgs& a, int x3, hipStream_t st);
 
+// ---- algorithmic HBM bytes (the roofline's HBM floor, sesa_profile_read2) ----
+// One tok_gemm launch: A read once in the form the kernel reads it (fp32 rows 4 B; pre-split planes 2 B per plane
+// read: fp16 / bf16 single pass one plane, bf16x3 hi + lo), conv mode the input grid once (+ the skip operand), the
+// weight image once (bf16x3 hi + lo 4 B per coefficient, else 2 B), the output once (fp32 4 B, or the split
+// epilogue's plane(s)) and the residual once.  x3: 0 bf16, 1 bf16x3, 2 fp16 (launch_tok_gemm's argument).
+inline double tok_gemm_bytes(const TokGemmArgs& a, const Gemm& gm, int x3) {
+  double k_sum = 0, n_out = 0, wcoef = 0;
+  const int ng = a.n_groups > 0 ? a.n_groups : (int)gm.groups.size();
+  for (int i = 0; i < ng && i < (int)gm.groups.size(); ++i) {
+    const TokGroup& g = gm.groups[i];
+    k_sum += g.K;
+    n_out += a.glu ? g.N / 2 : g.N;
+    wcoef += (double)g.N * g.K;
+  }
+  const double M = a.M;
+  double in;
+  if (a.conv) {
+    const double items = M / ((double)a.geo.P1 * a.geo.P2);
+    in = items * a.geo.Q1 * a.geo.Q2 * a.geo.Cin * 4.0 * (a.geo.x2 ? 2.0 : 1.0);
+  } else if (a.a_hi) {
+    in = M * k_sum * (a.a_lo && x3 == 1 ? 4.0 : 2.0);
+  } else {
+    in = M * k_sum * 4.0;
+  }
+  const double w = wcoef * (x3 == 1 ? 4.0 : 2.0);
+  const double out = M * n_out * (a.out_hi ? (a.out_lo ? 4.0 : 2.0) : 4.0) + (a.residual ? M * n_out * 4.0 : 0.0);
+  return in + w + out;
+}
+
+// One attention launch: Q, K, V (and the gate logits) read once in the form the kernel reads them (one fp16 plane
+// 2 B, bf16 hi + lo planes 4 B, fp32 rows 4 B), the output written once (fp16 plane 2 B, bf16 planes 4 B, fp32 4 B).
+inline double attention_bytes(const AttnArgs& a, int x3) {
+  const double dh = a.dh > 0 ? a.dh : 64, heads = a.heads, L = a.L, Lk = a.Lk > 0 ? a.Lk : a.L, ns = a.n_seq;
+  const double q_e = a.qkv16 ? 2.0 : a.qkv_hi ? (a.qkv_lo && x3 == 1 ? 4.0 : 2.0) : 4.0;
+  const double kv_e = (a.kv ? a.kv16 : a.qkv16) ? 2.0 : (a.kv ? a.kv_hi : a.qkv_hi) ? (x3 == 1 ? 4.0 : 2.0) : 4.0;
+  const double o_e = a.out_hi ? (a.out_f16 || x3 != 1 ? 2.0 : 4.0) : 4.0;
+  return ns * heads * (L * dh * q_e + 2.0 * Lk * dh * kv_e + L * dh * o_e + (a.g_off >= 0 ? L * q_e : 0.0));
+}
+
 }  // namespace sesa

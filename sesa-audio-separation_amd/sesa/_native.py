@@ -112,6 +112,9 @@ SIGNATURES = {
     "sesa_profile_enable": (c_int, [c_int]),
     "sesa_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
                                   ctypes.POINTER(ctypes.c_double)]),
+    "sesa_profile_read2": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "sesa_profile_floor": (c_int, [c_int, ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
 }
 
 KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6, "act": 7, "tokgemm": 8,
@@ -127,6 +130,22 @@ def profile_read(kclass):
     check(lib().sesa_profile_read(KCLASS[kclass] if isinstance(kclass, str) else kclass, ctypes.byref(ms),
                                   ctypes.byref(n), ctypes.byref(work)), "sesa_profile_read")
     return ms.value, n.value, work.value
+
+
+def profile_read2(kclass):
+    """(ms, launches, algorithmic work, algorithmic HBM bytes) of a kernel class (sesa_profile_read2)."""
+    ms, n, work, nb = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+    check(lib().sesa_profile_read2(KCLASS[kclass] if isinstance(kclass, str) else kclass, ctypes.byref(ms),
+                                   ctypes.byref(n), ctypes.byref(work), ctypes.byref(nb)), "sesa_profile_read2")
+    return ms.value, n.value, work.value, nb.value
+
+
+def profile_floor(kclass, peak_tflops, peak_gbs):
+    """Sum over the class's launches of max(FLOP / peak, bytes / HBM peak), ms (sesa_profile_floor)."""
+    f = ctypes.c_double()
+    check(lib().sesa_profile_floor(KCLASS[kclass] if isinstance(kclass, str) else kclass, float(peak_tflops),
+                                   float(peak_gbs), ctypes.byref(f)), "sesa_profile_floor")
+    return f.value
 
 
 class SesaError(RuntimeError):

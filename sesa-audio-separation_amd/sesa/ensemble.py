@@ -22,6 +22,9 @@ from . import _native as N
 from .audio_io import quantize_pcm, read_wav, write_audio
 
 METHODS = ["avg_wave", "median_wave", "max_wave", "min_wave", "max_fft", "min_fft", "median_fft"]
+# Member precisions of the configs[4] ensemble line (bench.py --model ensemble) and of its parity gate
+# (tests/test_ensemble_models.py: every blend method within 8e-5 of the reference on three fixtures).
+ENSEMBLE_PRECISIONS = {"mdx23c": "fp16mix", "bs_roformer": "fp16", "scnet": "fp16mix"}
 _SPECIAL = "[]()|&; "
 
 
@@ -47,15 +50,17 @@ def blend_device(waves, method, weights=None, buffer=32768):
 
 
 def ensemble_separate(members, mix_d, stem="vocals", method="avg_wave", weights=None, buffer=32768, rank=None,
-                      world=None, exec_batch=None, group=None, demix_hooks=None, blend_fn=None):
+                      world=None, exec_batch=None, group=None, demix_hooks=None, blend_fn=None, gather_to=0,
+                      simulate=False):
     """Multi-model ensemble of one track, all on the device (BASELINE configs[4]).
 
     The GUI's ensemble flow (processing.py:266-363 runs inference.py once per model, then
     ensemble.py blends the chosen stem files) without the per-model WAV round trip: every member
     ``(config, model)`` separates the device-resident mix [2, L] chunk-sharded over the process
-    group (sesa/parallel.py: contiguous chunk ranges per rank, one RCCL all_gather per model), the
-    members' ``stem`` outputs are stacked and blended with ``sesa_blend_f32`` (ensemble.py:258-407
-    semantics, float64).  Returns (blend [2, L] float64, {member index: stem [2, L] float32}).
+    group (sesa/parallel.py: contiguous chunk ranges per rank, one RCCL gather per model to rank
+    ``gather_to``), the members' ``stem`` outputs are stacked and blended with ``sesa_blend_f32``
+    (ensemble.py:258-407 semantics, float64) on that rank.  Returns (blend [2, L] float64, {member index:
+    stem [2, L] float32}) there and (None, {}) on the other ranks (``gather_to=None``: every rank blends).
     ``exec_batch``: chunks per forward, a list (one per member) or an int.  ``demix_hooks`` (local_fn /
     counter_fn / finalize_fn of demix_sharded) and ``blend_fn`` exist so the CPU test-suite can drive the
     sharding, the collectives and the member loop over gloo ranks with the oracle's OLA and blend."""
@@ -68,8 +73,11 @@ def ensemble_separate(members, mix_d, stem="vocals", method="avg_wave", weights=
             raise ValueError(f"ensemble member {i} has no '{stem}' stem (instruments: {names})")
         eb = exec_batch[i] if isinstance(exec_batch, (list, tuple)) else (exec_batch or 8)
         est = demix_sharded(cfg, model, mix_d, mix_d.device, rank=rank, world=world, exec_batch=eb, group=group,
-                            **(demix_hooks or {}))
-        stems.append(est[names.index(stem)])
+                            gather_to=gather_to, simulate=simulate, **(demix_hooks or {}))
+        if est is not None:
+            stems.append(est[names.index(stem)])
+    if not stems:
+        return None, {}
     x = torch.stack(stems)
     return (blend_fn or blend_device)(x, method, weights, buffer), {i: s for i, s in enumerate(stems)}
 

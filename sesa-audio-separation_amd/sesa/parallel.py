@@ -8,11 +8,15 @@ Chunks of the chunker/OLA are independent given the mix, so:
   utils.py:371-445 (C = samplerate * segment, no fades / pad, ``counter += 1``) -- and runs
   gather -> forward -> windowed OLA into a LOCAL span buffer of result rows covering only the
   samples its chunks touch ([start(lo_r), end(hi_r - 1)) of the padded track);
-* one ``all_gather_into_tensor`` of the fixed-size span buffers (RCCL, backend "nccl") -- the only
-  exchange; the seams (C - step samples between neighbours) are summed in rank order;
-* the counter is deterministic: every rank recomputes it for the whole plan with the same kernel
-  and chunk order as the single-GPU path (``sesa_ola_accumulate_f32`` with no result rows), so it
-  is bit-identical to it and is not exchanged; then ``result / counter`` is finalised.
+* one ``gather`` of the fixed-size span buffers to rank 0 (RCCL, backend "nccl": point-to-point
+  receives over rank 0's xGMI links) -- the only exchange; rank 0 sums the seams (C - step samples
+  between neighbours) in rank order.  Only rank 0 assembles and finalises: the other ranks receive
+  nothing (round 4 all-gathered every span to every rank, ~2.7 GB per rank for HTDemucs 30-min at
+  world 8, thrown away by all but rank 0).  ``gather_to=None`` keeps the all-gather form for callers
+  that want the stems on every rank;
+* the counter is deterministic: rank 0 recomputes it for the whole plan with the same kernel and
+  chunk order as the single-GPU path (``sesa_ola_accumulate_f32`` with no result rows), so it is
+  bit-identical to it and is not exchanged; then ``result / counter`` is finalised.
 
 Summation order at the seams differs from the reference's sequential chunk order only by the
 grouping of fp32 additions (rank partial sums), ~1e-7 relative.
@@ -163,27 +167,44 @@ def counter_device(plan, device):
     return counter
 
 
-def exchange_and_assemble(local, plan, rank, world, group=None):
-    """All-gather the span buffers and sum them into the full [rows, L_pad] result."""
+def exchange_and_assemble(local, plan, rank, world, group=None, gather_to=0, simulate=False):
+    """Gather the span buffers to rank ``gather_to`` (or all-gather them to every rank when it is None) and
+    sum them into the full [rows, L_pad] result; ranks that receive nothing return None.  ``simulate``: a
+    one-process rehearsal of rank ``rank``'s share of a ``world``-rank run (bench.py --rank-share): no
+    collective, only this rank's span is assembled."""
     rows, span_max = local.shape
-    if world > 1:
-        gathered = torch.empty(world * rows, span_max, device=local.device, dtype=local.dtype)
-        dist.all_gather_into_tensor(gathered, local.contiguous(), group=group)
-        gathered = gathered.view(world, rows, span_max)
+    local = local.contiguous()
+    if world > 1 and not simulate:
+        if gather_to is None:
+            gathered = torch.empty(world * rows, span_max, device=local.device, dtype=local.dtype)
+            dist.all_gather_into_tensor(gathered, local, group=group)
+            gathered = list(gathered.view(world, rows, span_max))
+        elif rank == gather_to:
+            gathered = [torch.empty_like(local) for _ in range(world)]
+            dist.gather(local, gathered, dst=gather_to if group is None else dist.get_global_rank(group, gather_to),
+                        group=group)
+        else:
+            dist.gather(local, None, dst=gather_to if group is None else dist.get_global_rank(group, gather_to),
+                        group=group)
+            return None
     else:
-        gathered = local[None]
+        gathered = {rank: local} if simulate else [local]
     full = torch.zeros(rows, plan["L_pad"], device=local.device, dtype=local.dtype)
     for r, (s, e) in enumerate(plan["spans"]):
-        if e > s:
-            full[:, s:e] += gathered[r, :, :e - s]
+        if e > s and (not simulate or r == rank):
+            full[:, s:e] += gathered[r][:, :e - s]
     return full
 
 
 def demix_sharded(config, model, mix_d, device=None, rank=None, world=None, exec_batch=8, group=None,
-                  local_fn=None, finalize_fn=None, counter_fn=None, mode="generic", streams=1):
+                  local_fn=None, finalize_fn=None, counter_fn=None, mode="generic", streams=1, gather_to=0,
+                  simulate=False):
     """Separate the device-resident mix [2, L] with chunks sharded across the process group.
     ``mode``: "generic" (inference_pytorch.demix_pytorch_optimized / utils.demix generic) or
-    "demucs" (utils.demix for model_type 'htdemucs').  Returns est [n_instr, 2, L] on every rank.
+    "demucs" (utils.demix for model_type 'htdemucs').  Returns est [n_instr, 2, L] on rank ``gather_to``
+    (every rank when ``gather_to`` is None) and None on the others.  ``simulate``: run only rank ``rank``'s
+    share of a ``world``-rank plan in this one process, no collective (the per-rank compute ceiling of a
+    multi-GPU run, measured on one GPU; its output is that share's samples only).
     ``local_fn`` / ``counter_fn`` / ``finalize_fn`` exist so the CPU test-suite can drive the
     sharding + collective + assembly with the oracle's OLA (gloo); the product path uses the HIP ops."""
     rank = dist.get_rank(group) if rank is None else rank
@@ -199,7 +220,9 @@ def demix_sharded(config, model, mix_d, device=None, rank=None, world=None, exec
         local = local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, streams)
     else:
         local = local_fn(config, model, mix_d, plan, rank, rows)
-    full = exchange_and_assemble(local, plan, rank, world, group)
+    full = exchange_and_assemble(local, plan, rank, world, group, gather_to, simulate)
+    if full is None:
+        return None
     counter = counter_device(plan, mix_d.device) if counter_fn is None else counter_fn(plan)
     if finalize_fn is None:
         from . import ops

@@ -11,7 +11,12 @@ vocals stems are blended by the reference ``AudioEnsembleEngine.process_waveform
 over run_ensemble's 32768-frame buffers (ensemble.py:258-407; weights normalised as :288-293).  The mix is
 3 s (132 300 samples, seed 13): 3 MDX23C chunks, 1 BS-Roformer chunk, 2 SCNet chunks.  ~2 min of CPU.
 
-Fixture: ensemble_full.npz  mix, vocals_<member>, blend_avg_wave (weights 0.5/0.3/0.2), blend_median_fft.
+Fixtures (round 5 adds two variants, and every blend method in each):
+  ensemble_full.npz         0.1-RMS mix, MDX23C unit affine, BS-Roformer / SCNet random affine, weight seed 0
+  ensemble_full_loud.npz    --variant loud:   the same mix scaled to 0.3 RMS
+  ensemble_full_wseed2.npz  --variant wseed2: 0.1-RMS mix, every member on weight seed 2 (random affine)
+Each holds mix, weights, vocals_<member>, blend_<method> for avg_wave (weights 0.5/0.3/0.2), median_wave,
+max_wave, min_wave, max_fft, min_fft, median_fft, plus mix_scale / weight_seed / affine_<member>.
 """
 import contextlib
 import io
@@ -65,7 +70,18 @@ def blend_ref(waves, method, weights=None, buffer=32768):
     return out
 
 
+METHODS = ("avg_wave", "median_wave", "max_wave", "min_wave", "max_fft", "min_fft", "median_fft")
+VARIANTS = {"base": ("ensemble_full.npz", 1.0, 0), "loud": ("ensemble_full_loud.npz", 3.0, 0),
+            "wseed2": ("ensemble_full_wseed2.npz", 1.0, 2)}
+
+
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", default="base", choices=sorted(VARIANTS))
+    args = ap.parse_args()
+    out_name, scale, seed = VARIANTS[args.variant]
+    mdx_affine = "unit" if seed == 0 else "random"
     mg.install_stubs()
     import make_golden_bsr as mgb
     import make_golden_scnet as mgs
@@ -73,23 +89,28 @@ def main():
     from pytorch_backend import PyTorchBackend
     _BE.append(PyTorchBackend(device="cpu", optimize_mode="default"))
     torch.set_num_threads(os.cpu_count())
-    mix = mg.mix_signal(13, L)
+    mix = (mg.mix_signal(13, L) * np.float32(scale)).astype(np.float32)
     stems = {}
     cfg = mg.load_cfg("config_vocals_mdx23c.yaml")
-    model, _ = mg.build_ref_model(cfg, "unit")
+    model, _ = mg.build_ref_model(cfg, mdx_affine, seed=seed)
     stems["mdx23c"] = demix_ref(model, cfg, mix)["vocals"]
     print("mdx23c done", flush=True)
     cfg = mgb._cfg("config_bs_roformer_vocals.yaml")
-    model, _ = mgb.build_ref(cfg, "random")
+    model, _ = mgb.build_ref(cfg, "random", seed)
     stems["bs_roformer"] = demix_ref(model, cfg, mix)["vocals"]
     print("bs_roformer done", flush=True)
     cfg = mgs._cfg("config_musdb18_scnet.yaml")
-    model, _ = mgs.build_ref(cfg, "random")
+    model, _ = mgs.build_ref(cfg, "random", seed)
     stems["scnet"] = demix_ref(model, cfg, mix)["vocals"]
     print("scnet done", flush=True)
     waves = np.stack([stems[k] for k in ("mdx23c", "bs_roformer", "scnet")]).astype(np.float64)
-    mg.save("ensemble_full.npz", mix=mix, weights=WEIGHTS, **{f"vocals_{k}": v for k, v in stems.items()},
-            blend_avg_wave=blend_ref(waves, "avg_wave", WEIGHTS), blend_median_fft=blend_ref(waves, "median_fft"))
+    # the reference blends are float64; stored as float32 (<= 1e-9 absolute here, against an 8e-5 RMS gate) to keep
+    # the three fixtures small
+    blends = {f"blend_{m}": blend_ref(waves, m, WEIGHTS if m == "avg_wave" else None).astype(np.float32)
+              for m in METHODS}
+    mg.save(out_name, mix=mix, weights=WEIGHTS, **{f"vocals_{k}": v for k, v in stems.items()}, **blends,
+            mix_scale=np.float32(scale), weight_seed=np.array(seed), affine_mdx23c=np.array(mdx_affine),
+            affine_bs_roformer=np.array("random"), affine_scnet=np.array("random"))
 
 
 if __name__ == "__main__":

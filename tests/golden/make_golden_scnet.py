@@ -37,10 +37,10 @@ def _cfg(name):
     return osc.load_cfg(os.path.join(mg.CFG_DIR, name))
 
 
-def build_ref(cfg, affine):
+def build_ref(cfg, affine, seed=0):
     from models.scnet import SCNet
     model = SCNet(**osc.model_kwargs(cfg)).eval()
-    sd = osc.synth_params(cfg, affine)
+    sd = osc.synth_params(cfg, affine, seed)
     ref_keys = [(k, tuple(v.shape)) for k, v in model.state_dict().items()]
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     return model, ref_keys

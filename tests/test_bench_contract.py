@@ -21,21 +21,37 @@ def test_default_precision():
     assert bench.default_precision("bs_roformer") == "fp16"
     for m in ("htdemucs", "scnet"):
         assert bench.default_precision(m) == "fp16mix"
-    # PMC stamps: the classes each model's fp16 mode puts on fp16 MFMA
-    assert bench.class_precision("hconv", "fp16mix", "htdemucs") == "fp16"
-    assert bench.class_precision("attn", "fp16mix", "htdemucs") == "fp16"
-    assert bench.class_precision("tokgemm", "fp16mix", "htdemucs") == "bf16x3"
-    assert bench.class_precision("tokgemm", "fp16mix", "scnet") == "fp16"
-    assert bench.class_precision("lstm", "fp16mix", "scnet") == "bf16x3"
-    assert bench.class_precision("simt", "fp16mix", "scnet") == "bf16x3"
-    assert bench.class_precision("conv3x3", "fp16") == "fp16"
-    assert bench.class_precision("tokgemm", "fp16") == "bf16x3"
-    assert bench.class_precision("tokgemm", "fp16", "bs_roformer") == "fp16"
-    assert bench.class_precision("attn", "fp16mix", "ensemble") == "fp16"
-    assert bench.class_precision("attn", "fp16", "htdemucs") == "bf16x3"
-    assert bench.class_precision("conv3x3", "fp16mix") == "fp16mix"
-    assert bench.class_precision("hconv", "fp16", "ensemble") == "bf16x3"
-    assert bench.class_precision("tokgemm", "bf16") == "bf16"
+    # PMC stamps / roofline pass counts: the arithmetic each class's launches run in
+    cp = bench.class_precision
+    assert cp("hconv", "fp16mix", "htdemucs") == "fp16"
+    assert cp("attn", "fp16mix", "htdemucs") == "fp16"
+    assert cp("tokgemm", "fp16mix", "htdemucs") == "fp16"       # HTDemucs fp16mix Linears: one fp16 pass
+    assert cp("tokgemm", "fp16mix", "scnet") == "fp16"
+    assert cp("lstm", "fp16mix", "scnet") == "bf16x3"
+    assert cp("simt", "fp16mix", "scnet") == "fp32"              # VALU kernels
+    assert cp("conv3x3", "fp16") == "fp16" and cp("conv3x3", "fp16mix") == "fp16"
+    assert cp("conv3x3", "fp16w2") == "fp16w2" and cp("conv3x3_x3", "fp16mix") == "bf16x3"
+    assert cp("tdf", "fp16mix") == "fp16" and cp("tdf", "fp16") == "bf16x3" and cp("act", "fp16mix") == "fp16mix"
+    assert cp("tokgemm", "fp16", "bs_roformer") == "fp16"
+    assert cp("tokgemm", "fp16w2", "bs_roformer") == "bf16x3"     # BS-Roformer has no fp16w2: built bf16x3
+    assert cp("attn", "fp16mix", "ensemble") == "fp16"
+    assert cp("attn", "fp16", "htdemucs") == "bf16x3"
+    assert cp("hconv", "fp16", "ensemble") == "bf16x3"
+    assert cp("tokgemm", "bf16", "bs_roformer") == "bf16"
+    assert cp("conv3x3", "bf16x3") == "bf16x3"
+    # the members a line actually built decide (bench.py passes them)
+    assert cp("tokgemm", "fp16mix", "ensemble", {"mdx23c": "bf16x3", "bs_roformer": "bf16x3", "scnet": "bf16x3"}) == "bf16x3"
+    assert cp("conv3x3", "fp16mix", "ensemble", {"mdx23c": "bf16x3", "bs_roformer": "fp16", "scnet": "fp16mix"}) == "bf16x3"
+
+
+def test_member_precision():
+    from sesa.ensemble import ENSEMBLE_PRECISIONS
+    for m in ("mdx23c", "bs_roformer", "scnet"):
+        assert bench.member_precision(m, "fp16mix", "ensemble") == ENSEMBLE_PRECISIONS[m]
+    assert bench.member_precision("bs_roformer", "fp16mix") == "fp16"
+    assert bench.member_precision("scnet", "fp16") == "bf16x3"
+    assert bench.member_precision("mdx23c", "fp16w2") == "fp16w2"
+    assert bench.member_precision("htdemucs", "fp16w2") == "bf16x3"
 
 
 def test_conv3x3_alg_bytes_by_precision():

@@ -82,36 +82,57 @@ def test_ensemble_separate_rejects_missing_stem():
 
 FULL_MEMBERS = (("mdx23c", "config_vocals_mdx23c.yaml"), ("bs_roformer", "config_bs_roformer_vocals.yaml"),
                 ("scnet", "config_musdb18_scnet.yaml"))
+ENSEMBLE_FIXTURES = ("ensemble_full.npz", "ensemble_full_loud.npz", "ensemble_full_wseed2.npz")
+BLEND_METHODS = ("avg_wave", "median_wave", "max_wave", "min_wave", "max_fft", "min_fft", "median_fft")
+# north_star's gate is 1e-4 per-sample RMS; the configs[4] blends are held to 8e-5 so that the bench precisions
+# keep a 20 % margin (round-4 median_fft sat at 9.29e-5 of 1e-4 on the quiet fixture)
+BLEND_GATE = 8e-5
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("precisions", [("bf16x3", "bf16x3", "bf16x3"), ("fp16mix", "fp16", "fp16mix")],
-                         ids=["bf16x3", "bench"])
-def test_full_width_ensemble_matches_reference(golden, precisions):
-    """BASELINE configs[4] at full width: the three full-size members (the bench line's precisions: MDX23C
-    fp16mix, BS-Roformer fp16, SCNet fp16mix -- and all bf16x3) on a 3 s mix, each stem and the
-    avg_wave (weighted) / median_fft blends against the REAL reference composition
-    (tests/golden/make_golden_ensemble_full.py: reference demix_pytorch_optimized per member, reference
-    AudioEnsembleEngine blend).  Gate: per-sample RMS <= 1e-4."""
-    from sesa.ensemble import ensemble_separate
+def _full_members(g, precisions):
     from sesa.utils import get_model_from_config
     from sesa.weights import synth_model_state, synth_state_dict
-    g = golden("ensemble_full.npz")
-    dev = torch.device("cuda:0")
+    seed = int(g["weight_seed"]) if "weight_seed" in g.files else 0
     members = []
     for (kind, cfg_name), prec in zip(FULL_MEMBERS, precisions):
         m, c = get_model_from_config(kind, os.path.join(CONFIGS, cfg_name))
-        m.load_state_dict(synth_state_dict(m, affine="unit") if kind == "mdx23c" else
-                          synth_model_state(m, affine="random"), strict=True)
+        affine = str(g[f"affine_{kind}"]) if f"affine_{kind}" in g.files else ("unit" if kind == "mdx23c" else "random")
+        m.load_state_dict(synth_state_dict(m, affine=affine, seed=seed) if kind == "mdx23c" else
+                          synth_model_state(m, affine=affine, seed=seed), strict=True)
         m.set_precision(prec)
         members.append((c, m))
+    return members
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fixture", ENSEMBLE_FIXTURES)
+@pytest.mark.parametrize("precisions", ["bf16x3", "bench"])
+def test_full_width_ensemble_matches_reference(golden, fixture, precisions):
+    """BASELINE configs[4] at full width: the three full-size members on a 3 s mix -- in bf16x3, and in the
+    precisions the configs[4] bench line runs them (sesa.ensemble.ENSEMBLE_PRECISIONS) -- each stem and EVERY
+    blend method against the REAL reference composition (tests/golden/make_golden_ensemble_full.py: reference
+    demix_pytorch_optimized per member, reference AudioEnsembleEngine blend over 32768-frame buffers), on three
+    fixtures: the 0.1-RMS mix, the same mix at 0.3 RMS, and a second weight draw.  Gate: stems <= 1e-4, blends
+    <= BLEND_GATE (8e-5) per-sample RMS."""
+    from sesa.ensemble import ENSEMBLE_PRECISIONS, blend_device, ensemble_separate
+    g = golden(fixture)
+    dev = torch.device("cuda:0")
+    precs = ("bf16x3",) * 3 if precisions == "bf16x3" else tuple(ENSEMBLE_PRECISIONS[k] for k, _ in FULL_MEMBERS)
+    members = _full_members(g, precs)
     mix_d = torch.from_numpy(g["mix"]).to(dev)
-    for method, key, w in (("avg_wave", "blend_avg_wave", list(g["weights"])), ("median_fft", "blend_median_fft", None)):
-        out, stems = ensemble_separate(members, mix_d, "vocals", method, weights=w, rank=0, world=1, exec_batch=2)
-        for i, (kind, _) in enumerate(FULL_MEMBERS):
-            err = rms(stems[i].cpu().numpy(), g[f"vocals_{kind}"])
-            print(f"{precisions} {kind} stem rms {err:.3e}")
-            assert err <= 1e-4, kind
-        err = rms(out.cpu().numpy(), g[key])
-        print(f"{precisions} {method} blend rms {err:.3e}")
-        assert out.shape == g[key].shape and err <= 1e-4
+    out, stems = ensemble_separate(members, mix_d, "vocals", "avg_wave", weights=list(g["weights"]), rank=0, world=1,
+                                   exec_batch=2)
+    worst = 0.0
+    for i, (kind, _) in enumerate(FULL_MEMBERS):
+        err = rms(stems[i].cpu().numpy(), g[f"vocals_{kind}"])
+        print(f"{fixture} {precs} {kind} stem rms {err:.3e}")
+        assert err <= 1e-4, kind
+    x = torch.stack([stems[i] for i in range(len(FULL_MEMBERS))])
+    keys = [m for m in BLEND_METHODS if f"blend_{m}" in g.files]
+    assert "avg_wave" in keys and "median_fft" in keys
+    for method in keys:
+        y = out if method == "avg_wave" else blend_device(x, method)
+        err = rms(y.cpu().numpy(), g[f"blend_{method}"])
+        worst = max(worst, err)
+        print(f"{fixture} {precs} {method} blend rms {err:.3e}")
+        assert y.shape == g[f"blend_{method}"].shape and err <= BLEND_GATE, method

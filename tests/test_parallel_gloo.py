@@ -122,9 +122,16 @@ def _worker(rank, world, port, bs, q, mode="generic", L=L_TRACK):
         else:
             est = demix_sharded(cfg, StandIn(), mix, rank=rank, world=world,
                                 local_fn=cpu_local, finalize_fn=cpu_finalize, counter_fn=make_cpu_counter(cfg),
-                                mode=mode)
+                                mode="generic" if mode == "allgather" else mode,
+                                gather_to=None if mode == "allgather" else 0)
+            if mode == "allgather":           # every rank holds the stems; they must agree with rank 0's
+                ref0 = est.clone()
+                dist.broadcast(ref0, 0)
+                assert torch.equal(est, ref0)
         if rank == 0:
             q.put(est.numpy())
+        elif mode != "allgather":
+            assert est is None                # gather to rank 0: the other ranks receive nothing
     finally:
         dist.destroy_process_group()
 
@@ -235,3 +242,33 @@ def test_world8_ensemble_two_members():
     ref = blend(np.stack([v1, v2]), "avg_wave", [0.6, 0.4], 32768)
     assert est.shape == ref.shape
     assert np.abs(est - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max())
+
+
+def test_allgather_form_matches_single_process():
+    """gather_to=None: the all-gather form (stems on every rank), world 3."""
+    from oracle.demix import demix as odemix
+    est = _run_world(3, "allgather")
+    ref = odemix(_cfg(1), StandIn(), _mix(), batch_size=1)
+    ref = np.stack([ref["vocals"], ref["other"]])
+    assert np.abs(est - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_rank_share_rehearsal_sums_to_whole(world):
+    """simulate=True (bench.py --rank-share): each rank's share run alone in one process, no collective.
+    The shares' finalised outputs sum to the whole track's (finalisation is a division by the shared
+    counter), so the per-rank rehearsal does exactly its share of the work."""
+    from oracle.demix import demix as odemix
+    from sesa.parallel import demix_sharded, shard_plan
+    cfg = _cfg(1)
+    mix = torch.from_numpy(_mix())
+    total = None
+    for r in range(world):
+        est = demix_sharded(cfg, StandIn(), mix, rank=r, world=world, local_fn=cpu_local, finalize_fn=cpu_finalize,
+                            counter_fn=make_cpu_counter(cfg), simulate=True)
+        total = est.numpy().astype(np.float64) if total is None else total + est.numpy()
+    ref = odemix(cfg, StandIn(), _mix(), batch_size=1)
+    ref = np.stack([ref["vocals"], ref["other"]])
+    assert np.abs(total - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max())
+    plan = shard_plan(cfg, L_TRACK, world)
+    assert sum(hi - lo for lo, hi in plan["ranges"]) == len(plan["flat"])
