@@ -455,8 +455,56 @@ def parity_leg(names, members, dev):
                        "weight_seed": seed, "affine": affine}
             worst = max(worst, err)
             del m
-    return {"gate": 1e-4, "within_gate": worst <= 1e-4, "worst_rms": worst, "fixtures": out,
-            "reference": "tests/golden/<fixture> (reference classes in fp32 on CPU, same name-keyed weights)"}
+    res = {"gate": 1e-4, "within_gate": worst <= 1e-4, "worst_rms": worst, "fixtures": out,
+           "reference": "tests/golden/<fixture> (reference classes in fp32 on CPU, same name-keyed weights)"}
+    if names == list(ENSEMBLE):
+        res["blend"] = ensemble_blend_parity({nm: m.precision for nm, (m, _, _) in zip(names, members)}, dev)
+        res["within_gate"] = res["within_gate"] and res["blend"]["worst_rms"] <= res["blend"]["gate"]
+    return res
+
+
+ENSEMBLE_FIXTURES = ("ensemble_full.npz", "ensemble_full_loud.npz", "ensemble_full_wseed2.npz")
+BLEND_METHODS = ("avg_wave", "median_wave", "max_wave", "min_wave", "max_fft", "min_fft", "median_fft")
+
+
+def ensemble_blend_parity(precisions, dev):
+    """configs[4] blend parity: the three full-width members in the precisions the line ran, on the reference's own
+    compositions (tests/golden/make_golden_ensemble_full.py: reference demix_pytorch_optimized per member, reference
+    AudioEnsembleEngine blend) of a 0.1-RMS mix, the same mix at 0.3 RMS and a second weight draw -- every blend
+    method (rms / rel / max), gated at 8e-5 (tests/test_ensemble_models.py)."""
+    from sesa.ensemble import blend_device, ensemble_separate
+    from sesa.utils import get_model_from_config
+    from sesa.weights import synth_model_state, synth_state_dict
+    out, worst = {}, 0.0
+    for fx in ENSEMBLE_FIXTURES:
+        g = np.load(os.path.join(REPO, "tests", "golden", fx), allow_pickle=False)
+        seed = int(g["weight_seed"])
+        members = []
+        for nm in ENSEMBLE:
+            m, c = get_model_from_config(nm, os.path.join(CFG_DIR, MODELS[nm][0]))
+            aff = str(g[f"affine_{nm}"])
+            m.load_state_dict(synth_state_dict(m, affine=aff, seed=seed) if nm == "mdx23c" else
+                              synth_model_state(m, affine=aff, seed=seed), strict=True)
+            m.set_precision(precisions[nm])
+            members.append((c, m))
+        blend0, stems = ensemble_separate(members, torch.from_numpy(g["mix"]).to(dev), "vocals", "avg_wave",
+                                          weights=list(g["weights"]), rank=0, world=1, exec_batch=2)
+        x = torch.stack([stems[i] for i in range(len(members))])
+        rec = {"input_rms": float(np.sqrt(np.mean(np.asarray(g["mix"], np.float64) ** 2))), "weight_seed": seed}
+        for i, nm in enumerate(ENSEMBLE):
+            ref = g[f"vocals_{nm}"].astype(np.float64)
+            y = stems[i].cpu().numpy().astype(np.float64)
+            rec[f"stem_{nm}"] = {"rms": float(np.sqrt(np.mean((y - ref) ** 2)))}
+        for meth in BLEND_METHODS:
+            y = (blend0 if meth == "avg_wave" else blend_device(x, meth)).cpu().numpy().astype(np.float64)
+            ref = g[f"blend_{meth}"].astype(np.float64)
+            err = float(np.sqrt(np.mean((y - ref) ** 2)))
+            rec[meth] = {"rms": err, "rel_rms": err / float(np.sqrt(np.mean(ref ** 2))),
+                         "max_abs": float(np.abs(y - ref).max())}
+            worst = max(worst, err)
+        out[fx] = rec
+        del members
+    return {"gate": 8e-5, "worst_rms": worst, "precisions": precisions, "fixtures": out}
 
 
 def synth_weights(model):
@@ -772,7 +820,7 @@ def main():
             line["parity"] = parity_leg(names, members, dev)
             line["parity_rms"] = line["parity"]["worst_rms"]
         if world == 1 and not args.no_cpu_baseline:
-            parts = [cpu_baseline(nm, cp, c, track_seconds, args.cpu_sample_chunks if len(names) == 1 else 2,
+            parts = [cpu_baseline(nm, cp, c, track_seconds, args.cpu_sample_chunks,
                                   config0=len(names) == 1 and not args.cpu_chunks_only)
                      for nm, (_, _, cp), c in zip(names, members, chunks)]
             if len(parts) == 1:

@@ -9,6 +9,16 @@
  * returns 0 on success or a negative SESA_ERR_* code with a thread-local message available
  * from sesa_last_error().
  *
+ * Concurrency: the network forwards (sesa_mdx23c_forward, sesa_bsr_forward, sesa_scnet_forward,
+ * sesa_htdemucs_forward) take all mutable state from the caller's workspace -- measured independent of its
+ * prior contents and writing nothing outside their buffers (tools/ws_guard.py, every model / precision) -- and
+ * are bit-reproducible run to run on one stream.  They are NOT re-entrant across streams of one device: with
+ * forwards of one handle in flight on 2-4 streams at once, 3 of 9 runs on MI355X differed from the one-stream
+ * result by up to 1.2e-3, while every configuration that device-synchronised after all launches but those of any
+ * one kernel class agreed bit for bit (tools/streams_bisect.py, profiles/r05_streams_bisect.txt); the cause is not
+ * found.  Callers serialise forwards on one stream per device (sesa/parallel.py refuses streams > 1); the other
+ * entry points (STFT / iSTFT / gather / OLA / blend) are plain streaming kernels without shared state.
+ *
  * Compute is fp32 in / fp32 out.  The MDX23C network runs its contractions on MFMA in one of
  * two precisions (sesa_mdx23c_config.precision):
  *   SESA_PREC_BF16X3 -- hi/lo bf16 split, 3 MFMA passes, fp32 accumulate (parity mode:
@@ -20,9 +30,10 @@
  *                       contraction bf16x3 (MDX23C only; the other models accept BF16X3 / BF16)
  *   SESA_PREC_F16MIX -- MDX23C: those convs per level as the plan of sesa_mdx23c_set_f16_plan says
  *                       (default: one fp16 pass everywhere except the encoder level-1 convs, bf16x3 --
- *                       they carry ~70 % of the fp16 rounding error at the stems);
+ *                       they carry ~70 % of the fp16 rounding error at the stems), the decoder TDF Linears fp16;
  *                       HTDemucs: the cross-transformer attention (QK^T, PV; fp32 softmax statistics),
- *                       the implicit-GEMM convs and 1x1 rewrites on one fp16 pass, the Linears bf16x3;
+ *                       the implicit-GEMM convs, 1x1 rewrites and the transformer / channel Linears on one fp16
+ *                       pass (norms and DConv statistics fp32 / fp64);
  *                       SCNet: the token GEMMs (3x3 convs, LSTM input projections, Linears) on one fp16
  *                       pass, the LSTM recurrence bf16x3
  */

@@ -53,6 +53,7 @@
 #include <cstdlib>
 #include <map>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "sesa_common.hpp"
@@ -307,9 +308,13 @@ __global__ void __launch_bounds__(kT) htd_dc_conv_valu_kernel(const float* __res
 int dc_valu_h(int h) { return h > kDcVMaxH ? 0 : h <= 6 ? 6 : h <= 8 ? 8 : h <= 12 ? 12 : 16; }
 
 // Per (t-block, row): G = gelu(gn1(U)) into LDS, then entry e of (sum G | sum G G^T) summed over the
-// block's positions in fp64 and added to the row's totals.
+// block's positions in fp64 and added to the row's totals.  Round 5: the block's positions are cut into
+// S = kT / nS slices, thread (slice s, entry e) sums its slice (fp64 products of the fp32 G values, as before) and
+// the S partials meet in LDS -- at h = 6 (27 entries) the round-4 form kept 27 of 256 threads busy with
+// 128-long dependent fp64 FMA chains (80 ms per 30-min step); the sums are regrouped, not rounded differently.
 __global__ void __launch_bounds__(kT) htd_dc_gram_kernel(DcArgs a) {
   __shared__ float Gs[kDcG][kDcMaxH + 1];
+  __shared__ double part[kT];
   const int row = blockIdx.y;
   const int t0 = blockIdx.x * kDcG;
   const int T = a.T, h = a.h;
@@ -323,20 +328,166 @@ __global__ void __launch_bounds__(kT) htd_dc_gram_kernel(DcArgs a) {
   }
   __syncthreads();
   const int nS = dc_ns(h);
-  for (int e = threadIdx.x; e < nS; e += kT) {
+  const int S = nS >= kT ? 1 : min(kT / nS, 16);       // position slices (entries x slices <= kT)
+  for (int e0 = 0; e0 < nS; e0 += kT) {
+    const int e = e0 + (nS >= kT ? threadIdx.x : threadIdx.x % nS);
+    const int sl = nS >= kT ? 0 : threadIdx.x / nS;
     double acc = 0.0;
-    if (e < h) {
-      for (int p = 0; p < np; ++p) acc += (double)Gs[p][e];
-    } else {
-      int j = 0, r = e - h;
-      while (r >= h - j) {
-        r -= h - j;
-        ++j;
+    if (e < nS && sl < S) {
+      const int p0 = sl * np / S, p1 = (sl + 1) * np / S;
+      if (e < h) {
+        for (int p = p0; p < p1; ++p) acc += (double)Gs[p][e];
+      } else {
+        int j = 0, r = e - h;
+        while (r >= h - j) {
+          r -= h - j;
+          ++j;
+        }
+        const int k = j + r;
+        for (int p = p0; p < p1; ++p) acc = fma((double)Gs[p][j], (double)Gs[p][k], acc);
       }
-      const int k = j + r;
-      for (int p = 0; p < np; ++p) acc = fma((double)Gs[p][j], (double)Gs[p][k], acc);
     }
-    atomicAdd(&a.gram[(int64_t)row * nS + e], acc);
+    if (S == 1) {
+      if (e < nS) atomicAdd(&a.gram[(int64_t)row * nS + e], acc);
+      continue;
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < nS) {
+      double tot = 0.0;
+      for (int q = 0; q < S; ++q) tot += part[q * nS + threadIdx.x];
+      atomicAdd(&a.gram[(int64_t)row * nS + threadIdx.x], tot);
+    }
+  }
+}
+
+// htd_dc_apply_kernel's work as a streaming kernel over channel groups: thread (position lane pl, channel group cq)
+// keeps CPT channels' W2 columns (a and gate halves), GroupNorm-2 affine, LayerScale in registers and walks the
+// workgroup's positions pl, pl + PL, ... four at a time, each X read / write one 16-B (CPT 4) or 8-B (CPT 2) access:
+// every lane busy (the round-4 kernel mapped lane = channel, idling 16 of 64 lanes at C = 48) and four positions'
+// loads in flight per thread (it kept one 4-B load per lane in flight, ~15 % of the HBM rate at level 0).
+// Same arithmetic per channel as htd_dc_apply_kernel (same fma order), so the output is bit-identical.
+template <int HM, int CPT>
+__global__ void __launch_bounds__(kT) htd_dc_apply_q_kernel(DcArgs a) {
+  __shared__ __attribute__((aligned(16))) float Gs[kDcP][HM];
+  __shared__ double red[2 * (kT / 64)];
+  const int row = blockIdx.y;
+  const int t0 = blockIdx.x * kDcP;
+  const int T = a.T, C = a.C, h = a.h;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float m1, r1;
+  gn_stats(a.st1 + 2 * row, (double)T * h, m1, r1);
+  float m2, r2;
+  {
+    const int nS = dc_ns(h);
+    const double* gr = a.gram + (int64_t)row * nS;
+    const double* coefS = a.gc;
+    const double* wbar = a.gc + (nS - h);
+    const double* v2 = wbar + h;
+    double s1 = 0.0, s2 = 0.0;
+    for (int e = threadIdx.x; e < nS; e += kT) {
+      if (e < h) {
+        s1 += wbar[e] * gr[e];
+        s2 += v2[e] * gr[e];
+      } else {
+        s2 += coefS[e - h] * gr[e];
+      }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+      s1 += __shfl_xor(s1, o);
+      s2 += __shfl_xor(s2, o);
+    }
+    if (lane == 0) {
+      red[2 * wv] = s1;
+      red[2 * wv + 1] = s2;
+    }
+    __syncthreads();
+    s1 = 0.0;
+    s2 = 0.0;
+    for (int i = 0; i < kT / 64; ++i) {
+      s1 += red[2 * i];
+      s2 += red[2 * i + 1];
+    }
+    const double sb = a.gc[nS + h], sbb = a.gc[nS + h + 1];
+    const double n = (double)T * 2 * C;
+    const double mu = (s1 + (double)T * sb) / n;
+    const double var = fmax((s2 + (double)T * sbb) / n - mu * mu, 0.0);
+    m2 = (float)mu;
+    r2 = (float)(1.0 / sqrt(var + 1e-5));
+  }
+  for (int i = threadIdx.x; i < kDcP * HM; i += kT) {   // pad columns h .. HM are zero
+    const int p = i / HM, j = i - p * HM;
+    const int t = t0 + p;
+    float g = 0.f;
+    if (t < T && j < h) {
+      const float u = a.U[((int64_t)row * T + t) * h + j];
+      g = gelu_erf((u - m1) * r1 * a.g1[j] + a.be1[j]);
+    }
+    Gs[p][j] = g;
+  }
+  __syncthreads();
+  const int NQ = C / CPT, PL = kT / NQ;                 // channel groups, position lanes (host: NQ <= kT)
+  const int pl = threadIdx.x / NQ, cq = threadIdx.x - pl * NQ;
+  if (pl >= PL) return;
+  const int c0 = cq * CPT;
+  float wa[CPT][HM], wg[CPT][HM], ba[CPT], bg[CPT], ga[CPT], gg[CPT], oa[CPT], og[CPT], sc[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const int c = c0 + q;
+#pragma unroll
+    for (int j = 0; j < HM; ++j) {
+      wa[q][j] = j < h ? a.W2t[(int64_t)j * 2 * C + c] : 0.f;
+      wg[q][j] = j < h ? a.W2t[(int64_t)j * 2 * C + C + c] : 0.f;
+    }
+    ba[q] = a.b2[c];
+    bg[q] = a.b2[C + c];
+    ga[q] = a.g2[c] * r2;
+    gg[q] = a.g2[C + c] * r2;
+    oa[q] = a.be2[c];
+    og[q] = a.be2[C + c];
+    sc[q] = a.scale[c];
+  }
+  using VT = std::conditional_t<CPT == 4, float4, std::conditional_t<CPT == 2, float2, float>>;
+  constexpr int UP = 4;                                  // positions in flight per thread
+  float* xrow = a.X + (int64_t)row * T * C + c0;
+  for (int pb = pl; pb < kDcP; pb += UP * PL) {
+    VT xv[UP];
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int p = pb + u * PL, t = t0 + p;
+      if (p < kDcP && t < T) xv[u] = *reinterpret_cast<const VT*>(xrow + (int64_t)t * C);
+    }
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int p = pb + u * PL, t = t0 + p;
+      if (p >= kDcP || t >= T) continue;
+      float va[CPT], vg[CPT];
+#pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        va[q] = ba[q];
+        vg[q] = bg[q];
+      }
+#pragma unroll
+      for (int j4 = 0; j4 < HM; j4 += 4) {
+        const float4 g = *reinterpret_cast<const float4*>(&Gs[p][j4]);
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+          va[q] = fmaf(wa[q][j4], g.x, va[q]);
+          vg[q] = fmaf(wg[q][j4], g.x, vg[q]);
+          va[q] = fmaf(wa[q][j4 + 1], g.y, va[q]);
+          vg[q] = fmaf(wg[q][j4 + 1], g.y, vg[q]);
+          va[q] = fmaf(wa[q][j4 + 2], g.z, va[q]);
+          vg[q] = fmaf(wg[q][j4 + 2], g.z, vg[q]);
+          va[q] = fmaf(wa[q][j4 + 3], g.w, va[q]);
+          vg[q] = fmaf(wg[q][j4 + 3], g.w, vg[q]);
+        }
+      }
+      float* xe = reinterpret_cast<float*>(&xv[u]);
+#pragma unroll
+      for (int q = 0; q < CPT; ++q)
+        xe[q] = xe[q] + sc[q] * (fmaf(va[q] - m2, ga[q], oa[q]) * sigm(fmaf(vg[q] - m2, gg[q], og[q])));
+      *reinterpret_cast<VT*>(xrow + (int64_t)t * C) = xv[u];
+    }
   }
 }
 
@@ -1450,7 +1601,13 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       hipLaunchKernelGGL(htd_dc_gram_kernel, dim3((unsigned)((Tn + kDcG - 1) / kDcG), (unsigned)rows), dim3(kT), 0, st,
                          a);
       const dim3 ga((unsigned)((Tn + kDcP - 1) / kDcP), (unsigned)rows);
-      if (h <= 8) hipLaunchKernelGGL(htd_dc_apply_kernel<8>, ga, dim3(kT), 0, st, a);
+      // the channel-group streaming form where its registers allow (SESA_HTD_DCAPPLY=0: the round-4 kernel, A/B)
+      static const bool apq = !(getenv("SESA_HTD_DCAPPLY") && std::string(getenv("SESA_HTD_DCAPPLY")) == "0");
+      if (apq && h <= 8 && C % 4 == 0 && C / 4 <= kT) hipLaunchKernelGGL((htd_dc_apply_q_kernel<8, 4>), ga, dim3(kT), 0, st, a);
+      else if (apq && h <= 16 && C % 2 == 0 && C / 2 <= kT)
+        hipLaunchKernelGGL((htd_dc_apply_q_kernel<16, 2>), ga, dim3(kT), 0, st, a);
+      else if (apq && h <= 32 && C <= kT) hipLaunchKernelGGL((htd_dc_apply_q_kernel<32, 1>), ga, dim3(kT), 0, st, a);
+      else if (h <= 8) hipLaunchKernelGGL(htd_dc_apply_kernel<8>, ga, dim3(kT), 0, st, a);
       else if (h <= 16) hipLaunchKernelGGL(htd_dc_apply_kernel<16>, ga, dim3(kT), 0, st, a);
       else if (h <= 32) hipLaunchKernelGGL(htd_dc_apply_kernel<32>, ga, dim3(kT), 0, st, a);
       else hipLaunchKernelGGL(htd_dc_apply_kernel<64>, ga, dim3(kT), 0, st, a);

@@ -2,7 +2,9 @@
 // kernel class live inside the timed region.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "sesa_common.hpp"
@@ -35,6 +37,22 @@ hipEvent_t get_event() {
 
 bool profiling() { return g_on; }
 
+// SESA_DEBUG_SYNC (diagnostic, tools/streams_bisect.py): "all" -- hipDeviceSynchronize after every libsesa launch,
+// so no two launches ever run concurrently; "except:<k>" -- after every launch except those of kernel class k, so
+// only class k's launches overlap work on other streams.  Unset: nothing.
+namespace {
+int debug_sync_mode() {   // -2 off, -1 all, k >= 0 all but class k
+  static const int v = [] {
+    const char* e = getenv("SESA_DEBUG_SYNC");
+    if (!e) return -2;
+    if (std::string(e) == "all") return -1;
+    if (std::string(e).rfind("except:", 0) == 0) return atoi(e + 7);
+    return -2;
+  }();
+  return v;
+}
+}  // namespace
+
 void* profile_begin(hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_on) return nullptr;
@@ -44,6 +62,8 @@ void* profile_begin(hipStream_t st) {
 }
 
 void profile_end(void* token, hipStream_t st, int kclass, double work, double bytes) {
+  const int dbg = debug_sync_mode();
+  if (dbg != -2 && dbg != kclass) (void)hipDeviceSynchronize();
   if (!token) return;
   std::lock_guard<std::mutex> lk(g_mu);
   hipEvent_t e1 = get_event();

@@ -484,10 +484,17 @@ __global__ void __launch_bounds__(kThreads, 2) tap_gemm_kernel(ConvArgs a) {
 // holds only the images the mode reads (one A, one W: 55 KB); the shortcut stages keep their bf16 hi / lo
 // layout (78 KB), so a stage is the larger of the two.
 constexpr int kActMaxC = 1024;
+// MDMA (MI4 only): the main chunks are staged by LDS-DMA (buffer_load ... lds) instead of through VGPRs: each lane's
+// source offset for its halo slot is computed ONCE per tile (out-of-image halo slots get an offset past num_records,
+// so the hardware writes zeros -- no clamping, masking or select per chunk), the chunk advance is folded into the
+// buffer resource base (SALU), and one counted wait + barrier per chunk replaces the register staging
+// (load_item / store_main: ~200 VALU and 7 ds_write_b128 per thread per chunk).  The A image is padded to whole
+// 1-KiB DMA pieces (37 KiB), so a stage is 55 KiB and two stages sit in the same LDS as before.
 template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0, bool MI4 = false, int SCR = 0,
-          int SCD = 2, bool ORD = false>
+          int SCD = 2, bool ORD = false, int MDMA = 0>
 __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   static_assert(F16 == 0 || X3, "the fp16 modes keep the shortcut chunks bf16x3");
+  static_assert(!MDMA || (MI4 && F16 == 1 && !ACT), "MDMA: the fp16 32-row tile on pre-activated planes");
   static_assert(!MI4 || (F16 == 1 && !ACT), "MI4: fp16 single pass on pre-activated planes");
   static_assert(!SCR || (XTRA && X3), "SCR: the bf16x3 fused shortcut from registers / per-wave LDS-DMA");
   static_assert(SCR != 2 || MI4, "SCR 2: the 32-row tile (one wave = 4 rows of 32 positions)");
@@ -501,7 +508,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   constexpr int W_BYTES = 9 * BN * 32;
   constexpr int W1_BYTES = BN * 32;
   // main stage: [A hi][A lo if ALO][W hi][W lo if WLO]; shortcut stage: [A hi][A lo][W1 hi][W1 lo]
-  constexpr int WOFF_M = (ALO ? 2 : 1) * A_BYTES;
+  constexpr int A_IMG_M = MDMA ? (A_BYTES + 1023) / 1024 * 1024 : A_BYTES;   // MDMA: whole 1-KiB pieces
+  constexpr int WOFF_M = MDMA ? A_IMG_M : (ALO ? 2 : 1) * A_BYTES;
   constexpr int WOFF_X = 2 * A_BYTES;
   constexpr int STAGE_M = WOFF_M + (WLO ? 2 : 1) * W_BYTES;
   constexpr int STAGE_X = XTRA ? WOFF_X + 2 * W1_BYTES : 0;
@@ -770,15 +778,72 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   constexpr std::true_type kExt{};
 
   // ---- main chunks: straight-line pipelined body, clamped (redundant) prefetch at the tail ----
+  // MDMA: this wave's DMA pieces per chunk (A pieces first, then the W image's), wave-uniform piece index
+  constexpr int MD_A_PC = A_IMG_M / 1024, MD_PC = MD_A_PC + W_BYTES / 1024, MD_PPW = (MD_PC + 7) / 8;
+  uint32_t mdo[MDMA ? MD_PPW : 1];   // per-lane source byte offsets (A: from the chunk-0 plane base; W: image)
+  const int wv = __builtin_amdgcn_readfirstlane(wm);
+  auto md_issue = [&](int kc, char* stg) {
+    if constexpr (MDMA) {
+      const uint32_t plane_bytes = (uint32_t)((int64_t)a.T_in * a.F_in * C * 2);
+      const char* abase = reinterpret_cast<const char*>(src.hi + (int64_t)b * a.T_in * a.F_in * C) + kc * 32;
+      const char* wbase = reinterpret_cast<const char*>(wblk) + (int64_t)kc * 2 * W_BYTES;
+      const __amdgpu_buffer_rsrc_t ra =
+          __builtin_amdgcn_make_buffer_rsrc((void*)const_cast<char*>(abase), (short)0, (int)(plane_bytes - kc * 32), 0x00020000);
+      const __amdgpu_buffer_rsrc_t rw =
+          __builtin_amdgcn_make_buffer_rsrc((void*)const_cast<char*>(wbase), (short)0, W_BYTES, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < MD_PPW; ++i) {
+        // (the voffset as int: an unsigned lvalue here made the host pass silently drop this kernel's launch stub)
+        const int pc = wv + 8 * i;
+        if (pc < MD_A_PC)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(stg + pc * 1024), 16,
+                                                   (int)mdo[i], 0, 0, 0);
+        else if (pc < MD_PC)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rw, (__attribute__((address_space(3))) void*)(stg + WOFF_M + (pc - MD_A_PC) * 1024), 16, (int)mdo[i], 0, 0, 0);
+      }
+    }
+  };
   auto main_phase = [&]() __attribute__((always_inline)) {
-    load_main(0);
-    if constexpr (ACT) __syncthreads();   // the LDS affine table, before the first staging step reads it
-    store_main(smem, 0);
-    load_main(min(1, n_main - 1));
-    __syncthreads();
+    if constexpr (MDMA) {
+      // halo slot of lane l in A piece pc: position p = 32 pc + l / 2, LDS half-slot l & 1, which holds channel half
+      // (l & 1) ^ ((p >> 3) & 1) (the fragment reads' swizzle)
+      constexpr uint32_t kOOB = 0x80000000u;
+#pragma unroll
+      for (int i = 0; i < MD_PPW; ++i) {
+        const int pc = wv + 8 * i;
+        uint32_t v = kOOB;
+        if (pc < MD_A_PC) {
+          const int p = pc * 32 + (lane >> 1);
+          const int hr = p / HW, hc = p - hr * HW;
+          const int ti = t_in0 + hr, fi = f_in0 + hc;
+          const int hf = (lane & 1) ^ ((p >> 3) & 1);
+          if (p < NPOS && ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in)
+            v = (uint32_t)((((int64_t)ti * a.F_in + fi) * C + 8 * hf) * 2);
+        } else if (pc < MD_PC) {
+          v = (uint32_t)((pc - MD_A_PC) * 1024 + lane * 16);
+        }
+        mdo[i] = v;
+      }
+      md_issue(0, smem);
+    } else {
+      load_main(0);
+      if constexpr (ACT) __syncthreads();   // the LDS affine table, before the first staging step reads it
+      store_main(smem, 0);
+      load_main(min(1, n_main - 1));
+      __syncthreads();
+    }
     for (int kc = 0; kc < n_main; ++kc) {
       char* cur = smem + (kc & 1) * STAGE;
       char* nxt = smem + ((kc + 1) & 1) * STAGE;
+      if constexpr (MDMA) {
+        // chunk kc landed for every wave (each waits for its own pieces; the barrier joins them), and every wave's
+        // fragment reads of the other stage (chunk kc - 1) retired -- chunk kc + 1 goes there
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kc + 1 < n_main) md_issue(kc + 1, nxt);
+      }
       Frags fr[2];
       if constexpr (MI4) {
         // dx-major: the 6 halo-row A fragments of column shift dx, then the 3 dy taps (B double-buffered)
@@ -808,13 +873,16 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
             for (int i = 0; i < MI; ++i)
   #pragma unroll
               for (int j = 0; j < NI; ++j) acc[i][j] = mfma32h(ar[i + dy], bq[q & 1][j], acc[i][j]);
-            if (q == 1) {
-              store_main(nxt, min(kc + 1, n_main - 1));
-              load_main(min(kc + 2, n_main - 1));
+            if constexpr (!MDMA) {
+              if (q == 1) {
+                store_main(nxt, min(kc + 1, n_main - 1));
+                load_main(min(kc + 2, n_main - 1));
+              }
             }
           });
         });
-        __syncthreads();
+        if constexpr (MDMA) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads of `cur` retired
+        else __syncthreads();
         continue;
       }
       read_frags(fr[0], cur, 0, 0, 0, W_BYTES, kMain);
@@ -862,6 +930,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
         });
       }
       __syncthreads();
+    }
+    if constexpr (MDMA) {
+      __builtin_amdgcn_s_barrier();   // every wave's reads of the last stage retired (the shortcut ring reuses it)
+      asm volatile("" ::: "memory");
     }
   };
   // ---- fused 1x1 shortcut chunks (centre tap) ----
@@ -2884,6 +2956,15 @@ bool conv3x3_scr_ring_enabled() {
   return v;
 }
 
+// The fp16 MI4 conv3x3's main chunks staged by LDS-DMA with per-tile precomputed halo offsets (conv3x3_db_kernel<MDMA>)
+// instead of through VGPRs: measured bit-identical and 3-4 % faster per level without the shortcut, ~1 % with it
+// (tools/conv_bench 57 mdma, profiles/r05_conv_bench_mdma.txt), +0.4 % end to end on one box.  SESA_CONV_MDMA=0: the
+// register-staged main phase (A/B).
+bool conv3x3_mdma_enabled() {
+  static const bool v = !(getenv("SESA_CONV_MDMA") && std::string(getenv("SESA_CONV_MDMA")) == "0");
+  return v;
+}
+
 bool tap_bn128_enabled() {
   static const bool v = !(getenv("SESA_TAP_BN128") && std::string(getenv("SESA_TAP_BN128")) == "0");
   return v;
@@ -3038,8 +3119,16 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
           // the DMA ring walks chunk pairs and addresses each batch item's shortcut image with 32-bit offsets
           const bool ring = a.x_chunks > 0 && !ord && conv3x3_scr_ring_enabled() && a.x_chunks % 2 == 0 &&
                             (int64_t)a.T_in * a.F_in * std::max(a.xin.src[0].C, a.xin.src[1].C) * 4 < (1ll << 31);
-          if (ring)
+          // MDMA: the batch item's fp16 plane addressed with 32-bit offsets
+          const bool mdma = conv3x3_mdma_enabled() && (int64_t)a.T_in * a.F_in * a.in.src[0].C * 2 < (1ll << 31);
+          if (ring && mdma)
+            hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, 2, 2, false, 1>), g32, dim3(512), 0, st,
+                               a);
+          else if (ring)
             hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, 2>), g32, dim3(512), 0, st, a);
+          else if (a.x_chunks == 0 && mdma)
+            hipLaunchKernelGGL((conv3x3_db_kernel<true, false, 0, false, 1, true, 0, 2, false, 1>), g32, dim3(512), 0, st,
+                               a);
           else if (a.x_chunks > 0 && ord)
             hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, false, 2, true>), g32, dim3(512), 0, st, a);
           else if (a.x_chunks > 0)

@@ -9,8 +9,10 @@ are accepted for CLI compatibility and map onto what exists on MI355X:
   3-pass bf16x3 parity precision: MDX23C ``fp16mix`` (its TFC 3x3 convs on one fp16 MFMA pass except the
   encoder level-1 ones: <= 5.3e-5 RMS on every full-chunk golden up to 0.3-RMS input -- the reference's AMP
   is fp16 autocast, :308-311, 1.35e-4 RMS), BS- / Mel-Band-Roformer ``fp16`` (QKV / out / FF Linears and
-  attention on fp16 MFMA), SCNet / HTDemucs single-pass ``bf16``; each gated at 1e-4 on the model's
-  full-width golden by tests/test_amp_precision.py.
+  attention on fp16 MFMA), SCNet / HTDemucs ``fp16mix`` (SCNet: 3x3 convs, LSTM input projections and Linears
+  on one fp16 pass, the LSTM recurrence bf16x3; HTDemucs: implicit-GEMM convs, 1x1 rewrites, transformer /
+  channel Linears and attention on one fp16 pass, norms and DConv fp32 / fp64); each gated at 1e-4 on the
+  model's full-width golden by tests/test_amp_precision.py.
 * ``optimize_mode`` ('channels_last' | 'compile' | 'jit' | 'default') -> no effect: the native
   forward already runs channels-last with fused prologues/epilogues, and there is no tracing
   compiler in the path.

@@ -23,8 +23,13 @@ from .audio_io import quantize_pcm, read_wav, write_audio
 
 METHODS = ["avg_wave", "median_wave", "max_wave", "min_wave", "max_fft", "min_fft", "median_fft"]
 # Member precisions of the configs[4] ensemble line (bench.py --model ensemble) and of its parity gate
-# (tests/test_ensemble_models.py: every blend method within 8e-5 of the reference on three fixtures).
-ENSEMBLE_PRECISIONS = {"mdx23c": "fp16mix", "bs_roformer": "fp16", "scnet": "fp16mix"}
+# (tests/test_ensemble_models.py: every blend method within 8e-5 of the reference on three fixtures).  The
+# spectral blends take the phase of file 0 -- the MDX23C stem -- and a magnitude from another member, so they
+# multiply MDX23C's relative error by that member's magnitude over MDX23C's in every bin: measured on MI355X
+# (tools/ens_parity_scan.py, profiles/r05_ens_parity_scan.txt) max_fft reaches 9.5e-4 and median_fft 1.4e-4 with
+# the MDX23C member in fp16mix (and 5.6e-4 / 1.3e-4 with only its level 0-1 convs in bf16x3), 4.1e-5 / 8.8e-6 with
+# it in bf16x3; BS-Roformer fp16 and SCNet fp16mix keep every blend within 4.1e-5.
+ENSEMBLE_PRECISIONS = {"mdx23c": "bf16x3", "bs_roformer": "fp16", "scnet": "fp16mix"}
 _SPECIAL = "[]()|&; "
 
 

@@ -33,8 +33,9 @@ class HTDemucs(NativeModule):
     """Reference-compatible HTDemucs backed by the native HIP forward."""
 
     _prefix = "htdemucs"
-    # fp16mix: the cross-transformer attention (fp32 softmax statistics), the implicit-GEMM convs and the 1x1
-    # rewrites on one fp16 MFMA pass; the transformer / channel Linears bf16x3
+    # fp16mix: the cross-transformer attention (fp32 softmax statistics), the implicit-GEMM convs, the 1x1
+    # rewrites and the transformer / channel Linears on one fp16 MFMA pass (SESA_HTD_PRESPLIT=0 keeps the Linears
+    # bf16x3); norms and the DConv statistics fp32 / fp64
     _precisions = ("bf16x3", "bf16", "fp16mix")
     _amp_precision = "fp16mix"  # --enable_amp (the reference's AMP is fp16 autocast): 5.9e-6 full segment
 

@@ -79,6 +79,7 @@ def _runs(group):
 
 
 _SIDE_STREAMS = {}
+_ALLOW_STREAMS = False   # diagnostics only (tools/streams_bisect.py): lift the streams > 1 refusal below
 
 
 def side_streams(device, n):
@@ -99,7 +100,7 @@ def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, 
     after an event on its forward's stream (the result equals streams = 1 up to the order of the norm
     statistics' fp64 atomic adds, which concurrent forwards interleave)."""
     from . import ops
-    if int(streams) > 1:
+    if int(streams) > 1 and not _ALLOW_STREAMS:
         # measured on MI355X (tools/streams_debug2.py, profiles/r04_streams_debug.txt): streams = 2 changed 415
         # samples of the first group's span by up to 9e-4 while streams = 3 and every single-stream run agreed
         # bit for bit, and a forward on a side stream alone is bit-identical -- an unresolved ordering hazard, so

@@ -27,6 +27,17 @@ def test_library_exports_every_header_symbol():
     assert set(syms) == set(_native.SIGNATURES), set(syms) ^ set(_native.SIGNATURES)
 
 
+def test_library_has_no_unresolved_own_symbols():
+    """Every libsesa symbol the library references is defined in it: a kernel whose host launch stub the compiler
+    dropped would otherwise only surface as a load failure on the GPU box (nm -u, demangled)."""
+    import subprocess
+    from sesa import _native
+    nm = "/opt/rocm/lib/llvm/bin/llvm-nm" if os.path.exists("/opt/rocm/lib/llvm/bin/llvm-nm") else "nm"
+    out = subprocess.run([nm, "-u", "-C", _native.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    own = [ln for ln in out.splitlines() if "sesa::" in ln or " sesa_" in ln]
+    assert not own, own[:5]
+
+
 def test_error_path_without_device():
     """Argument validation happens before any device work and reports through sesa_last_error."""
     from sesa import _native

@@ -136,8 +136,8 @@ def test_forward_batch_items_independent(golden, dev):
 @pytest.mark.gpu
 @pytest.mark.parametrize("precision", ["bf16x3", "fp16mix"])
 def test_forward_full_segment_matches_reference(golden, dev, precision):
-    """fp16mix: the cross-transformer attention (QK^T, PV; fp32 softmax statistics), the implicit-GEMM convs and
-    the 1x1 rewrites on one fp16 MFMA pass; the transformer Linears bf16x3."""
+    """fp16mix: the cross-transformer attention (QK^T, PV; fp32 softmax statistics), the implicit-GEMM convs, the
+    1x1 rewrites and the transformer / channel Linears on one fp16 MFMA pass."""
     g = golden("htdemucs_full_segment.npz")
     m, _ = _model("config_musdb18_htdemucs.yaml", precision=precision)
     y = m(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()

@@ -50,7 +50,8 @@ def stem(kind, cfg_name, g, prec, plan=None):
     finally:
         if plan:
             _native.check(_native.lib().sesa_mdx23c_set_f16_plan(prev.value, None))
-    return est[0].clone()
+    from sesa.config import prefer_target_instrument
+    return est[prefer_target_instrument(c).index("vocals")].clone()
 
 
 def main():
