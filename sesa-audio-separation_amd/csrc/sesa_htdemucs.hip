@@ -214,6 +214,7 @@ struct DcArgs {
                        // sum_c W2[c][:], v2[h] = 2 sum_c b2[c] W2[c][:], sum b2, sum b2^2
 };
 constexpr int kDcP = 64;      // positions per workgroup (apply)
+constexpr int kDcPQ = 256;    // positions per workgroup (htd_dc_apply_q_kernel: its per-thread W2 setup amortised)
 constexpr int kDcG = 128;     // positions per workgroup (Gram)
 constexpr int kDcMaxH = 64;
 
@@ -307,6 +308,82 @@ __global__ void __launch_bounds__(kT) htd_dc_conv_valu_kernel(const float* __res
 }
 int dc_valu_h(int h) { return h > kDcVMaxH ? 0 : h <= 6 ? 6 : h <= 8 ? 8 : h <= 12 ? 12 : 16; }
 
+// htd_dc_conv_valu_kernel with the input rows staged through LDS: the workgroup's P positions plus the 2 dil halo
+// rows are copied by coalesced 16-B loads (consecutive lanes, consecutive quads) into rows padded to C + 4 floats --
+// conflict-free ds_read_b128 for any C % 4 == 0 -- so each thread's tap rows come from LDS instead of 16-B global
+// loads strided C floats apart across the wave (64 cache lines per load instruction).  Same weights, same
+// accumulation order (16-channel groups, then taps, quads, channels); taps past the row edges read staged zeros
+// (fma with 0 adds nothing), so U and the GroupNorm sums are unchanged.
+template <int H, int P>
+__global__ void __launch_bounds__(P) htd_dc_conv_lds_kernel(const float* __restrict__ X, int T, int C, int dil, int h,
+                                                            const float* __restrict__ w, const float* __restrict__ b1,
+                                                            float* __restrict__ U, double* __restrict__ st1) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  __shared__ double red[2 * (P / 64)];
+  const int row = blockIdx.y;
+  const int t0 = blockIdx.x * P;
+  const int CS = C + 4, nq = C / 4, nrow = P + 2 * dil;
+  const float* xr = X + (int64_t)row * T * C;
+  for (int e = threadIdx.x; e < nrow * nq; e += P) {
+    const int r = e / nq, q = e - r * nq;
+    const int t = t0 - dil + r;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (t >= 0 && t < T) v = *reinterpret_cast<const f32x4*>(xr + (int64_t)t * C + 4 * q);
+    *reinterpret_cast<f32x4*>(xs + r * CS + 4 * q) = v;
+  }
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  float acc[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) acc[j] = b1[j];
+  double s = 0.0, ss = 0.0;
+  if (t < T) {
+    for (int c0 = 0; c0 < C; c0 += 16) {
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap) {
+        const float* xp = xs + (threadIdx.x + tap * dil) * CS + c0;
+        const float* wt = w + ((size_t)tap * C + c0) * H;
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          if (c0 + 4 * qd >= C) break;
+          const f32x4 xv = *reinterpret_cast<const f32x4*>(xp + 4 * qd);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int j = 0; j < H; ++j) acc[j] = fmaf(wt[(4 * qd + q) * H + j], xv[q], acc[j]);
+        }
+      }
+    }
+    float* up = U + ((int64_t)row * T + t) * h;
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+      if (j < h) {
+        up[j] = acc[j];
+        s += (double)acc[j];
+        ss += (double)acc[j] * (double)acc[j];
+      }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    s += __shfl_xor(s, o);
+    ss += __shfl_xor(ss, o);
+  }
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    red[2 * wv] = s;
+    red[2 * wv + 1] = ss;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a0 = 0.0, a1 = 0.0;
+    for (int i = 0; i < P / 64; ++i) {
+      a0 += red[2 * i];
+      a1 += red[2 * i + 1];
+    }
+    atomicAdd(&st1[2 * row], a0);
+    atomicAdd(&st1[2 * row + 1], a1);
+  }
+}
+
 // Per (t-block, row): G = gelu(gn1(U)) into LDS, then entry e of (sum G | sum G G^T) summed over the
 // block's positions in fp64 and added to the row's totals.  Round 5: the block's positions are cut into
 // S = kT / nS slices, thread (slice s, entry e) sums its slice (fp64 products of the fp32 G values, as before) and
@@ -361,6 +438,39 @@ __global__ void __launch_bounds__(kT) htd_dc_gram_kernel(DcArgs a) {
   }
 }
 
+// The round-4 Gram kernel (one thread per entry over the block's positions), kept for A/B: SESA_HTD_DCGRAM=0.
+__global__ void __launch_bounds__(kT) htd_dc_gram_v0_kernel(DcArgs a) {
+  __shared__ float Gs[kDcG][kDcMaxH + 1];
+  const int row = blockIdx.y;
+  const int t0 = blockIdx.x * kDcG;
+  const int T = a.T, h = a.h;
+  const int np = min(kDcG, T - t0);
+  float m1, r1;
+  gn_stats(a.st1 + 2 * row, (double)T * h, m1, r1);
+  for (int i = threadIdx.x; i < np * h; i += kT) {
+    const int p = i / h, j = i - p * h;
+    const float u = a.U[((int64_t)row * T + t0 + p) * h + j];
+    Gs[p][j] = gelu_erf((u - m1) * r1 * a.g1[j] + a.be1[j]);
+  }
+  __syncthreads();
+  const int nS = dc_ns(h);
+  for (int e = threadIdx.x; e < nS; e += kT) {
+    double acc = 0.0;
+    if (e < h) {
+      for (int p = 0; p < np; ++p) acc += (double)Gs[p][e];
+    } else {
+      int j = 0, r = e - h;
+      while (r >= h - j) {
+        r -= h - j;
+        ++j;
+      }
+      const int k = j + r;
+      for (int p = 0; p < np; ++p) acc = fma((double)Gs[p][j], (double)Gs[p][k], acc);
+    }
+    atomicAdd(&a.gram[(int64_t)row * nS + e], acc);
+  }
+}
+
 // htd_dc_apply_kernel's work as a streaming kernel over channel groups: thread (position lane pl, channel group cq)
 // keeps CPT channels' W2 columns (a and gate halves), GroupNorm-2 affine, LayerScale in registers and walks the
 // workgroup's positions pl, pl + PL, ... four at a time, each X read / write one 16-B (CPT 4) or 8-B (CPT 2) access:
@@ -369,10 +479,10 @@ __global__ void __launch_bounds__(kT) htd_dc_gram_kernel(DcArgs a) {
 // Same arithmetic per channel as htd_dc_apply_kernel (same fma order), so the output is bit-identical.
 template <int HM, int CPT>
 __global__ void __launch_bounds__(kT) htd_dc_apply_q_kernel(DcArgs a) {
-  __shared__ __attribute__((aligned(16))) float Gs[kDcP][HM];
+  __shared__ __attribute__((aligned(16))) float Gs[kDcPQ][HM];
   __shared__ double red[2 * (kT / 64)];
   const int row = blockIdx.y;
-  const int t0 = blockIdx.x * kDcP;
+  const int t0 = blockIdx.x * kDcPQ;
   const int T = a.T, C = a.C, h = a.h;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float m1, r1;
@@ -415,7 +525,7 @@ __global__ void __launch_bounds__(kT) htd_dc_apply_q_kernel(DcArgs a) {
     m2 = (float)mu;
     r2 = (float)(1.0 / sqrt(var + 1e-5));
   }
-  for (int i = threadIdx.x; i < kDcP * HM; i += kT) {   // pad columns h .. HM are zero
+  for (int i = threadIdx.x; i < kDcPQ * HM; i += kT) {   // pad columns h .. HM are zero
     const int p = i / HM, j = i - p * HM;
     const int t = t0 + p;
     float g = 0.f;
@@ -450,17 +560,17 @@ __global__ void __launch_bounds__(kT) htd_dc_apply_q_kernel(DcArgs a) {
   using VT = std::conditional_t<CPT == 4, float4, std::conditional_t<CPT == 2, float2, float>>;
   constexpr int UP = 4;                                  // positions in flight per thread
   float* xrow = a.X + (int64_t)row * T * C + c0;
-  for (int pb = pl; pb < kDcP; pb += UP * PL) {
+  for (int pb = pl; pb < kDcPQ; pb += UP * PL) {
     VT xv[UP];
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
       const int p = pb + u * PL, t = t0 + p;
-      if (p < kDcP && t < T) xv[u] = *reinterpret_cast<const VT*>(xrow + (int64_t)t * C);
+      if (p < kDcPQ && t < T) xv[u] = *reinterpret_cast<const VT*>(xrow + (int64_t)t * C);
     }
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
       const int p = pb + u * PL, t = t0 + p;
-      if (p >= kDcP || t >= T) continue;
+      if (p >= kDcPQ || t >= T) continue;
       float va[CPT], vg[CPT];
 #pragma unroll
       for (int q = 0; q < CPT; ++q) {
@@ -1552,14 +1662,37 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       if (Hv) {
         // dilated k3 conv over T on the VALU (fp32) + GroupNorm(1, h) sums -> U [rows][T][h]
         void* t0 = profile_begin(st);
-        const dim3 g((unsigned)((Tn + kT - 1) / kT), (unsigned)rows);
+        // LDS-staged rows (SESA_HTD_DCCONV=0: the round-4 global-load kernel, A/B): 256 positions per workgroup,
+        // 128 where the staged rows would pass 64 KiB (C > 56)
+        static const bool dcl = !(getenv("SESA_HTD_DCCONV") && std::string(getenv("SESA_HTD_DCCONV")) == "0");
+        const int P = (256 + 2 * Ly.dil) * (C + 4) * 4 <= 65536 ? 256 : 128;
+        const size_t lds = (size_t)(P + 2 * Ly.dil) * (C + 4) * 4;
+        if (dcl && lds <= 65536) {
+          const dim3 g((unsigned)((Tn + P - 1) / P), (unsigned)rows);
+#define SESA_DCL(HV, PV) hipLaunchKernelGGL((htd_dc_conv_lds_kernel<HV, PV>), g, dim3(PV), lds, st, X, Tn, C, Ly.dil, h, \
+                                            Wb + Ly.w1v, Wb + Ly.b1v, U, rowst)
+          if (P == 256) {
+            if (Hv == 6) SESA_DCL(6, 256);
+            else if (Hv == 8) SESA_DCL(8, 256);
+            else if (Hv == 12) SESA_DCL(12, 256);
+            else SESA_DCL(16, 256);
+          } else {
+            if (Hv == 6) SESA_DCL(6, 128);
+            else if (Hv == 8) SESA_DCL(8, 128);
+            else if (Hv == 12) SESA_DCL(12, 128);
+            else SESA_DCL(16, 128);
+          }
+#undef SESA_DCL
+        } else {
+          const dim3 g((unsigned)((Tn + kT - 1) / kT), (unsigned)rows);
 #define SESA_DCV(HV) hipLaunchKernelGGL(htd_dc_conv_valu_kernel<HV>, g, dim3(kT), 0, st, X, Tn, C, Ly.dil, h, \
                                         Wb + Ly.w1v, Wb + Ly.b1v, U, rowst)
-        if (Hv == 6) SESA_DCV(6);
-        else if (Hv == 8) SESA_DCV(8);
-        else if (Hv == 12) SESA_DCV(12);
-        else SESA_DCV(16);
+          if (Hv == 6) SESA_DCV(6);
+          else if (Hv == 8) SESA_DCV(8);
+          else if (Hv == 12) SESA_DCV(12);
+          else SESA_DCV(16);
 #undef SESA_DCV
+        }
         if (hipGetLastError() != hipSuccess) {
           rc = SESA_ERR_HIP;
           set_error("htdemucs: DConv conv launch failed");
@@ -1598,15 +1731,21 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         hipLaunchKernelGGL(htd_item_stats_kernel,
                            dim3((unsigned)std::min<int64_t>((n_item + kT * 8 - 1) / (kT * 8), 512), (unsigned)rows),
                            dim3(kT), 0, st, U, n_item, rowst);
-      hipLaunchKernelGGL(htd_dc_gram_kernel, dim3((unsigned)((Tn + kDcG - 1) / kDcG), (unsigned)rows), dim3(kT), 0, st,
-                         a);
+      static const bool gram_v0 = getenv("SESA_HTD_DCGRAM") && std::string(getenv("SESA_HTD_DCGRAM")) == "0";
+      if (gram_v0)
+        hipLaunchKernelGGL(htd_dc_gram_v0_kernel, dim3((unsigned)((Tn + kDcG - 1) / kDcG), (unsigned)rows), dim3(kT), 0,
+                           st, a);
+      else
+        hipLaunchKernelGGL(htd_dc_gram_kernel, dim3((unsigned)((Tn + kDcG - 1) / kDcG), (unsigned)rows), dim3(kT), 0,
+                           st, a);
       const dim3 ga((unsigned)((Tn + kDcP - 1) / kDcP), (unsigned)rows);
       // the channel-group streaming form where its registers allow (SESA_HTD_DCAPPLY=0: the round-4 kernel, A/B)
       static const bool apq = !(getenv("SESA_HTD_DCAPPLY") && std::string(getenv("SESA_HTD_DCAPPLY")) == "0");
-      if (apq && h <= 8 && C % 4 == 0 && C / 4 <= kT) hipLaunchKernelGGL((htd_dc_apply_q_kernel<8, 4>), ga, dim3(kT), 0, st, a);
+      const dim3 gq((unsigned)((Tn + kDcPQ - 1) / kDcPQ), (unsigned)rows);
+      if (apq && h <= 8 && C % 4 == 0 && C / 4 <= kT) hipLaunchKernelGGL((htd_dc_apply_q_kernel<8, 4>), gq, dim3(kT), 0, st, a);
       else if (apq && h <= 16 && C % 2 == 0 && C / 2 <= kT)
-        hipLaunchKernelGGL((htd_dc_apply_q_kernel<16, 2>), ga, dim3(kT), 0, st, a);
-      else if (apq && h <= 32 && C <= kT) hipLaunchKernelGGL((htd_dc_apply_q_kernel<32, 1>), ga, dim3(kT), 0, st, a);
+        hipLaunchKernelGGL((htd_dc_apply_q_kernel<16, 2>), gq, dim3(kT), 0, st, a);
+      else if (apq && h <= 32 && C <= kT) hipLaunchKernelGGL((htd_dc_apply_q_kernel<32, 1>), gq, dim3(kT), 0, st, a);
       else if (h <= 8) hipLaunchKernelGGL(htd_dc_apply_kernel<8>, ga, dim3(kT), 0, st, a);
       else if (h <= 16) hipLaunchKernelGGL(htd_dc_apply_kernel<16>, ga, dim3(kT), 0, st, a);
       else if (h <= 32) hipLaunchKernelGGL(htd_dc_apply_kernel<32>, ga, dim3(kT), 0, st, a);

@@ -493,8 +493,13 @@ __device__ __forceinline__ uint32_t dpp_xor1u(uint32_t x) {
 // HT (half tile; fp16 ring only): 256 threads, 256 tokens x 128 columns (4 waves of 128 x 64), a 24 KiB ring
 // slot, two workgroups per CU -- one workgroup's epilogue runs beside the other's main loop instead of
 // idling the MFMA pipe (the epilogues of the fp16 Linears cost as much as their main loops).
-template <int EP, bool M16 = false, int DEPTH = 2, bool HT = false>
+// PERS (HT ring only): persistent workgroups -- 2 per CU, each walks tiles wgi = blockIdx.x, + gridDim.x, ... of the
+// a.pers_tiles the grid would have had -- and the second half of the grid (the second slot of every CU) starts a.stagger
+// x 8128 cycles late, so the two co-resident workgroups run out of phase: one's VALU-bound epilogue (GELU / rotary /
+// fp16 packing) beside the other's MFMA-bound main loop, where a one-tile-per-workgroup grid keeps them in lockstep.
+template <int EP, bool M16 = false, int DEPTH = 2, bool HT = false, bool PERS = false>
 __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kernel(TokGemmArgs a) {
+  static_assert(!PERS || HT, "persistent: the half-tile fp16 ring");
   constexpr int NT = HT ? 256 : 512, BM = 256, BK = kTokBK, WN = HT ? 2 : 4;
   constexpr int NW = NT / 64;                              // waves
   constexpr int TN = HT ? 128 : 256;                       // tile columns
@@ -522,13 +527,18 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
   float* rs = reinterpret_cast<float*>(smem + RING);
   int* rpos = reinterpret_cast<int*>(rs + BM);
 
+  const int n_wg = PERS ? a.pers_tiles : (int)gridDim.x;
+  if (PERS && blockIdx.x >= gridDim.x / 2)
+    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  for (int wgi = blockIdx.x; wgi < n_wg; wgi += (PERS ? (int)gridDim.x : n_wg)) {
+  if (PERS) __syncthreads();   // the previous tile's epilogue is done with the LDS the ring and tables reuse
   const TokGroup g = a.groups[blockIdx.y];
   const int n_tiles2 = HT ? a.n_tiles_n : (a.n_tiles_n + 1) >> 1;   // TN-column tiles
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = xcd_tile(wgi, n_wg);
   const int n_tile2 = tile % n_tiles2;
   const int m_tile = tile / n_tiles2;
   const int n0 = n_tile2 * TN;
-  if (n0 >= g.N) return;
+  if (n0 >= g.N) continue;
   const int m0 = m_tile * BM;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -724,18 +734,26 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
+    continue;
   }
 
   // ---- epilogue ----
+  // Lane / wave indices re-derived behind an optimisation barrier: every epilogue address then depends on a value the
+  // compiler cannot hoist above the main loop (it used to compute ~128 per-element store addresses before the main
+  // loop and spill them to scratch across it, profiles/r05_tokgemm_spills.txt)
+  int etid = tid;
+  asm volatile("" : "+v"(etid));
+  const int elane = etid & 63, ewave = etid >> 6;
+  const int ewm = ewave / WN, ewn = ewave % WN;
+  const int el32 = elane & 31, eh = elane >> 5;
   const float* lres = reinterpret_cast<const float*>(smem);
   const float2* lrope = reinterpret_cast<const float2*>(smem);
   if constexpr ((EP & EP_ROPE) != 0) {
 #pragma unroll
     for (int i = 0; i < 64 / NW; ++i) {                    // piece q: tile rows 4 q .. 4 q + 3 (256 B each)
-      const int q = wave + NW * i;
-      const int row = 4 * q + (lane >> 4);
-      const float2* src = a.rope + (int64_t)rpos[row] * 32 + (lane & 15) * 2;
+      const int q = ewave + NW * i;
+      const int row = 4 * q + (elane >> 4);
+      const float2* src = a.rope + (int64_t)rpos[row] * 32 + (elane & 15) * 2;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + q * 1024), 16, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -749,17 +767,32 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
   float bias[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int n = n0 + (wn * NI + j) * BLK + (M16 ? (lane & 15) : l32);
+    const int n = n0 + (ewn * NI + j) * BLK + (M16 ? (elane & 15) : el32);
     bias[j] = (g.b_off >= 0 && n < g.N) ? a.bias[g.b_off + n] : 0.f;
   }
+  // FULL-tile output bases (the tile's first row and column); per-element offsets are 32-bit (< 256 rows x o_ld)
+  uint16_t* const out16_tile = (EP & EP_SPLIT) ? a.out_hi + (int64_t)m0 * a.o_ld + g.o_off + n0 : nullptr;
+  float* const out32_tile = (EP & EP_SPLIT) ? nullptr : a.out + (int64_t)m0 * a.o_ld + g.o_off + n0;
   auto row_of = [&](int i, int r) -> int {
-    return M16 ? (wm * MI + i) * 16 + 4 * (lane >> 4) + r : (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    return M16 ? (ewm * MI + i) * 16 + 4 * (elane >> 4) + r : (ewm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * eh;
+  };
+  // FULL-tile store addresses: one 64-bit tile base and a per-elane 32-bit part, so that (i, r) -- compile-time in the
+  // unrolled block loops -- only adds a constant (row_of = lane_row + (ewm MI + i) BLK + const(r)).  Written as
+  // 64-bit expressions per element, the compiler hoisted ~128 per-element addresses to the kernel start and spilled
+  // them to scratch (profiles/r05_tokgemm_spills.txt: 32-56 VGPRs of scratch spills per epilogue variant).
+  const int lane_row = M16 ? 4 * (elane >> 4) : 4 * eh;
+  auto row_c = [&](int i, int r) -> int { return (ewm * MI + i) * BLK + (M16 ? r : (r & 3) + 8 * (r >> 2)); };
+  // LDS stage image offset of (row_of(i, r), column nl): the 32-B group swizzle (row >> 2) & 3 is (elane >> 4) & 3 for
+  // the 16x16 blocks and (2 (r >> 2) + eh) & 3 for the 32x32 ones
+  auto stage_off = [&](int i, int r, int nl) -> int {
+    const int sw = M16 ? ((elane >> 4) & 3) : ((2 * (r >> 2) + eh) & 3);
+    return (row_c(i, r) + lane_row) * (2 * TN) + ((2 * nl) ^ (sw << 5));
   };
   // one MFMA block: FULL = no row / column guards; row of accumulator register r of block i
   auto block = [&](auto I, auto J, auto P, auto FULLT) {
     constexpr int i = decltype(I)::value, j = decltype(J)::value, p = decltype(P)::value;
     constexpr bool FULL = decltype(FULLT)::value;
-    const int nl = (wn * NI + j) * BLK + (M16 ? (lane & 15) : l32);
+    const int nl = (ewn * NI + j) * BLK + (M16 ? (elane & 15) : el32);
     const int n = n0 + nl;
     Acc v = acc[i][j];
     if constexpr ((EP & EP_RAW) == 0) {
@@ -791,7 +824,7 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
           const float y = (d & 1) ? fmaf(x, cs.x, partner * cs.y) : fmaf(x, cs.x, -partner * cs.y);
           x = rot ? y : x;
         }
-        if constexpr ((EP & EP_RES) != 0) x += lres[(ml - p * 64 - wm * 64) * TN + nl];
+        if constexpr ((EP & EP_RES) != 0) x += lres[(ml - p * 64 - ewm * 64) * TN + nl];
         v[r] = x;
       }
     }
@@ -806,11 +839,10 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
         if (FULL && stage16) {
           // into the LDS tile image (row stride 2 TN bytes, 32-B groups XOR-permuted by (row >> 2) & 3: the
           // four row groups of one store land in different banks); written out in full lines below
-          const int ml = row_of(i, r);
-          if (!(l32 & 1))
-            *reinterpret_cast<uint32_t*>(smem + ml * (2 * TN) + ((2 * nl) ^ (((ml >> 2) & 3) << 5))) = hb | (hn << 16);
+          if (!(el32 & 1)) *reinterpret_cast<uint32_t*>(smem + stage_off(i, r, nl)) = hb | (hn << 16);
         } else if (FULL) {
-          if (!(l32 & 1)) *reinterpret_cast<uint32_t*>(a.out_hi + o) = hb | (hn << 16);
+          if (!(el32 & 1))
+            *reinterpret_cast<uint32_t*>(out16_tile + ((row_c(i, r) + lane_row) * a.o_ld + nl)) = hb | (hn << 16);
         } else if (m < a.M && n < g.N) {
           a.out_hi[o] = (uint16_t)hb;
         }
@@ -825,11 +857,11 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
         split_bf16(v[r], hi, lo);
         const uint32_t hb = __builtin_bit_cast(uint16_t, hi), lb = __builtin_bit_cast(uint16_t, lo);
         const int64_t o = (int64_t)m * a.o_ld + g.o_off + n;
-        // both exchanges in uniform control flow (a DPP read of a lane masked off by a branch yields 0)
+        // both exchanges in uniform control flow (a DPP read of a elane masked off by a branch yields 0)
         const uint32_t hn = dpp_xor1u(hb), ln = dpp_xor1u(lb);
         if (FULL) {
-          const uint32_t pv = (l32 & 1) ? ln | (lb << 16) : hb | (hn << 16);
-          uint16_t* dst = (l32 & 1) ? a.out_lo + o - 1 : a.out_hi + o;
+          const uint32_t pv = (el32 & 1) ? ln | (lb << 16) : hb | (hn << 16);
+          uint16_t* dst = (el32 & 1) ? a.out_lo + o - 1 : a.out_hi + o;
           *reinterpret_cast<uint32_t*>(dst) = pv;
         } else if (m < a.M && n < g.N) {
           a.out_hi[o] = (uint16_t)hb;
@@ -840,7 +872,8 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
 #pragma unroll
       for (int r = 0; r < RPB; ++r) {
         const int m = m0 + row_of(i, r);
-        if (FULL || (m < a.M && n < g.N)) a.out[(int64_t)m * a.o_ld + g.o_off + n] = v[r];
+        if (FULL) out32_tile[(row_c(i, r) + lane_row) * a.o_ld + nl] = v[r];
+        else if (m < a.M && n < g.N) a.out[(int64_t)m * a.o_ld + g.o_off + n] = v[r];
       }
     }
   };
@@ -848,21 +881,21 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
     Unroll<0, 2>::run([&](auto P) {                        // row half p
       constexpr int p = decltype(P)::value;
       if constexpr ((EP & EP_RES) != 0) {
-        if (p == 1) {                                      // every wave is done with half 0
+        if (p == 1) {                                      // every ewave is done with half 0
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
         }
         // 128 local rows of TN fp32 (1 KiB piece = 1024 / (4 TN) rows); local row rl <-> tile row (half p of
-        // each wm)
+        // each ewm)
         constexpr int RPP = 256 / TN, LPR = 64 / RPP;      // rows per piece, lanes per row
 #pragma unroll
         for (int i = 0; i < 128 / RPP / NW; ++i) {
-          const int pc = wave + NW * i;
-          const int rl = pc * RPP + lane / LPR;
+          const int pc = ewave + NW * i;
+          const int rl = pc * RPP + elane / LPR;
           const int row = rl < 64 ? p * 64 + rl : 128 + p * 64 + (rl - 64);
           const int m = min(m0 + row, a.M - 1);
-          int col = n0 + (lane % LPR) * 4;
+          int col = n0 + (elane % LPR) * 4;
           if (col + 4 > g.N) col = n0;                     // columns >= N are never used
           const float* src = a.residual + (int64_t)m * a.o_ld + g.o_off + col;
           __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0,
@@ -872,7 +905,7 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
       }
-      Unroll<p * (MI / 2), (p + 1) * (MI / 2)>::run([&](auto I) {   // the blocks of rows wm 128 + p 64 ..
+      Unroll<p * (MI / 2), (p + 1) * (MI / 2)>::run([&](auto I) {   // the blocks of rows ewm 128 + p 64 ..
         Unroll<0, NI>::run([&](auto J) { block(I, J, P, FULLT); });
       });
     });
@@ -881,14 +914,14 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
   else run(std::false_type{});
   if constexpr ((EP & EP_SPLIT) != 0 && F16) {
     if (full && stage16) {
-      // the fp16 tile from LDS as full rows: 16 B per lane, 2 TN bytes contiguous per row
+      // the fp16 tile from LDS as full rows: 16 B per elane, 2 TN bytes contiguous per row
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       constexpr int C16 = 2 * TN / 16;                     // 16-B groups per row
 #pragma unroll 4
       for (int it = 0; it < BM * C16 / NT; ++it) {
-        const int e = tid + it * NT;
+        const int e = etid + it * NT;
         const int row = e / C16, c16 = e % C16;
         const u32x4 v = *reinterpret_cast<const u32x4*>(smem + row * (2 * TN) + ((16 * c16) ^ (((row >> 2) & 3) << 5)));
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(a.out_hi + (int64_t)(m0 + row) * a.o_ld + g.o_off + n0 +
@@ -896,6 +929,7 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
       }
     }
   }
+  }   // tiles
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1739,8 +1773,26 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
     // output (profiles/r04_bsr_halftile_ab_*.json, r04_bsr_ff1stage_ab_*.json); SESA_TOKGEMM_HT=0: 256 x 256
     static const bool ht = !(getenv("SESA_TOKGEMM_HT") && std::string(getenv("SESA_TOKGEMM_HT")) == "0");
     const dim3 ght((unsigned)(((a.M + 255) / 256) * a.n_tiles_n), (unsigned)a.n_groups);
+    // SESA_TOKGEMM_PERS=1: the half tile as a persistent grid of two workgroups per CU, the second slot delayed by
+    // SESA_TOKGEMM_STAGGER x 8128 cycles (tok_gemm_glds_kernel<PERS>; A/B)
+    static const bool pers = getenv("SESA_TOKGEMM_PERS") && std::string(getenv("SESA_TOKGEMM_PERS")) == "1";
+    static const int stagger = getenv("SESA_TOKGEMM_STAGGER") ? atoi(getenv("SESA_TOKGEMM_STAGGER")) : 1;
+    static const int n_cu = [] {
+      int d = 0, n = 0;
+      (void)hipGetDevice(&d);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
+      return n > 0 ? n : 256;
+    }();
+    TokGemmArgs ap = a;
+    const bool use_pers = pers && ght.x > 2u * (unsigned)n_cu && (2 * n_cu) % 8 == 0;
+    const dim3 gpers((unsigned)(2 * n_cu), (unsigned)a.n_groups);
+    if (use_pers) {
+      ap.pers_tiles = (int)ght.x;
+      ap.stagger = stagger;
+    }
 #define SESA_GLDS16(EPV)                                                                                   \
-  if (m16 && ht) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 3, true>), ght, dim3(256), 0, st, a);    \
+  if (m16 && ht && use_pers) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 3, true, true>), gpers, dim3(256), 0, st, ap); \
+  else if (m16 && ht) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 3, true>), ght, dim3(256), 0, st, a);    \
   else if (m16 && depth == 4) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 4>), gbig, dim3(512), 0, st, a); \
   else if (m16 && depth == 3) hipLaunchKernelGGL((tok_gemm_glds_kernel<EPV, true, 3>), gbig, dim3(512), 0, st, a); \
   else SESA_GLDS(EPV)

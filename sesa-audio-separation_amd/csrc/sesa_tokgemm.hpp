@@ -78,6 +78,10 @@ struct TokGemmArgs {
   uint16_t* out_lo;
   // conv mode: 64-column tiles (n_tiles_n then counts ceil(N / 64)) for narrow convolutions
   int bn64;
+  // persistent launch (tok_gemm_glds_kernel<PERS>, set by launch_tok_gemm): tiles of the full grid, and the delay of
+  // the second half of the workgroups in units of s_sleep(127)
+  int pers_tiles;
+  int stagger;
 };
 
 // Split fp32 rows into bf16 planes for tok_gemm's pre-split A: hi = bf16(x), lo = bf16(x - hi),

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round 5 lease E: the GPU suite on the tree (MDMA default, HTDemucs DConv apply / Gram rewrite, ensemble gate over
-# three fixtures x seven methods), then benches: HTDemucs (A/B of the DConv apply), ensemble (blend parity), MDX23C.
+# Round 5 lease E: the GPU suite on the tree (MDMA default, HTDemucs DConv apply / Gram / LDS-staged k3 conv, ensemble
+# gate over three fixtures x seven methods), then benches: HTDemucs (A/B of the DConv kernels), BS-Roformer (A/B of the
+# persistent staggered token GEMMs), ensemble (blend parity), MDX23C.
 set -e
 O=gpurun_out/r05e
 mkdir -p $O
@@ -9,12 +10,16 @@ echo "[r05e] $(date +%T) gpu suite"
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -s > $O/gputest.txt 2>&1 || rc=$?
 tail -3 $O/gputest.txt
 if [ "${rc:-0}" != 0 ]; then echo "[r05e] gpu suite rc=$rc"; [ "$rc" = 1 ] || exit "$rc"; fi
-echo "[r05e] $(date +%T) bench htdemucs"
-timeout -k 10 300 python bench.py --model htdemucs --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_htd.json 2> $O/bench_htd.err
-echo "[r05e] $(date +%T) bench htdemucs (round-4 DConv apply)"
-SESA_HTD_DCAPPLY=0 timeout -k 10 300 python bench.py --model htdemucs --steps 3 --warmup 1 --no-cpu-baseline --no-parity > $O/bench_htd_old.json 2> $O/bench_htd_old.err
-echo "[r05e] $(date +%T) bench ensemble"
-timeout -k 10 400 python bench.py --model ensemble --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_ens.json 2> $O/bench_ens.err
-echo "[r05e] $(date +%T) bench mdx23c"
-timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_mdx.json 2> $O/bench_mdx.err
+b() {
+  echo "[r05e] $(date +%T) bench $1"
+  timeout -k 10 400 env $2 python bench.py $3 --no-cpu-baseline > $O/bench_$1.json 2> $O/bench_$1.err
+}
+b htd "X=1" "--model htdemucs --steps 3 --warmup 1"
+b htd_old "SESA_HTD_DCAPPLY=0 SESA_HTD_DCCONV=0" "--model htdemucs --steps 3 --warmup 1 --no-parity"
+b bsr "X=1" "--model bs_roformer --steps 3 --warmup 1 --no-parity"
+b bsr_pers1 "SESA_TOKGEMM_PERS=1 SESA_TOKGEMM_STAGGER=1" "--model bs_roformer --steps 3 --warmup 1"
+b bsr_pers2 "SESA_TOKGEMM_PERS=1 SESA_TOKGEMM_STAGGER=2" "--model bs_roformer --steps 3 --warmup 1 --no-parity"
+b bsr2 "X=1" "--model bs_roformer --steps 3 --warmup 1 --no-parity"
+b ens "X=1" "--model ensemble --steps 3 --warmup 1"
+b mdx "X=1" "--steps 5 --warmup 1"
 echo "[r05e] $(date +%T) done"
