@@ -1664,10 +1664,12 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         void* t0 = profile_begin(st);
         // LDS-staged rows (SESA_HTD_DCCONV=0: the round-4 global-load kernel, A/B): 256 positions per workgroup,
         // 128 where the staged rows would pass 64 KiB (C > 56)
+        // measured (profiles/r05_htd_dconv_*_kernel_stats.txt): 298 -> 256 ms per 3 passes at h = 6 (256 positions per
+        // workgroup), 204 -> 216 at h = 12 (128 positions: the LDS rows of C = 96), so the LDS form at 256 positions only
         static const bool dcl = !(getenv("SESA_HTD_DCCONV") && std::string(getenv("SESA_HTD_DCCONV")) == "0");
         const int P = (256 + 2 * Ly.dil) * (C + 4) * 4 <= 65536 ? 256 : 128;
         const size_t lds = (size_t)(P + 2 * Ly.dil) * (C + 4) * 4;
-        if (dcl && lds <= 65536) {
+        if (dcl && lds <= 65536 && P == 256) {
           const dim3 g((unsigned)((Tn + P - 1) / P), (unsigned)rows);
 #define SESA_DCL(HV, PV) hipLaunchKernelGGL((htd_dc_conv_lds_kernel<HV, PV>), g, dim3(PV), lds, st, X, Tn, C, Ly.dil, h, \
                                             Wb + Ly.w1v, Wb + Ly.b1v, U, rowst)
@@ -1731,7 +1733,9 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         hipLaunchKernelGGL(htd_item_stats_kernel,
                            dim3((unsigned)std::min<int64_t>((n_item + kT * 8 - 1) / (kT * 8), 512), (unsigned)rows),
                            dim3(kT), 0, st, U, n_item, rowst);
-      static const bool gram_v0 = getenv("SESA_HTD_DCGRAM") && std::string(getenv("SESA_HTD_DCGRAM")) == "0";
+      // the one-thread-per-entry Gram kernel by default: the sliced form measured slower (238 -> 270 ms per 3 passes,
+      // profiles/r05_htd_dconv_*_kernel_stats.txt); SESA_HTD_DCGRAM=1 selects it
+      static const bool gram_v0 = !(getenv("SESA_HTD_DCGRAM") && std::string(getenv("SESA_HTD_DCGRAM")) == "1");
       if (gram_v0)
         hipLaunchKernelGGL(htd_dc_gram_v0_kernel, dim3((unsigned)((Tn + kDcG - 1) / kDcG), (unsigned)rows), dim3(kT), 0,
                            st, a);
@@ -1742,10 +1746,10 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       // the channel-group streaming form where its registers allow (SESA_HTD_DCAPPLY=0: the round-4 kernel, A/B)
       static const bool apq = !(getenv("SESA_HTD_DCAPPLY") && std::string(getenv("SESA_HTD_DCAPPLY")) == "0");
       const dim3 gq((unsigned)((Tn + kDcPQ - 1) / kDcPQ), (unsigned)rows);
-      if (apq && h <= 8 && C % 4 == 0 && C / 4 <= kT) hipLaunchKernelGGL((htd_dc_apply_q_kernel<8, 4>), gq, dim3(kT), 0, st, a);
-      else if (apq && h <= 16 && C % 2 == 0 && C / 2 <= kT)
+      // per-kernel rocprofv3 on MI355X (profiles/r05_htd_dconv_*_kernel_stats.txt): the channel-group form wins at
+      // 8 < h <= 16 (level 1: 251 -> 227 ms per 3 passes) and loses at h <= 8 (455 -> 498) and h <= 32 (135 -> 141)
+      if (apq && h > 8 && h <= 16 && C % 2 == 0 && C / 2 <= kT)
         hipLaunchKernelGGL((htd_dc_apply_q_kernel<16, 2>), gq, dim3(kT), 0, st, a);
-      else if (apq && h <= 32 && C <= kT) hipLaunchKernelGGL((htd_dc_apply_q_kernel<32, 1>), gq, dim3(kT), 0, st, a);
       else if (h <= 8) hipLaunchKernelGGL(htd_dc_apply_kernel<8>, ga, dim3(kT), 0, st, a);
       else if (h <= 16) hipLaunchKernelGGL(htd_dc_apply_kernel<16>, ga, dim3(kT), 0, st, a);
       else if (h <= 32) hipLaunchKernelGGL(htd_dc_apply_kernel<32>, ga, dim3(kT), 0, st, a);
