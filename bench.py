@@ -84,10 +84,12 @@ KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, bf16x3 v_mfm
          "tokgemm": "tok_gemm_glds_kernel + tok_gemm_kernel (token-major Linear layers, bf16x3 "
                     "v_mfma_f32_32x32x16_bf16 / v_mfma_f32_16x16x32_bf16)",
          "lstm": "scn_lstm_mfma_kernel (bi-LSTM recurrence, bf16x3 v_mfma_f32_32x32x16_bf16)",
+         "dft": "scn_dft_mfma_kernel (SCNet feature conversion: rfft / irfft over T as a GEMM against the packed "
+                "DFT matrix, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "hconv": "tok_gemm_kernel<conv> (HTDemucs implicit-GEMM convolutions, v_mfma_f32_32x32x16_bf16)",
          "attn": "attn_kernel (flash attention, S^T = K Q^T, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "simt": "fp32 VALU kernels (SCNet: scn_cm_in / scn_cm_out ConvolutionModule, scn_sdconv / scn_convtr band "
-                 "convs, scn_rfft / scn_irfft feature conversion; HTDemucs: htd_dc_conv_valu / htd_dc_gram / htd_dc_apply "
+                 "convs; HTDemucs: htd_dc_conv_valu / htd_dc_gram / htd_dc_apply "
                  "DConv, norms)"}
 
 
@@ -127,7 +129,8 @@ _TOK_SRC = ("sesa_tokgemm.hip", "sesa_tokgemm.hpp", "sesa_common.hpp")
 KSRC = {"conv3x3": _MDX_SRC, "tdf": _MDX_SRC, "act": _MDX_SRC, "conv1x1": _MDX_SRC, "down": _MDX_SRC,
         "up": _MDX_SRC, "tokgemm": _TOK_SRC + ("sesa_bsroformer.hip",), "attn": _TOK_SRC + ("sesa_bsroformer.hip",),
         "hconv": _TOK_SRC + ("sesa_htdemucs.hip",), "lstm": ("sesa_scnet.hip", "sesa_tokgemm.hpp", "sesa_common.hpp"),
-        "simt": ("sesa_scnet.hip", "sesa_common.hpp"), "conv3x3_x3": _MDX_SRC,
+        "simt": ("sesa_scnet.hip", "sesa_common.hpp"), "dft": ("sesa_scnet.hip", "sesa_tokgemm.hpp", "sesa_common.hpp"),
+        "conv3x3_x3": _MDX_SRC,
         "stft": ("sesa_spectral.hip", "sesa_common.hpp"), "istft": ("sesa_spectral.hip", "sesa_common.hpp"),
         "ola": ("sesa_ola.hip", "sesa_common.hpp")}
 
@@ -182,7 +185,7 @@ def class_precision(kclass, precision, model="mdx23c", members=None):
     BS-Roformer fp16, SCNet fp16mix or HTDemucs fp16mix member (HTDemucs: unless SESA_HTD_PRESPLIT=0 keeps its
     Linears bf16x3), else that member's mode (bf16 / bf16x3); attention fp16 for BS-Roformer fp16 / HTDemucs
     fp16mix; HTDemucs' implicit-GEMM convs fp16 in fp16mix; the LSTM recurrence bf16x3 (bf16 in the bf16 mode);
-    simt is fp32 VALU."""
+    SCNet's feature-conversion DFTs bf16x3; simt is fp32 VALU."""
     if members is None:
         names = ("mdx23c", "bs_roformer", "scnet") if model == "ensemble" else (model,)
         members = {n: member_precision(n, precision, model) for n in names}
@@ -206,6 +209,8 @@ def class_precision(kclass, precision, model="mdx23c", members=None):
         return "fp32"
     if kclass == "lstm":
         return "bf16" if members.get("scnet") == "bf16" else "bf16x3"
+    if kclass == "dft":
+        return "bf16x3"
     f16 = {"bs_roformer": "fp16", "scnet": "fp16mix", "htdemucs": "fp16mix"}
     users = {"tokgemm": ("bs_roformer", "scnet", "htdemucs"), "attn": ("bs_roformer", "htdemucs"),
              "hconv": ("htdemucs",)}.get(kclass, ())
@@ -716,7 +721,7 @@ def main():
         return r
 
     compute_classes = ("conv3x3", "conv3x3_x3", "conv1x1", "down", "up", "tdf", "tokgemm", "attn", "lstm", "simt",
-                       "hconv")
+                       "hconv", "dft")
     roofs = {kc: rf for kc in compute_classes if (rf := class_roof(kc))}
     # dominant kernel class: the model's own, or the class with the most kernel time
     kclass = MODELS[args.model][2] or max(roofs, key=lambda k: roofs[k]["ms_per_step"])
@@ -801,7 +806,7 @@ def main():
         line["hbm_kernels"] = {"peak_gbs": 8000.0, **hbm}
         classes = {}
         for kc in ("conv3x3", "conv3x3_x3", "conv1x1", "down", "up", "tdf", "act", "tokgemm", "attn", "lstm", "simt",
-                   "hconv", "stft", "istft", "ola"):
+                   "hconv", "dft", "stft", "istft", "ola"):
             kms, kn, kw = _native.profile_read(kc)
             if kn:
                 classes[kc] = {"ms_per_step": round(kms / args.steps, 2), "launches": kn}

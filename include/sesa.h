@@ -338,7 +338,8 @@ int sesa_flac_encode(const float* in, int64_t frames, int channels, int sample_r
 #define SESA_KCLASS_OLA 12    /* chunk gather / overlap-add / finalize (work = HBM bytes)     */
 #define SESA_KCLASS_HCONV 13  /* HTDemucs implicit-GEMM convolutions (tok_gemm conv mode)    */
 #define SESA_KCLASS_CONV3X3_X3 14 /* MDX23C fp16 modes: the TFC 3x3 convs that stay bf16x3 (plan '3', T < 32) */
-#define SESA_KCLASS_COUNT 15
+#define SESA_KCLASS_DFT 15    /* SCNet feature-conversion DFTs over T on MFMA (work = 2 M K N GEMM FLOP) */
+#define SESA_KCLASS_COUNT 16
 int sesa_profile_enable(int enable);   /* 1: start recording (clears previous records), 0: stop */
 int sesa_profile_read(int kclass, double* total_ms, int64_t* launches, double* total_work);
 /* as sesa_profile_read, plus the class's ALGORITHMIC HBM bytes (each operand read once, each result written once,

@@ -703,6 +703,214 @@ __global__ void __launch_bounds__(kT) htd_dc_apply_kernel(DcArgs a) {
   }
 }
 
+// Round 5: one DConv layer of a frequency-branch row in ONE kernel (rows of T <= kDcRowT positions, h <= 16): the
+// workgroup owns the whole row, so the three passes of the split form (k3 conv + GroupNorm-1 sums -> U in HBM; Gram
+// of G = gelu(gn1(U)) -> atomics; apply) become phases separated by barriers, U / G never leave the chip and no
+// statistic needs an atomic.  Phase 1: thread = position, the dilated k3 conv exactly as htd_dc_conv_valu_kernel
+// (same 16-channel groups, tap / quad / channel order, so U is bit-identical); phase 2: GroupNorm(1, h) over the row
+// (fp64, block reduction); phase 3: G into LDS, the row's Gram sums by (entry, position slice) threads in fp64 and the
+// GroupNorm(1, 2C) moments from them (htd_dc_apply_kernel's quadratic forms); phase 4: the 1x1 conv, GN2, GLU,
+// LayerScale and residual as htd_dc_apply_q_kernel (thread = position lane x CPT channels, W2 columns in registers,
+// UP positions' 16-B / 8-B X accesses in flight) -- X is read from HBM in phase 1 and again here (the row was just
+// read: L2 / MALL), written once.  HBM bytes per position: 8 C (+ L2 re-read) against 12 C + 16 h for the split form.
+constexpr int kDcRowT = 512;   // threads per workgroup = max positions per row
+template <int H, int CPT>
+__global__ void __launch_bounds__(kDcRowT) htd_dc_row_kernel(DcArgs a, const float* __restrict__ w1,
+                                                             const float* __restrict__ b1, int dil) {
+  __shared__ __attribute__((aligned(16))) float Gs[kDcRowT][H];
+  __shared__ double red[2 * (kDcRowT / 64)];
+  __shared__ double part[kDcRowT];
+  __shared__ double tot[dc_ns(H)];
+  __shared__ float mom[4];
+  const int row = blockIdx.x;
+  const int T = a.T, C = a.C, h = a.h;
+  const int t = threadIdx.x;
+  const float* xr = a.X + (int64_t)row * T * C;
+  // ---- phase 1: U[t][0..h) = b1 + k3 dilated conv (zero padding) ----
+  float acc[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) acc[j] = b1[j];
+  if (t < T) {
+    const float* xp[3];
+    bool ok[3];
+#pragma unroll
+    for (int tap = 0; tap < 3; ++tap) {
+      const int tt = t + (tap - 1) * dil;
+      ok[tap] = tt >= 0 && tt < T;
+      xp[tap] = xr + (int64_t)(ok[tap] ? tt : t) * C;
+    }
+    f32x4 cur[3][4], nxt[3][4];
+    auto load = [&](f32x4 (&r)[3][4], int c0) {
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap)
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          const int c = min(c0 + 4 * qd, C - 4);
+          r[tap][qd] = *reinterpret_cast<const f32x4*>(xp[tap] + c);
+        }
+    };
+    load(cur, 0);
+    for (int c0 = 0; c0 < C; c0 += 16) {
+      if (c0 + 16 < C) load(nxt, c0 + 16);
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap) {
+        if (!ok[tap]) continue;
+        const float* wt = w1 + ((size_t)tap * C + c0) * H;
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (c0 + 4 * qd + q >= C) continue;
+#pragma unroll
+            for (int j = 0; j < H; ++j) acc[j] = fmaf(wt[(4 * qd + q) * H + j], cur[tap][qd][q], acc[j]);
+          }
+      }
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap)
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) cur[tap][qd] = nxt[tap][qd];
+    }
+  }
+  // ---- phase 2: GroupNorm(1, h) of U over the row ----
+  double s = 0.0, ss = 0.0;
+  if (t < T) {
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+      if (j < h) {
+        s += (double)acc[j];
+        ss += (double)acc[j] * (double)acc[j];
+      }
+  }
+  block_sum2(s, ss, red);
+  float m1, r1;
+  {
+    const double n = (double)T * h;
+    const double mu = s / n;
+    const double var = fmax(ss / n - mu * mu, 0.0);
+    m1 = (float)mu;
+    r1 = (float)(1.0 / sqrt(var + 1e-5));
+  }
+  // ---- phase 3: G = gelu(gn1(U)) into LDS (zero past T and past h); Gram sums; GN2 moments ----
+#pragma unroll
+  for (int j = 0; j < H; ++j)
+    Gs[t][j] = (t < T && j < h) ? gelu_erf((acc[j] - m1) * r1 * a.g1[j] + a.be1[j]) : 0.f;
+  __syncthreads();
+  const int nS = dc_ns(h);
+  {
+    const int S = min(kDcRowT / nS, 32);               // position slices
+    const int e = t % nS, sl = t / nS;
+    double v = 0.0;
+    if (sl < S) {
+      const int p0 = sl * T / S, p1 = (sl + 1) * T / S;
+      if (e < h) {
+        for (int p = p0; p < p1; ++p) v += (double)Gs[p][e];
+      } else {
+        int j = 0, r = e - h;
+        while (r >= h - j) {
+          r -= h - j;
+          ++j;
+        }
+        const int k = j + r;
+        for (int p = p0; p < p1; ++p) v = fma((double)Gs[p][j], (double)Gs[p][k], v);
+      }
+    }
+    part[t] = v;
+    __syncthreads();
+    if (t < nS) {
+      double q = 0.0;
+      for (int i = 0; i < S; ++i) q += part[i * nS + t];
+      tot[t] = q;
+    }
+    __syncthreads();
+    if (t < 64) {
+      const double* coefS = a.gc;
+      const double* wbar = a.gc + (nS - h);
+      const double* v2 = wbar + h;
+      double s1 = 0.0, s2 = 0.0;
+      for (int i = t; i < nS; i += 64) {
+        if (i < h) {
+          s1 += wbar[i] * tot[i];
+          s2 += v2[i] * tot[i];
+        } else {
+          s2 += coefS[i - h] * tot[i];
+        }
+      }
+      for (int o = 32; o >= 1; o >>= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+      }
+      if (t == 0) {
+        const double sb = a.gc[nS + h], sbb = a.gc[nS + h + 1];
+        const double n = (double)T * 2 * C;
+        const double mu = (s1 + (double)T * sb) / n;
+        const double var = fmax((s2 + (double)T * sbb) / n - mu * mu, 0.0);
+        mom[0] = (float)mu;
+        mom[1] = (float)(1.0 / sqrt(var + 1e-5));
+      }
+    }
+    __syncthreads();
+  }
+  const float m2 = mom[0], r2 = mom[1];
+  // ---- phase 4: V = W2 G + b2, GN2, GLU, LayerScale, residual (in place) ----
+  const int NQ = C / CPT, PL = kDcRowT / NQ;           // channel groups, position lanes (host: NQ <= kDcRowT)
+  const int pl = t / NQ, cq = t - pl * NQ;
+  if (pl >= PL) return;
+  const int c0 = cq * CPT;
+  float wa[CPT][H], wg[CPT][H], ba[CPT], bg[CPT], ga[CPT], gg[CPT], oa[CPT], og[CPT], sc[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const int c = c0 + q;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      wa[q][j] = j < h ? a.W2t[(int64_t)j * 2 * C + c] : 0.f;
+      wg[q][j] = j < h ? a.W2t[(int64_t)j * 2 * C + C + c] : 0.f;
+    }
+    ba[q] = a.b2[c];
+    bg[q] = a.b2[C + c];
+    ga[q] = a.g2[c] * r2;
+    gg[q] = a.g2[C + c] * r2;
+    oa[q] = a.be2[c];
+    og[q] = a.be2[C + c];
+    sc[q] = a.scale[c];
+  }
+  using VT = std::conditional_t<CPT == 4, float4, std::conditional_t<CPT == 2, float2, float>>;
+  constexpr int UP = 4;
+  float* xrow = a.X + (int64_t)row * T * C + c0;
+  for (int pb = pl; pb < T; pb += UP * PL) {
+    VT xv[UP];
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int p = pb + u * PL;
+      if (p < T) xv[u] = *reinterpret_cast<const VT*>(xrow + (int64_t)p * C);
+    }
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int p = pb + u * PL;
+      if (p >= T) continue;
+      float va[CPT], vg[CPT];
+#pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        va[q] = ba[q];
+        vg[q] = bg[q];
+      }
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        const float g = Gs[p][j];
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+          va[q] = fmaf(wa[q][j], g, va[q]);
+          vg[q] = fmaf(wg[q][j], g, vg[q]);
+        }
+      }
+      float* xe = reinterpret_cast<float*>(&xv[u]);
+#pragma unroll
+      for (int q = 0; q < CPT; ++q)
+        xe[q] = xe[q] + sc[q] * (fmaf(va[q] - m2, ga[q], oa[q]) * sigm(fmaf(vg[q] - m2, gg[q], og[q])));
+      *reinterpret_cast<VT*>(xrow + (int64_t)p * C) = xv[u];
+    }
+  }
+}
+
 // ---- transformer norms ------------------------------------------------------------------------
 // One wave per row: out = LayerNorm(in) * g + b (+ tab[row % n_tok]) (eps 1e-5, biased variance)
 __global__ void __launch_bounds__(kT) htd_layernorm_kernel(const float* __restrict__ in, float* __restrict__ out,
@@ -1654,6 +1862,43 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     for (const DcLayer& Ly : layers) {
       static const bool valu_on = !(getenv("SESA_HTD_DCONV_VALU") && std::string(getenv("SESA_HTD_DCONV_VALU")) == "0");
       const int Hv = valu_on && Ly.w1v >= 0 && C % 4 == 0 ? dc_valu_h(h) : 0;
+      // whole-row fused layer (htd_dc_row_kernel) for short rows -- the frequency branch (SESA_HTD_DCROW=0: split form)
+      static const bool row_on = !(getenv("SESA_HTD_DCROW") && std::string(getenv("SESA_HTD_DCROW")) == "0");
+      const int cpt = Hv <= 8 ? 4 : 2;
+      if (row_on && Hv && Tn <= kDcRowT && C % cpt == 0 && C / cpt <= kDcRowT) {
+        DcArgs a{};
+        a.X = X;
+        a.rows = rows;
+        a.T = Tn;
+        a.C = C;
+        a.h = h;
+        a.g1 = Wb + Ly.g1;
+        a.be1 = Wb + Ly.be1;
+        a.W2t = Wb + Ly.w2t;
+        a.b2 = Wb + Ly.b2;
+        a.g2 = Wb + Ly.g2;
+        a.be2 = Wb + Ly.be2;
+        a.scale = Wb + Ly.scale;
+        a.gc = m->d_f64 + Ly.gc;
+        void* tok = profile_begin(st);
+        const dim3 g((unsigned)rows), blk(kDcRowT);
+        const float* w1 = Wb + Ly.w1v;
+        const float* bb = Wb + Ly.b1v;
+        if (Hv == 6) hipLaunchKernelGGL((htd_dc_row_kernel<6, 4>), g, blk, 0, st, a, w1, bb, Ly.dil);
+        else if (Hv == 8) hipLaunchKernelGGL((htd_dc_row_kernel<8, 4>), g, blk, 0, st, a, w1, bb, Ly.dil);
+        else if (Hv == 12) hipLaunchKernelGGL((htd_dc_row_kernel<12, 2>), g, blk, 0, st, a, w1, bb, Ly.dil);
+        else hipLaunchKernelGGL((htd_dc_row_kernel<16, 2>), g, blk, 0, st, a, w1, bb, Ly.dil);
+        if (hipGetLastError() != hipSuccess) {
+          rc = SESA_ERR_HIP;
+          set_error("htdemucs: DConv row kernel launch failed");
+          return;
+        }
+        // k3 conv + 1x1 conv FLOPs (fp32 VALU); bytes: X read once and written once (U / G stay on chip)
+        profile_end(tok, st, SESA_KCLASS_SIMT,
+                    2.0 * rows * Tn * ((double)h * 3.0 * C + 2.0 * h * 2 * C + 0.5 * h * h),
+                    8.0 * rows * Tn * (double)C);
+        continue;
+      }
       if (hipMemsetAsync(rowst, 0, (size_t)rows * (2 + nS) * sizeof(double), st) != hipSuccess) {
         rc = SESA_ERR_HIP;
         set_error("htdemucs: memset");

@@ -1197,6 +1197,138 @@ __global__ void __launch_bounds__(kST) scn_irfft_kernel(const float* __restrict_
   }
 }
 
+// ---- FeatureConversion on the matrix cores (round 5) ------------------------------------------
+// Both directions as one GEMM per sequence r:  out_r[m][n] = sum_k D[m][k] in_r[k][n].  D is constant per model
+// (the ortho scale and the Hermitian weights folded in) and packed at finalize as bf16 hi / lo in MFMA A-fragment
+// order, [MT][KS][hi, lo][64 lanes][8]: one 1 KiB contiguous load per fragment, L2-resident across the grid.
+// in_r is staged once per workgroup into LDS as bf16 hi / lo with k contiguous (the B fragments); 3-pass bf16x3
+// v_mfma_f32_32x32x16_bf16 (hi.hi + hi.lo + lo.hi), fp32 accumulation.
+//   rfft : D [2K][T]; rows m < K -> real part of bin m, m >= K -> imaginary part of bin m - K
+//          in_r[t][n] = X[r][t][n];                     out row m -> Y[r][m mod K][(m >= K) C + n]
+//   irfft: D [T][2K]; cols k < K -> real part of bin k, k >= K -> imaginary part of bin k - K
+//          in_r[k][n] = Y[r][k mod K][(k >= K) Ch + n];  out row t -> X[r][t][n]
+struct DftArgs {
+  const float* in;
+  int64_t in_rs;           // floats per sequence
+  int KK, Kh, ld, off2;    // k extent; rows k < Kh at k ld, rows k >= Kh at (k - Kh) ld + off2
+  int N;                   // columns
+  const uint16_t* D;       // packed matrix
+  int MT, KS;              // 32-row tiles, 16-deep k steps (KP = 16 KS >= KK, zero padded)
+  int Mtot, Mh, old, ooff2;
+  int64_t out_rs;
+  float* out;
+};
+constexpr int kDftWaves = 8;
+
+__host__ __device__ constexpr size_t dft_lds_bytes(int nblk, int KS) {
+  return (size_t)32 * nblk * (16 * KS + 8) * 2 * sizeof(uint16_t);
+}
+
+template <int NBLK>
+__global__ void __launch_bounds__(64 * kDftWaves) scn_dft_mfma_kernel(DftArgs a) {
+  constexpr int NB = 32 * NBLK, MPW = 4 / NBLK;  // wave tile: MPW M-tiles x NBLK N-tiles (64 accumulators)
+  extern __shared__ __align__(16) uint16_t dls[];
+  const int KP = 16 * a.KS, RS = KP + 8;  // RS * 2 B = 16 (mod 32) words: conflict-free ds_read_b128 rows
+  uint16_t* Bh = dls;
+  uint16_t* Bl = dls + NB * RS;
+  const int64_t r = blockIdx.y;
+  const int n0 = blockIdx.x * NB;
+  const float* src = a.in + r * a.in_rs;
+  // stage in_r[0, KP)[n0, n0 + NB) -> LDS (bf16 hi / lo, two k per 32-bit store); coalesced along n
+  for (int i = threadIdx.x; i < NB * (KP / 2); i += 64 * kDftWaves) {
+    const int n = i % NB, k = 2 * (i / NB), nn = n0 + n;
+    float v[2] = {0.f, 0.f};
+    if (nn < a.N) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int kk = k + e;
+        if (kk < a.KK)
+          v[e] = src[(kk < a.Kh ? (int64_t)kk * a.ld : (int64_t)(kk - a.Kh) * a.ld + a.off2) + nn];
+      }
+    }
+    __bf16 h0, l0, h1, l1;
+    split_bf16(v[0], h0, l0);
+    split_bf16(v[1], h1, l1);
+    const uint32_t ph = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    const uint32_t pl = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+    *reinterpret_cast<uint32_t*>(Bh + n * RS + k) = ph;
+    *reinterpret_cast<uint32_t*>(Bl + n * RS + k) = pl;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int ngroups = (a.MT + MPW - 1) / MPW;
+  for (int g = w; g < ngroups; g += kDftWaves) {
+    // tiles past MT re-read the last tile (valid memory); their rows are >= Mtot and never stored
+    const bf16x8* dp[MPW];
+#pragma unroll
+    for (int i = 0; i < MPW; ++i)
+      dp[i] = reinterpret_cast<const bf16x8*>(a.D) + (int64_t)min(g * MPW + i, a.MT - 1) * a.KS * 2 * 64 + lane;
+    f32x16 acc[MPW][NBLK];
+#pragma unroll
+    for (int i = 0; i < MPW; ++i)
+#pragma unroll
+      for (int j = 0; j < NBLK; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    bf16x8 ah[2][MPW], al[2][MPW];
+#pragma unroll
+    for (int i = 0; i < MPW; ++i) {
+      ah[0][i] = dp[i][0];
+      al[0][i] = dp[i][64];
+    }
+    const uint16_t* bh0 = Bh + l32 * RS + 8 * hh;
+    const uint16_t* bl0 = Bl + l32 * RS + 8 * hh;
+    auto step = [&](int ks, const bf16x8 (&h)[MPW], const bf16x8 (&l)[MPW]) {
+      bf16x8 bh[NBLK], bl[NBLK];
+#pragma unroll
+      for (int j = 0; j < NBLK; ++j) {
+        bh[j] = *reinterpret_cast<const bf16x8*>(bh0 + j * 32 * RS + 16 * ks);
+        bl[j] = *reinterpret_cast<const bf16x8*>(bl0 + j * 32 * RS + 16 * ks);
+      }
+#pragma unroll
+      for (int i = 0; i < MPW; ++i)
+#pragma unroll
+        for (int j = 0; j < NBLK; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    for (int ks = 0; ks < a.KS; ks += 2) {
+      if (ks + 1 < a.KS) {
+#pragma unroll
+        for (int i = 0; i < MPW; ++i) {
+          ah[1][i] = dp[i][((int64_t)(ks + 1) * 2) * 64];
+          al[1][i] = dp[i][((int64_t)(ks + 1) * 2 + 1) * 64];
+        }
+      }
+      step(ks, ah[0], al[0]);
+      if (ks + 2 < a.KS) {
+#pragma unroll
+        for (int i = 0; i < MPW; ++i) {
+          ah[0][i] = dp[i][((int64_t)(ks + 2) * 2) * 64];
+          al[0][i] = dp[i][((int64_t)(ks + 2) * 2 + 1) * 64];
+        }
+      }
+      if (ks + 1 < a.KS) step(ks + 1, ah[1], al[1]);
+    }
+    float* dst = a.out + r * a.out_rs;
+#pragma unroll
+    for (int i = 0; i < MPW; ++i)
+#pragma unroll
+      for (int j = 0; j < NBLK; ++j) {
+        const int n = n0 + 32 * j + l32;
+        if (n >= a.N) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int mm = (g * MPW + i) * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
+          if (mm >= a.Mtot) continue;
+          dst[(mm < a.Mh ? (int64_t)mm * a.old : (int64_t)(mm - a.Mh) * a.old + a.ooff2) + n] = acc[i][j][e];
+        }
+      }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 struct Param {
   std::string name;
@@ -1241,6 +1373,9 @@ struct sesa_scnet {
   uint16_t* d_w = nullptr;    // token-GEMM bf16 hi/lo images
   float* d_bias = nullptr;
   float2* d_twT = nullptr;    // (cos, sin)(2 pi m / T)
+  uint16_t* d_dft = nullptr;  // FeatureConversion DFT matrices, packed bf16 hi / lo ([0] rfft, [1] irfft)
+  int dft_mt[2] = {0, 0}, dft_ks[2] = {0, 0};
+  size_t dft_off[2] = {0, 0};
   bool finalized = false;
 };
 
@@ -1282,6 +1417,13 @@ size_t al(size_t floats) { return (floats * 4 + 255) / 256 * 256; }
 // keeps the exact-fp32 VALU kernel (scn_conv3x3_kernel) for A/B.
 bool scn_conv3_mfma() {
   static const bool v = !(getenv("SESA_SCN_CONV3_VALU") && std::string(getenv("SESA_SCN_CONV3_VALU")) == "1");
+  return v;
+}
+
+// FeatureConversion DFTs on MFMA (scn_dft_mfma_kernel, bf16x3); SESA_SCN_DFT=0 keeps the fp32 VALU direct DFTs
+// (scn_rfft_kernel / scn_irfft_kernel) for A/B.
+bool scn_dft_mfma() {
+  static const bool v = !(getenv("SESA_SCN_DFT") && std::string(getenv("SESA_SCN_DFT")) == "0");
   return v;
 }
 
@@ -1706,8 +1848,48 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
     const double ang = 2.0 * M_PI * i / m->T;
     twT[i] = make_float2((float)cos(ang), (float)sin(ang));
   }
-  for (void* p : {(void*)m->d_f32, (void*)m->d_w, (void*)m->d_bias, (void*)m->d_twT})
+  // FeatureConversion DFT matrices (separation.py:20-34, norm = "ortho"), built in double and split hi / lo in
+  // A-fragment order: [MT][KS][hi, lo][64 lanes][8], lane -> row 32 mt + lane % 32, k 16 ks + 8 (lane / 32) + e.
+  std::vector<uint16_t> dft;
+  {
+    const int T = m->T, K = m->K;
+    const double s = 1.0 / std::sqrt((double)T);
+    for (int dir = 0; dir < 2; ++dir) {
+      const int M = dir == 0 ? 2 * K : T, KK = dir == 0 ? T : 2 * K;
+      const int MT = (M + 31) / 32, KS = (KK + 15) / 16;
+      auto val = [&](int row, int col) -> double {
+        if (row >= M || col >= KK) return 0.0;
+        if (dir == 0) {  // row = bin (re | im), col = frame
+          const int k = row < K ? row : row - K;
+          const double ang = 2.0 * M_PI * (double)(((int64_t)k * col) % T) / T;
+          return row < K ? s * std::cos(ang) : -s * std::sin(ang);
+        }
+        const int k = col < K ? col : col - K;  // row = frame, col = bin (re | im)
+        const bool edge = k == 0 || k == K - 1;
+        const double ang = 2.0 * M_PI * (double)(((int64_t)k * row) % T) / T;
+        if (col < K) return s * (edge ? 1.0 : 2.0) * std::cos(ang);
+        return edge ? 0.0 : -2.0 * s * std::sin(ang);
+      };
+      m->dft_mt[dir] = MT;
+      m->dft_ks[dir] = KS;
+      m->dft_off[dir] = dft.size();
+      dft.resize(dft.size() + (size_t)MT * KS * 2 * 64 * 8);
+      uint16_t* o = dft.data() + m->dft_off[dir];
+      for (int mt = 0; mt < MT; ++mt)
+        for (int ks = 0; ks < KS; ++ks)
+          for (int ln = 0; ln < 64; ++ln)
+            for (int e = 0; e < 8; ++e) {
+              const float v = (float)val(32 * mt + ln % 32, 16 * ks + 8 * (ln / 32) + e);
+              const uint16_t hb = f2bf(v);
+              const size_t base = ((((size_t)mt * KS + ks) * 2) * 64 + ln) * 8 + e;
+              o[base] = hb;
+              o[base + 64 * 8] = f2bf(v - bf2f(hb));
+            }
+    }
+  }
+  for (void* p : {(void*)m->d_f32, (void*)m->d_w, (void*)m->d_bias, (void*)m->d_twT, (void*)m->d_dft})
     if (p) (void)hipFree(p);
+  m->d_dft = nullptr;
   m->d_f32 = nullptr;
   m->d_w = nullptr;
   m->d_bias = nullptr;
@@ -1720,11 +1902,14 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
                "scnet finalize: hipMalloc bias");
   SESA_REQUIRE(hipMalloc(&m->d_twT, twT.size() * sizeof(float2)) == hipSuccess, SESA_ERR_NOMEM,
                "scnet finalize: hipMalloc twiddles");
+  SESA_REQUIRE(hipMalloc(&m->d_dft, dft.size() * 2) == hipSuccess, SESA_ERR_NOMEM,
+               "scnet finalize: hipMalloc DFT matrices");
   hipStream_t st = as_stream(stream);
   SESA_CHECK_HIP(hipMemcpyAsync(m->d_f32, f32.data(), f32.size() * 4, hipMemcpyHostToDevice, st));
   if (!blob.empty()) SESA_CHECK_HIP(hipMemcpyAsync(m->d_w, blob.data(), blob.size() * 2, hipMemcpyHostToDevice, st));
   if (!bias.empty()) SESA_CHECK_HIP(hipMemcpyAsync(m->d_bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice, st));
   SESA_CHECK_HIP(hipMemcpyAsync(m->d_twT, twT.data(), twT.size() * sizeof(float2), hipMemcpyHostToDevice, st));
+  SESA_CHECK_HIP(hipMemcpyAsync(m->d_dft, dft.data(), dft.size() * 2, hipMemcpyHostToDevice, st));
   SESA_CHECK_HIP(hipStreamSynchronize(st));
   for (auto& L : m->dp) {
     const int rc = lstm_mfma_prepare(L.H);
@@ -1750,6 +1935,10 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
   SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_in_gen_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024));
   SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_cm_out_gen_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+  SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_dft_mfma_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+  SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_dft_mfma_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024));
   m->finalized = true;
   return SESA_OK;
@@ -2026,6 +2215,40 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     // FeatureConversion
     void* tok = profile_begin(st);
     const float scale = (float)(1.0 / std::sqrt((double)T));
+    if (scn_dft_mfma()) {
+      const int dir = i % 2, Ch = d / 2;
+      DftArgs a{};
+      a.in = X;
+      a.D = m->d_dft + m->dft_off[dir];
+      a.MT = m->dft_mt[dir];
+      a.KS = m->dft_ks[dir];
+      a.out = Y;
+      if (dir == 0) {  // X [R][T][d] -> Y [R][K][2d]
+        a.in_rs = (int64_t)T * d;
+        a.KK = T, a.Kh = T, a.ld = d, a.off2 = 0, a.N = d;
+        a.Mtot = 2 * K, a.Mh = K, a.old = 2 * d, a.ooff2 = d;
+        a.out_rs = (int64_t)K * 2 * d;
+      } else {         // Y [R][K][2 Ch] -> X [R][T][Ch]
+        a.in_rs = (int64_t)K * 2 * Ch;
+        a.KK = 2 * K, a.Kh = K, a.ld = 2 * Ch, a.off2 = Ch, a.N = Ch;
+        a.Mtot = T, a.Mh = T, a.old = Ch, a.ooff2 = 0;
+        a.out_rs = (int64_t)T * Ch;
+      }
+      SESA_REQUIRE(16 * a.KS >= a.KK && 32 * a.MT >= a.Mtot, SESA_ERR_INVALID, "scnet: DFT matrix geometry");
+      const bool wide = dft_lds_bytes(2, a.KS) <= 160 * 1024;
+      const int nb = wide ? 64 : 32;
+      dim3 grid((unsigned)((a.N + nb - 1) / nb), (unsigned)(B * Fn));
+      if (wide)
+        hipLaunchKernelGGL(scn_dft_mfma_kernel<2>, grid, dim3(64 * kDftWaves), dft_lds_bytes(2, a.KS), st, a);
+      else
+        hipLaunchKernelGGL(scn_dft_mfma_kernel<1>, grid, dim3(64 * kDftWaves), dft_lds_bytes(1, a.KS), st, a);
+      SESA_CHECK_LAUNCH();
+      // flops: the dense GEMM the matrix cores run (one pass); bytes: activations read once, written once
+      profile_end(tok, st, SESA_KCLASS_DFT, 2.0 * B * Fn * (double)a.Mtot * a.KK * a.N,
+                  4.0 * B * Fn * ((double)a.KK * a.N + (double)a.Mtot * a.N));
+      std::swap(X, Y);
+      continue;
+    }
     if (i % 2 == 0) {
       dim3 grid((unsigned)((K + 31) / 32), (unsigned)((d + 63) / 64), (unsigned)(B * Fn));
       hipLaunchKernelGGL(scn_rfft_kernel, grid, dim3(kST), 0, st, X, T, d, m->d_twT, scale, Y);
@@ -2099,7 +2322,7 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
 
 extern "C" int sesa_scnet_destroy(sesa_scnet* m) {
   if (!m) return SESA_OK;
-  for (void* p : {(void*)m->d_f32, (void*)m->d_w, (void*)m->d_bias, (void*)m->d_twT})
+  for (void* p : {(void*)m->d_f32, (void*)m->d_w, (void*)m->d_bias, (void*)m->d_twT, (void*)m->d_dft})
     if (p) (void)hipFree(p);
   for (auto& L : m->dp)
     for (int l = 0; l < 2; ++l) {

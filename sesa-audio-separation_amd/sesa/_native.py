@@ -118,7 +118,7 @@ SIGNATURES = {
 }
 
 KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6, "act": 7, "tokgemm": 8,
-          "attn": 9, "lstm": 10, "simt": 11, "ola": 12, "hconv": 13, "conv3x3_x3": 14}
+          "attn": 9, "lstm": 10, "simt": 11, "ola": 12, "hconv": 13, "conv3x3_x3": 14, "dft": 15}
 
 
 def profile_enable(on):

@@ -29,6 +29,7 @@ def test_default_precision():
     assert cp("tokgemm", "fp16mix", "scnet") == "fp16"
     assert cp("lstm", "fp16mix", "scnet") == "bf16x3"
     assert cp("simt", "fp16mix", "scnet") == "fp32"              # VALU kernels
+    assert cp("dft", "fp16mix", "scnet") == "bf16x3"             # feature-conversion DFTs on MFMA
     assert cp("conv3x3", "fp16") == "fp16" and cp("conv3x3", "fp16mix") == "fp16"
     assert cp("conv3x3", "fp16w2") == "fp16w2" and cp("conv3x3_x3", "fp16mix") == "bf16x3"
     assert cp("tdf", "fp16mix") == "fp16" and cp("tdf", "fp16") == "bf16x3" and cp("act", "fp16mix") == "fp16mix"

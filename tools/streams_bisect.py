@@ -16,7 +16,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLASSES = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6, "act": 7, "ola": 12,
-           "conv3x3_x3": 14, "tokgemm": 8, "attn": 9, "lstm": 10, "simt": 11, "hconv": 13}
+           "conv3x3_x3": 14, "tokgemm": 8, "attn": 9, "lstm": 10, "simt": 11, "hconv": 13, "dft": 15}
 REPS = 3
 
 
@@ -67,7 +67,7 @@ def main():
     precision = sys.argv[2] if len(sys.argv) > 2 else "bf16x3"
     kset = {"mdx23c": ["conv3x3", "conv1x1", "down", "up", "tdf", "stft", "istft", "act", "ola", "conv3x3_x3"],
             "bs_roformer": ["tokgemm", "attn", "act", "stft", "istft", "ola"],
-            "scnet": ["tokgemm", "lstm", "simt", "act", "stft", "istft", "ola"],
+            "scnet": ["tokgemm", "lstm", "simt", "dft", "act", "stft", "istft", "ola"],
             "htdemucs": ["tokgemm", "hconv", "attn", "simt", "stft", "istft", "ola"]}[model]
     configs = ["none", "all"] + [f"except:{CLASSES[k]}" for k in kset]
     for sync in configs:
