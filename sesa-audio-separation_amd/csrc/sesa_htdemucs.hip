@@ -146,6 +146,50 @@ __global__ void __launch_bounds__(kT) htd_item_stats_kernel(const float* __restr
   }
 }
 
+// htd_item_stats_kernel over 16-B quads (n_item % 4 == 0, 16-B aligned items): four quads in flight per thread;
+// every element still enters the fp64 sums on its own (same terms, regrouped per thread)
+__global__ void __launch_bounds__(kT) htd_item_stats4_kernel(const float* __restrict__ x, int64_t n_item,
+                                                             double* __restrict__ stats) {
+  __shared__ double red[2 * (kT / 64)];
+  const int64_t b = blockIdx.y;
+  const f32x4* xb = reinterpret_cast<const f32x4*>(x + b * n_item);
+  const int64_t nq = n_item >> 2, stride = (int64_t)gridDim.x * kT;
+  double s = 0, ss = 0;
+  for (int64_t i0 = (int64_t)blockIdx.x * kT + threadIdx.x; i0 < nq; i0 += 4 * stride) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride;
+      v[u] = i < nq ? __builtin_nontemporal_load(xb + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const double d = v[u][e];
+        s += d;
+        ss = fma(d, d, ss);
+      }
+  }
+  block_sum2(s, ss, red);
+  if (threadIdx.x == 0) {
+    atomicAdd(&stats[2 * b], s);
+    atomicAdd(&stats[2 * b + 1], ss);
+  }
+}
+// launch helper: the quad form where the items allow it (SESA_HTD_STATS4=0: the scalar kernel, A/B)
+void launch_item_stats(const float* x, int64_t n_item, int items, double* stats, hipStream_t st) {
+  static const bool q4 = !(getenv("SESA_HTD_STATS4") && std::string(getenv("SESA_HTD_STATS4")) == "0");
+  if (q4 && n_item % 4 == 0 && ((uintptr_t)x & 15) == 0) {
+    const int64_t nq = n_item / 4;
+    hipLaunchKernelGGL(htd_item_stats4_kernel, dim3((unsigned)std::min<int64_t>((nq + kT * 4 - 1) / (kT * 4), 512), items),
+                       dim3(kT), 0, st, x, n_item, stats);
+  } else {
+    hipLaunchKernelGGL(htd_item_stats_kernel, dim3((unsigned)std::min<int64_t>((n_item + kT * 8 - 1) / (kT * 8), 512), items),
+                       dim3(kT), 0, st, x, n_item, stats);
+  }
+}
+
 // mean and unbiased std in fp32, as torch's x.mean() / x.std() return them (:575-576, :582-583)
 __device__ __forceinline__ void mean_std(const double* st, int64_t n, float& mean, float& std_) {
   const double mu = st[0] / (double)n;
@@ -911,6 +955,201 @@ __global__ void __launch_bounds__(kDcRowT) htd_dc_row_kernel(DcArgs a, const flo
   }
 }
 
+// htd_dc_row_kernel, occupancy form (the default): phase 1 stages the row through LDS in 16-channel slices
+// ([T + 2 dil][16 + 4] floats, 41 KiB: coalesced 64-B row pieces instead of 16-B loads strided C floats across the
+// wave, each X element fetched once per tap-free slice), the slice buffer is reused for G, and phase 4 folds GN2's
+// affine into the W2 columns (y = sum (w ga) G + (b - m2) ga + o) with two channels per thread -- ~47 KiB of LDS and
+// <= 96 VGPRs, so three 512-thread rows share a CU and one row's load phase overlaps another's arithmetic (the first
+// form held one or two).  U is bit-identical (same fma order; taps past the row edges multiply staged zeros).
+constexpr int kDcRowCS = 20;                 // LDS slice row stride (floats)
+constexpr int kDcRowMaxRows = 520;           // T + 2 dil
+template <int H>
+__global__ void __launch_bounds__(kDcRowT) htd_dc_row2_kernel(DcArgs a, const float* __restrict__ w1,
+                                                              const float* __restrict__ b1, int dil) {
+  static_assert(kDcRowT * H <= kDcRowMaxRows * kDcRowCS, "G reuses the slice buffer");
+  __shared__ __attribute__((aligned(16))) float xs[kDcRowMaxRows * kDcRowCS];
+  __shared__ double red[2 * (kDcRowT / 64)];
+  __shared__ double part[kDcRowT];
+  __shared__ double tot[dc_ns(H)];
+  __shared__ float mom[2];
+  const int row = blockIdx.x;
+  const int T = a.T, C = a.C, h = a.h;
+  const int t = threadIdx.x;
+  const float* xr = a.X + (int64_t)row * T * C;
+  const int nrow = T + 2 * dil;
+  // ---- phase 1 ----
+  float acc[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) acc[j] = b1[j];
+  constexpr int NL = (kDcRowMaxRows * 4 + kDcRowT - 1) / kDcRowT;
+  for (int c0 = 0; c0 < C; c0 += 16) {
+    f32x4 v[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = t + i * kDcRowT, r = e >> 2, q = e & 3, tt = r - dil;
+      v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (r < nrow && tt >= 0 && tt < T && c0 + 4 * q < C) v[i] = *reinterpret_cast<const f32x4*>(xr + (int64_t)tt * C + c0 + 4 * q);
+    }
+    __syncthreads();   // the previous slice's readers are done
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = t + i * kDcRowT, r = e >> 2, q = e & 3;
+      if (r < nrow) *reinterpret_cast<f32x4*>(xs + r * kDcRowCS + 4 * q) = v[i];
+    }
+    __syncthreads();
+    if (t < T) {
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap) {
+        const float* xp = xs + (t + tap * dil) * kDcRowCS;
+        const float* wt = w1 + ((size_t)tap * C + c0) * H;
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          if (c0 + 4 * qd >= C) break;
+          const f32x4 xv = *reinterpret_cast<const f32x4*>(xp + 4 * qd);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int j = 0; j < H; ++j) acc[j] = fmaf(wt[(4 * qd + q) * H + j], xv[q], acc[j]);
+        }
+      }
+    }
+  }
+  // ---- phase 2 ----
+  double s = 0.0, ss = 0.0;
+  if (t < T) {
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+      if (j < h) {
+        s += (double)acc[j];
+        ss += (double)acc[j] * (double)acc[j];
+      }
+  }
+  block_sum2(s, ss, red);   // (its barriers also end phase 1's slice reads: xs is free for G)
+  float m1, r1;
+  {
+    const double n = (double)T * h;
+    const double mu = s / n;
+    const double var = fmax(ss / n - mu * mu, 0.0);
+    m1 = (float)mu;
+    r1 = (float)(1.0 / sqrt(var + 1e-5));
+  }
+  // ---- phase 3 ----
+  float* Gs = xs;   // [kDcRowT][H]
+#pragma unroll
+  for (int j = 0; j < H; ++j)
+    Gs[t * H + j] = (t < T && j < h) ? gelu_erf((acc[j] - m1) * r1 * a.g1[j] + a.be1[j]) : 0.f;
+  __syncthreads();
+  const int nS = dc_ns(h);
+  {
+    const int S = min(kDcRowT / nS, 32);
+    const int e = t % nS, sl = t / nS;
+    double v = 0.0;
+    if (sl < S) {
+      const int p0 = sl * T / S, p1 = (sl + 1) * T / S;
+      if (e < h) {
+        for (int p = p0; p < p1; ++p) v += (double)Gs[p * H + e];
+      } else {
+        int j = 0, r = e - h;
+        while (r >= h - j) {
+          r -= h - j;
+          ++j;
+        }
+        const int k = j + r;
+        for (int p = p0; p < p1; ++p) v = fma((double)Gs[p * H + j], (double)Gs[p * H + k], v);
+      }
+    }
+    part[t] = v;
+    __syncthreads();
+    if (t < nS) {
+      double q = 0.0;
+      for (int i = 0; i < S; ++i) q += part[i * nS + t];
+      tot[t] = q;
+    }
+    __syncthreads();
+    if (t < 64) {
+      const double* coefS = a.gc;
+      const double* wbar = a.gc + (nS - h);
+      const double* v2 = wbar + h;
+      double s1 = 0.0, s2 = 0.0;
+      for (int i = t; i < nS; i += 64) {
+        if (i < h) {
+          s1 += wbar[i] * tot[i];
+          s2 += v2[i] * tot[i];
+        } else {
+          s2 += coefS[i - h] * tot[i];
+        }
+      }
+      for (int o = 32; o >= 1; o >>= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+      }
+      if (t == 0) {
+        const double sb = a.gc[nS + h], sbb = a.gc[nS + h + 1];
+        const double n = (double)T * 2 * C;
+        const double mu = (s1 + (double)T * sb) / n;
+        const double var = fmax((s2 + (double)T * sbb) / n - mu * mu, 0.0);
+        mom[0] = (float)mu;
+        mom[1] = (float)(1.0 / sqrt(var + 1e-5));
+      }
+    }
+    __syncthreads();
+  }
+  const float m2 = mom[0], r2 = mom[1];
+  // ---- phase 4: two channels per thread, GN2 affine folded into the W2 columns ----
+  constexpr int CPT = 2;
+  const int NQ = C / CPT, PL = kDcRowT / NQ;
+  const int pl = t / NQ, cq = t - pl * NQ;
+  if (pl >= PL) return;
+  const int c0 = cq * CPT;
+  float wa[CPT][H], wg[CPT][H], ca[CPT], cg[CPT], sc[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const int c = c0 + q;
+    const float ga = a.g2[c] * r2, gg = a.g2[C + c] * r2;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      wa[q][j] = j < h ? a.W2t[(int64_t)j * 2 * C + c] * ga : 0.f;
+      wg[q][j] = j < h ? a.W2t[(int64_t)j * 2 * C + C + c] * gg : 0.f;
+    }
+    ca[q] = (a.b2[c] - m2) * ga + a.be2[c];
+    cg[q] = (a.b2[C + c] - m2) * gg + a.be2[C + c];
+    sc[q] = a.scale[c];
+  }
+  constexpr int UP = 4;
+  float* xrow = a.X + (int64_t)row * T * C + c0;
+  for (int pb = pl; pb < T; pb += UP * PL) {
+    float2 xv[UP];
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int p = pb + u * PL;
+      if (p < T) xv[u] = *reinterpret_cast<const float2*>(xrow + (int64_t)p * C);
+    }
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int p = pb + u * PL;
+      if (p >= T) continue;
+      float ya[CPT], yg[CPT];
+#pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        ya[q] = ca[q];
+        yg[q] = cg[q];
+      }
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        const float g = Gs[p * H + j];
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+          ya[q] = fmaf(wa[q][j], g, ya[q]);
+          yg[q] = fmaf(wg[q][j], g, yg[q]);
+        }
+      }
+      xv[u].x = xv[u].x + sc[0] * (ya[0] * sigm(yg[0]));
+      xv[u].y = xv[u].y + sc[1] * (ya[1] * sigm(yg[1]));
+      *reinterpret_cast<float2*>(xrow + (int64_t)p * C) = xv[u];
+    }
+  }
+}
+
 // ---- transformer norms ------------------------------------------------------------------------
 // One wave per row: out = LayerNorm(in) * g + b (+ tab[row % n_tok]) (eps 1e-5, biased variance)
 __global__ void __launch_bounds__(kT) htd_layernorm_kernel(const float* __restrict__ in, float* __restrict__ out,
@@ -951,6 +1190,73 @@ __global__ void __launch_bounds__(kT) htd_layernorm_kernel(const float* __restri
       if (olo) olo[r * D + i] = __builtin_bit_cast(uint16_t, lo);
     } else {
       y[i] = o;
+    }
+  }
+}
+
+// htd_layernorm_kernel for D % 256 == 0 (the cross transformer's D = 512): the row is read once into registers as
+// 16-B quads (lane l holds elements 4 l + 256 k), mean and variance from the registers (two-pass, as before), and
+// the normalised row stored as 16-B fp32 / 8-B fp16 / 8-B bf16 hi + lo pieces -- the scalar form read the row three
+// times and stored 2-B elements (135 us per launch, ~2.7 TB/s).
+template <int NV>
+__global__ void __launch_bounds__(kT) htd_layernorm_v_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                             int64_t rows, const float* __restrict__ g,
+                                                             const float* __restrict__ be,
+                                                             const float* __restrict__ tab, int n_tok,
+                                                             uint16_t* __restrict__ ohi, uint16_t* __restrict__ olo,
+                                                             int f16) {
+  constexpr int D = NV * 256;
+  const int64_t r = (int64_t)blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const float* x = in + r * D;
+  f32x4 v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + 256 * k + 4 * lane));
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[k][e] - mean;
+      q = fmaf(d, d, q);
+    }
+  for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = 1.0f / sqrtf(q / (float)D + 1e-5f);
+  const float* tr = tab ? tab + (r % n_tok) * D : nullptr;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = 256 * k + 4 * lane;
+    const f32x4 gv = *reinterpret_cast<const f32x4*>(g + i), bv = *reinterpret_cast<const f32x4*>(be + i);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[k][e] - mean) * rstd * gv[e] + bv[e];
+    if (tr) {
+      const f32x4 tv = *reinterpret_cast<const f32x4*>(tr + i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] += tv[e];
+    }
+    if (ohi && f16) {
+      const auto h2 = [](float a, float b) {
+        return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
+      };
+      *reinterpret_cast<uint2*>(ohi + r * D + i) = make_uint2(h2(o[0], o[1]), h2(o[2], o[3]));
+    } else if (ohi) {
+      __bf16 hi[4], lo[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split_bf16(o[e], hi[e], lo[e]);
+      const auto b2 = [](__bf16 a, __bf16 b) {
+        return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+      };
+      *reinterpret_cast<uint2*>(ohi + r * D + i) = make_uint2(b2(hi[0], hi[1]), b2(hi[2], hi[3]));
+      if (olo) *reinterpret_cast<uint2*>(olo + r * D + i) = make_uint2(b2(lo[0], lo[1]), b2(lo[2], lo[3]));
+    } else {
+      *reinterpret_cast<f32x4*>(out + r * D + i) = o;
     }
   }
 }
@@ -1738,14 +2044,12 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   {
     void* tok = profile_begin(st);
     const int64_t nf = (int64_t)kF0 * T * 2 * ach;
-    hipLaunchKernelGGL(htd_item_stats_kernel, dim3(std::min<int64_t>((nf + kT * 8 - 1) / (kT * 8), 512), B), dim3(kT), 0,
-                       st, X0, nf, st_f);
+    launch_item_stats(X0, nf, B, st_f, st);
     SESA_CHECK_LAUNCH();
     hipLaunchKernelGGL(htd_norm_freq_kernel, blocks(B * nf), dim3(kT), 0, st, X0, nf, (int64_t)B * nf, st_f);
     SESA_CHECK_LAUNCH();
     const int64_t nt = (int64_t)ach * L;
-    hipLaunchKernelGGL(htd_item_stats_kernel, dim3(std::min<int64_t>((nt + kT * 8 - 1) / (kT * 8), 512), B), dim3(kT), 0,
-                       st, x, nt, st_t);
+    launch_item_stats(x, nt, B, st_t, st);
     SESA_CHECK_LAUNCH();
     hipLaunchKernelGGL(htd_norm_time_kernel, blocks((int64_t)B * L), dim3(kT), 0, st, x, ach, L, (int64_t)B * L, st_t,
                        XT0);
@@ -1863,9 +2167,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       static const bool valu_on = !(getenv("SESA_HTD_DCONV_VALU") && std::string(getenv("SESA_HTD_DCONV_VALU")) == "0");
       const int Hv = valu_on && Ly.w1v >= 0 && C % 4 == 0 ? dc_valu_h(h) : 0;
       // whole-row fused layer (htd_dc_row_kernel) for short rows -- the frequency branch (SESA_HTD_DCROW=0: split form)
-      static const bool row_on = !(getenv("SESA_HTD_DCROW") && std::string(getenv("SESA_HTD_DCROW")) == "0");
-      const int cpt = Hv <= 8 ? 4 : 2;
-      if (row_on && Hv && Tn <= kDcRowT && C % cpt == 0 && C / cpt <= kDcRowT) {
+      // SESA_HTD_DCROW=1: the first (register-staged) row kernel, =0: the split form
+      static const int row_mode = getenv("SESA_HTD_DCROW") ? atoi(getenv("SESA_HTD_DCROW")) : 2;
+      const int cpt = row_mode == 2 ? 2 : Hv <= 8 ? 4 : 2;
+      const bool row2_fits = Tn + 2 * Ly.dil <= kDcRowMaxRows && C % 16 == 0;
+      if (row_mode && Hv && Tn <= kDcRowT && C % cpt == 0 && C / cpt <= kDcRowT && (row_mode != 2 || row2_fits)) {
         DcArgs a{};
         a.X = X;
         a.rows = rows;
@@ -1884,7 +2190,12 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         const dim3 g((unsigned)rows), blk(kDcRowT);
         const float* w1 = Wb + Ly.w1v;
         const float* bb = Wb + Ly.b1v;
-        if (Hv == 6) hipLaunchKernelGGL((htd_dc_row_kernel<6, 4>), g, blk, 0, st, a, w1, bb, Ly.dil);
+        if (row_mode == 2) {
+          if (Hv == 6) hipLaunchKernelGGL((htd_dc_row2_kernel<6>), g, blk, 0, st, a, w1, bb, Ly.dil);
+          else if (Hv == 8) hipLaunchKernelGGL((htd_dc_row2_kernel<8>), g, blk, 0, st, a, w1, bb, Ly.dil);
+          else if (Hv == 12) hipLaunchKernelGGL((htd_dc_row2_kernel<12>), g, blk, 0, st, a, w1, bb, Ly.dil);
+          else hipLaunchKernelGGL((htd_dc_row2_kernel<16>), g, blk, 0, st, a, w1, bb, Ly.dil);
+        } else if (Hv == 6) hipLaunchKernelGGL((htd_dc_row_kernel<6, 4>), g, blk, 0, st, a, w1, bb, Ly.dil);
         else if (Hv == 8) hipLaunchKernelGGL((htd_dc_row_kernel<8, 4>), g, blk, 0, st, a, w1, bb, Ly.dil);
         else if (Hv == 12) hipLaunchKernelGGL((htd_dc_row_kernel<12, 2>), g, blk, 0, st, a, w1, bb, Ly.dil);
         else hipLaunchKernelGGL((htd_dc_row_kernel<16, 2>), g, blk, 0, st, a, w1, bb, Ly.dil);
@@ -1975,9 +2286,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       a.gc = m->d_f64 + Ly.gc;
       const int64_t n_item = (int64_t)Tn * h;
       if (!Hv)   // (the VALU conv accumulated these already)
-        hipLaunchKernelGGL(htd_item_stats_kernel,
-                           dim3((unsigned)std::min<int64_t>((n_item + kT * 8 - 1) / (kT * 8), 512), (unsigned)rows),
-                           dim3(kT), 0, st, U, n_item, rowst);
+        launch_item_stats(U, n_item, rows, rowst, st);
       // the one-thread-per-entry Gram kernel by default: the sliced form measured slower (238 -> 270 ms per 3 passes,
       // profiles/r05_htd_dconv_*_kernel_stats.txt); SESA_HTD_DCGRAM=1 selects it
       static const bool gram_v0 = !(getenv("SESA_HTD_DCGRAM") && std::string(getenv("SESA_HTD_DCGRAM")) == "1");
@@ -2074,9 +2383,22 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     float* Ax = F32(pl.ax);
     float* At = F32(pl.at);
     float* FF = F32(pl.ff);
+    // LayerNorm launch: the register-resident 16-B form for D % 256 == 0 (SESA_HTD_LNV=0: the scalar kernel, A/B)
+    static const bool lnv = !(getenv("SESA_HTD_LNV") && std::string(getenv("SESA_HTD_LNV")) == "0");
+    auto ln_launch = [&](const float* in, float* o, int64_t rows, const float* gp, const float* bp, const float* tab,
+                         int ntok, uint16_t* ohi, uint16_t* olo, int f16) {
+      const dim3 grid((unsigned)((rows + 3) / 4));
+      if (lnv && D % 256 == 0 && D <= 1024) {
+        if (D == 256) hipLaunchKernelGGL(htd_layernorm_v_kernel<1>, grid, dim3(kT), 0, st, in, o, rows, gp, bp, tab, ntok, ohi, olo, f16);
+        else if (D == 512) hipLaunchKernelGGL(htd_layernorm_v_kernel<2>, grid, dim3(kT), 0, st, in, o, rows, gp, bp, tab, ntok, ohi, olo, f16);
+        else if (D == 768) hipLaunchKernelGGL(htd_layernorm_v_kernel<3>, grid, dim3(kT), 0, st, in, o, rows, gp, bp, tab, ntok, ohi, olo, f16);
+        else hipLaunchKernelGGL(htd_layernorm_v_kernel<4>, grid, dim3(kT), 0, st, in, o, rows, gp, bp, tab, ntok, ohi, olo, f16);
+      } else {
+        hipLaunchKernelGGL(htd_layernorm_kernel, grid, dim3(kT), 0, st, in, o, rows, D, gp, bp, tab, ntok, ohi, olo, f16);
+      }
+    };
     auto ln = [&](const float* in, float* o, int64_t rows, int64_t g, int64_t b, const float* tab, int ntok) {
-      hipLaunchKernelGGL(htd_layernorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(kT), 0, st, in, o, rows, D,
-                         Wb + g, Wb + b, tab, ntok, (uint16_t*)nullptr, (uint16_t*)nullptr);
+      ln_launch(in, o, rows, Wb + g, Wb + b, tab, ntok, (uint16_t*)nullptr, (uint16_t*)nullptr, 0);
     };
     // Transformer GEMM operands as bf16 hi / lo planes written once by their producer (LayerNorm,
     // attention, FF1 epilogue) into the same buffers (4 B per element either way), so every Linear of the
@@ -2090,9 +2412,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     // LayerNorm -> planes of `o` (rows x D)
     auto lnp = [&](const float* in, float* o, int64_t rows, int64_t g, int64_t b) {
       if (!ps) return ln(in, o, rows, g, b, nullptr, 1);
-      hipLaunchKernelGGL(htd_layernorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(kT), 0, st, in, o, rows, D,
-                         Wb + g, Wb + b, (const float*)nullptr, 1, hi_of(o), l16 ? nullptr : lo_of(o, rows * D),
-                         (int)l16);
+      ln_launch(in, o, rows, Wb + g, Wb + b, (const float*)nullptr, 1, hi_of(o), l16 ? nullptr : lo_of(o, rows * D),
+                (int)l16);
     };
     // Linear with a pre-split A (planes of `xin`, rows x K = x_ld); optional split output (planes of o)
     auto plin = [&](const Gemm& gm, float* xin, int64_t x_ld, float* o, int64_t o_ld, int64_t M, int act,
@@ -2183,8 +2504,7 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         rc = SESA_ERR_HIP;
         return;
       }
-      hipLaunchKernelGGL(htd_item_stats_kernel, dim3(std::min<int64_t>((n_item + kT * 8 - 1) / (kT * 8), 512), B),
-                         dim3(kT), 0, st, Xs, n_item, sts);
+      launch_item_stats(Xs, n_item, B, sts, st);
       hipLaunchKernelGGL(htd_gn_apply_kernel, blocks(B * n_item), dim3(kT), 0, st, Xs, n_item, D, sts, Wb + g, Wb + b,
                          (int64_t)B * n_item);
       profile_end(tok, st, SESA_KCLASS_SIMT, 8.0 * (double)B * n_item, 8.0 * (double)B * n_item);
