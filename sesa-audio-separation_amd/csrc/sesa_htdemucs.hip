@@ -1150,6 +1150,149 @@ __global__ void __launch_bounds__(kDcRowT) htd_dc_row2_kernel(DcArgs a, const fl
   }
 }
 
+// ---- decoder rewrite conv (fp16mix): 3x3 over (F, T) (NTAP 9) or k3 over the time-branch length (NTAP 3), the skip
+// added on load, bias + GLU in the epilogue (demucs4ht.py HDecLayer: z = glu(rewrite(x + skip))).  Halo tiles in LDS
+// instead of tok_gemm_kernel<conv>'s per-row gathers: a workgroup owns FR rows x (256 / FR) positions and 48 output
+// channels (96 GEMM columns: per 32-column block 16 'a' + 16 'gate' channels); per 16-channel chunk the (x + skip)
+// halo is staged once as fp16 ([row][col][16 ch], 32 B per position, 16-B halves swizzled by bit 3 of the position so
+// any 16 consecutive positions read conflict-free) and the chunk's pre-swizzled fp16 weight image [tap][96][16] is
+// copied beside it; every tap's A fragments are read from the halo at the tap's offset (9 taps, one staging).
+// Double-buffered (one barrier per chunk, chunk kc + 1's loads in registers under chunk kc's 54 MFMAs per wave).
+// Wave w: FR 4 -> halo row w, 64 positions; FR 1 -> positions 64 w .. 64 w + 63.  v_mfma_f32_32x32x16_f16, fp32
+// accumulation; (x + skip) rounded once to fp16 exactly as tok_gemm_kernel<conv, F16> does.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+struct RwArgs {
+  const float* x;      // [B][F][T][C]
+  const float* skip;   // same shape
+  const uint16_t* w;   // [C / 48][C / 16][NTAP][96][16] fp16, pre-swizzled, each chunk image padded to rw_image_bytes
+  const float* bias;   // [2C]: a then gate (the Conv bias as stored)
+  float* out;          // [B][F][T][C]
+  int B, F, T, C;
+};
+constexpr int kRwCols = 96;
+__host__ __device__ constexpr int rw_image_bytes(int ntap) { return ntap * kRwCols * 32; }   // whole 1 KiB pieces
+template <int FR, int NTAP>
+__global__ void __launch_bounds__(256, 2) htd_rw3_kernel(RwArgs a) {
+  constexpr int TT = 256 / FR, PF = NTAP == 9 ? 1 : 0;
+  constexpr int HR = FR + 2 * PF, HC = TT + 2, HP = HR * HC;          // halo rows / cols / positions
+  constexpr int X_BYTES = HP * 32;
+  constexpr int W_BYTES = rw_image_bytes(NTAP);                       // 9 or 27 KiB: whole 1 KiB DMA pieces
+  constexpr int STAGE = X_BYTES + W_BYTES;
+  constexpr int XI = (HP * 4 + 255) / 256;                           // halo quads per thread
+  constexpr int NPC = W_BYTES / 1024, WPW = (NPC + 3) / 4;            // weight DMA pieces (per wave, rounded up)
+  constexpr int MI = 2, NI = 3;
+  static_assert(FR * TT == 256 && W_BYTES % 1024 == 0 && 4 * STAGE <= 163840, "tile; two workgroups per CU");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int cg = blockIdx.y, C = a.C;
+  const int ntt = (a.T + TT - 1) / TT, nfr = (a.F + FR - 1) / FR;
+  int tile = blockIdx.x;
+  const int ti = tile % ntt;
+  tile /= ntt;
+  const int fi = tile % nfr, b = tile / nfr;
+  const int t0 = ti * TT, f0 = fi * FR;
+  const int nk = C / 16;
+  const uint16_t* wsrc = a.w + (int64_t)cg * nk * (W_BYTES / 2);
+  f32x4 xr[XI], sr[XI];
+  auto load = [&](int kc) {
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 256 * i, p = e >> 2, q = e & 3;
+      const int hr = p / HC, hc = p - hr * HC;
+      const int f = f0 + hr - PF, t = t0 + hc - 1;
+      const bool ok = e < HP * 4 && f >= 0 && f < a.F && t >= 0 && t < a.T;
+      const int64_t off = ok ? (((int64_t)b * a.F + f) * a.T + t) * C + kc * 16 + 4 * q : 0;
+      xr[i] = ok ? *reinterpret_cast<const f32x4*>(a.x + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      sr[i] = ok ? *reinterpret_cast<const f32x4*>(a.skip + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  // the chunk's weight image straight into LDS (global_load_lds: 1 KiB per wave instruction, lane-linear)
+  auto dma_w = [&](int kc, char* stg) {
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      const int pc = w + 4 * i;
+      if (pc >= NPC) continue;   // (wave-uniform)
+      const uint16_t* src = wsrc + (int64_t)kc * (W_BYTES / 2) + pc * 512 + lane * 8;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stg + X_BYTES + pc * 1024), 16,
+                                       0, 0);
+    }
+  };
+  auto store = [&](char* stg) {
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 256 * i, p = e >> 2, q = e & 3;
+      if (e >= HP * 4) continue;
+      const f32x4 v = xr[i] + sr[i];
+      const auto h2 = [](float x, float y) {
+        return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)y) << 16);
+      };
+      const int off = p * 32 + ((((q >> 1) ^ (p >> 3)) & 1) << 4) + ((q & 1) << 3);
+      *reinterpret_cast<uint2*>(stg + off) = make_uint2(h2(v[0], v[1]), h2(v[2], v[3]));
+    }
+  };
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // this wave's halo origin: row (FR 4: w), column offset of its 64 positions
+  const int wr0 = FR == 4 ? w : 0, wc0 = FR == 4 ? 0 : 64 * w;
+  load(0);
+  dma_w(0, smem);
+  store(smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    if (kc + 1 < nk) {
+      load(kc + 1);
+      dma_w(kc + 1, smem + ((kc + 1) & 1) * STAGE);   // that buffer's readers (chunk kc - 1) are behind the barrier
+    }
+    const char* stg = smem + (kc & 1) * STAGE;
+#pragma unroll
+    for (int tap = 0; tap < NTAP; ++tap) {
+      const int df = NTAP == 9 ? tap / 3 : 0, dt = NTAP == 9 ? tap % 3 : tap;   // halo offsets (0..2)
+      f16x8 af[MI], bf[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int p = (wr0 + df) * HC + wc0 + 32 * i + l32 + dt;
+        af[i] = *reinterpret_cast<const f16x8*>(stg + p * 32 + (((h ^ (p >> 3)) & 1) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int q = tap * kRwCols + 32 * j + l32;
+        bf[j] = *reinterpret_cast<const f16x8*>(stg + X_BYTES + q * 32 + (((h ^ (q >> 3)) & 1) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kc + 1 < nk) store(smem + ((kc + 1) & 1) * STAGE);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the weight DMA landed
+    __syncthreads();
+  }
+  // epilogue: bias, GLU across lane pairs (l32 ^ 16: the block's gate half), lanes l32 < 16 store
+  const int f = f0 + wr0;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int ch = cg * 48 + 16 * j + (l32 & 15);
+    const float bv = a.bias[(l32 < 16 ? 0 : C) + ch];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = acc[i][j][r] + bv;
+        const float g = __shfl_xor(v, 16);
+        const int t = t0 + wc0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (l32 < 16 && f < a.F && t < a.T)
+          a.out[(((int64_t)b * a.F + f) * a.T + t) * C + ch] = v * (1.0f / (1.0f + __expf(-g)));
+      }
+  }
+}
+
 // ---- transformer norms ------------------------------------------------------------------------
 // One wave per row: out = LayerNorm(in) * g + b (+ tab[row % n_tok]) (eps 1e-5, biased variance)
 __global__ void __launch_bounds__(kT) htd_layernorm_kernel(const float* __restrict__ in, float* __restrict__ out,
@@ -1373,6 +1516,7 @@ struct Branch {   // one encoder / decoder level of one branch
   Gemm conv, rewrite, drewrite, convtr;
   std::vector<DcLayer> edc, ddc;
   int h;          // DConv hidden channels
+  int64_t rw_img = -1, rw_bias = -1;   // decoder rewrite for htd_rw3_kernel (fp16mix): d_w / d_f32 offsets
 };
 
 struct TLayer {
@@ -1830,6 +1974,32 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
       pack_rewrite(B.rewrite, ep, B.Cout, 1);
       if (c.dconv_mode & 1) pack_dconv(B.edc, ep, B.Cout, B.h);
       pack_rewrite(B.drewrite, dp, B.Cout, br ? 3 : 9);
+      if (f16w && B.Cout % 48 == 0) {   // htd_rw3_kernel image: [C / 48][C / 16][taps][96][16] fp16, halves swizzled
+        const auto& W = P(m, dp + ".rewrite.weight");   // [2C][C][taps]
+        const int C = B.Cout, taps = br ? 3 : 9;
+        while (blob.size() % 8) blob.push_back(0);
+        B.rw_img = (int64_t)blob.size();
+        for (int cg = 0; cg < C / 48; ++cg)
+          for (int kc = 0; kc < C / 16; ++kc) {
+            const size_t img0 = blob.size();
+            for (int tap = 0; tap < taps; ++tap)
+              for (int col = 0; col < kRwCols; ++col) {
+                const int q = tap * kRwCols + col;
+                const int jb = col / 32, cc = col % 32;
+                const int co = cg * 48 + 16 * jb + (cc & 15) + (cc < 16 ? 0 : C);   // a (cc < 16) or gate row
+                uint16_t v16[16];
+                for (int e = 0; e < 16; ++e) {
+                  const int ci = kc * 16 + e;
+                  v16[e] = __builtin_bit_cast(uint16_t, (_Float16)W[((size_t)co * C + ci) * taps + tap]);
+                }
+                const int sw = (q >> 3) & 1;   // 16-B half h of the row lands at half h ^ sw
+                for (int hh = 0; hh < 2; ++hh)
+                  for (int e = 0; e < 8; ++e) blob.push_back(v16[8 * (hh ^ sw) + e]);
+              }
+            (void)img0;
+          }
+        B.rw_bias = put(P(m, dp + ".rewrite.bias"));
+      }
       if (c.dconv_mode & 2) pack_dconv(B.ddc, dp, B.Cout, B.h);
       {  // transposed conv: column n = r * Cdec + co (phase r), k = u * Cout + ci reads x[q - u], kernel tap r + S u
         const auto& W = P(m, dp + ".conv_tr.weight");   // [Cout(in)][Cdec][K](1)
@@ -2572,6 +2742,26 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   if (rc) return rc;
 
   // ---- 4. decoders (:636-654): x + skip -> rewrite (3x3 / k3) + GLU -> DConv -> conv_tr -> trim -> GELU ----
+  // the halo-tile rewrite kernel (fp16mix images present; SESA_HTD_RW3=0: tok_gemm_kernel<conv> for A/B).  Returns
+  // false when it does not apply, and the caller runs the implicit GEMM.
+  auto rw3 = [&](const Branch& br, const float* x, const float* skip, float* o, int F, int Tn, int taps) -> bool {
+    static const bool on = !(getenv("SESA_HTD_RW3") && std::string(getenv("SESA_HTD_RW3")) == "0");
+    if (!on || br.rw_img < 0 || rc) return false;
+    RwArgs ra{x, skip, m->d_w + br.rw_img, Wb + br.rw_bias, o, B, F, Tn, br.Cout};
+    const int FR = taps == 9 ? 4 : 1, TT = 256 / FR;
+    const dim3 g((unsigned)((int64_t)B * ((F + FR - 1) / FR) * ((Tn + TT - 1) / TT)), (unsigned)(br.Cout / 48));
+    void* t0 = profile_begin(st);
+    if (taps == 9) hipLaunchKernelGGL((htd_rw3_kernel<4, 9>), g, dim3(256), 0, st, ra);
+    else hipLaunchKernelGGL((htd_rw3_kernel<1, 3>), g, dim3(256), 0, st, ra);
+    if (hipGetLastError() != hipSuccess) {
+      rc = SESA_ERR_HIP;
+      set_error("htdemucs: rewrite kernel launch failed");
+      return true;
+    }
+    const double M = (double)B * F * Tn, N = 2.0 * br.Cout, K = (double)taps * br.Cout;
+    profile_end(t0, st, SESA_KCLASS_HCONV, 2.0 * M * N * K, M * br.Cout * 4.0 * 3.0);
+    return true;
+  };
   const std::vector<int> r9a = {-1, -1, -1, 0, 0, 0, 1, 1, 1}, r9b = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
   const std::vector<int> r3 = {-1, 0, 1};
   std::vector<int> tr_d1(Kk / St);
@@ -2585,8 +2775,9 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     const Branch& t = m->tm[i];
     const int act = i == 0 ? TOK_ACT_NONE : TOK_ACT_GELU;   // `last` decoder layer: no GELU
     // frequency branch: rewrite 3x3 over (F, T), skip added on load
-    conv_gemm(f.drewrite, cur_f, f.Cout, F32(pl.sf[i]), dB, f.Cout, f.Fout, T, f.Fout, T, 1, f.Cout, r9a, r9b,
-              TOK_ACT_NONE, 1, 1, 0, 0);
+    if (!rw3(f, cur_f, F32(pl.sf[i]), dB, f.Fout, T, 9))
+      conv_gemm(f.drewrite, cur_f, f.Cout, F32(pl.sf[i]), dB, f.Cout, f.Fout, T, f.Fout, T, 1, f.Cout, r9a, r9b,
+                TOK_ACT_NONE, 1, 1, 0, 0);
     if (c.dconv_mode & 2) dconv(f.ddc, dB, B * f.Fout, T, f.Cout, f.h);
     // ConvTranspose2d (K x 1, stride S x 1), trim pad rows at both ends (:178-179)
     float* nxt_f = F32(pl.dA);   // cur_f (also dA) was consumed by the rewrite above (stream order)
@@ -2594,8 +2785,9 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
               f.Fin, pad);
     cur_f = nxt_f;
     // time branch: rewrite conv1d k3 (skip on load) + GLU, DConv, ConvTranspose1d, trim [pad, pad + length)
-    conv_gemm(t.drewrite, cur_t, t.Cout, F32(pl.st[i]), tB, t.Cout, t.Fout, 1, t.Fout, 1, 1, t.Cout, r3, {},
-              TOK_ACT_NONE, 1, 1, 0, 0);
+    if (!rw3(t, cur_t, F32(pl.st[i]), tB, 1, t.Fout, 3))
+      conv_gemm(t.drewrite, cur_t, t.Cout, F32(pl.st[i]), tB, t.Cout, t.Fout, 1, t.Fout, 1, 1, t.Cout, r3, {},
+                TOK_ACT_NONE, 1, 1, 0, 0);
     if (c.dconv_mode & 2) dconv(t.ddc, tB, B, t.Fout, t.Cout, t.h);
     float* nxt_t = F32(pl.tA);
     conv_gemm(t.convtr, tB, t.Cout, nullptr, nxt_t, t.Cdec, t.Fout + 1, 1, t.Fout, 1, 1, t.Cout, tr_d1, {}, act, 0, St,
