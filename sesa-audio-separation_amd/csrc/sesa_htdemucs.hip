@@ -1150,8 +1150,9 @@ __global__ void __launch_bounds__(kDcRowT) htd_dc_row2_kernel(DcArgs a, const fl
   }
 }
 
-// ---- decoder rewrite conv (fp16mix): 3x3 over (F, T) (NTAP 9) or k3 over the time-branch length (NTAP 3), the skip
-// added on load, bias + GLU in the epilogue (demucs4ht.py HDecLayer: z = glu(rewrite(x + skip))).  Halo tiles in LDS
+// ---- rewrite convs (fp16mix): the decoder's 3x3 over (F, T) (NTAP 9) or k3 over the time-branch length (NTAP 3) with
+// the skip added on load, and the encoder's 1x1 (NTAP 1, no skip); bias + GLU in the epilogue (demucs4ht.py
+// HDecLayer: z = glu(rewrite(x + skip)); HEncLayer: y = glu(rewrite(x))).  Halo tiles in LDS
 // instead of tok_gemm_kernel<conv>'s per-row gathers: a workgroup owns FR rows x (256 / FR) positions and 48 output
 // channels (96 GEMM columns: per 32-column block 16 'a' + 16 'gate' channels); per 16-channel chunk the (x + skip)
 // halo is staged once as fp16 ([row][col][16 ch], 32 B per position, 16-B halves swizzled by bit 3 of the position so
@@ -1170,19 +1171,24 @@ struct RwArgs {
   int B, F, T, C;
 };
 constexpr int kRwCols = 96;
+constexpr int kRwOS = 52;   // epilogue LDS tile row stride (floats)
 __host__ __device__ constexpr int rw_image_bytes(int ntap) { return ntap * kRwCols * 32; }   // whole 1 KiB pieces
-template <int FR, int NTAP>
-__global__ void __launch_bounds__(256, 2) htd_rw3_kernel(RwArgs a) {
-  constexpr int TT = 256 / FR, PF = NTAP == 9 ? 1 : 0;
+// NWV waves (256 or 512 threads): wave w covers halo row w / WPR, positions 64 (w % WPR) .. + 63, WPR = NWV / FR waves
+// per row; the 8-wave form halves the per-position weight-image traffic and halo overhead at one workgroup per CU.
+template <int FR, int NTAP, int NWV = 4>
+__global__ void __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) htd_rw3_kernel(RwArgs a) {
+  static_assert(NTAP == 9 || NTAP == 3 || NTAP == 1, "3x3, k3 or 1x1");
+  constexpr int NT = 64 * NWV, WPR = NWV / FR, TT = 64 * WPR, PF = NTAP == 9 ? 1 : 0;
   constexpr int HR = FR + 2 * PF, HC = TT + 2, HP = HR * HC;          // halo rows / cols / positions
   constexpr int X_BYTES = HP * 32;
-  constexpr int W_BYTES = rw_image_bytes(NTAP);                       // 9 or 27 KiB: whole 1 KiB DMA pieces
+  constexpr int W_BYTES = rw_image_bytes(NTAP);                       // 3, 9 or 27 KiB: whole 1 KiB DMA pieces
   constexpr int STAGE = X_BYTES + W_BYTES;
-  constexpr int XI = (HP * 4 + 255) / 256;                           // halo quads per thread
-  constexpr int NPC = W_BYTES / 1024, WPW = (NPC + 3) / 4;            // weight DMA pieces (per wave, rounded up)
+  constexpr int XI = (HP * 4 + NT - 1) / NT;                         // halo quads per thread
+  constexpr int NPC = W_BYTES / 1024, WPW = (NPC + NWV - 1) / NWV;    // weight DMA pieces (per wave, rounded up)
   constexpr int MI = 2, NI = 3;
-  static_assert(FR * TT == 256 && W_BYTES % 1024 == 0 && 4 * STAGE <= 163840, "tile; two workgroups per CU");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int OS_BYTES = 64 * NWV * kRwOS * 4, SMEM = 2 * STAGE > OS_BYTES ? 2 * STAGE : OS_BYTES;
+  static_assert(WPR * FR == NWV && W_BYTES % 1024 == 0 && (NWV == 4 ? 2 : 1) * SMEM <= 163840, "tile / LDS");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int cg = blockIdx.y, C = a.C;
   const int ntt = (a.T + TT - 1) / TT, nfr = (a.F + FR - 1) / FR;
@@ -1197,20 +1203,20 @@ __global__ void __launch_bounds__(256, 2) htd_rw3_kernel(RwArgs a) {
   auto load = [&](int kc) {
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const int e = tid + 256 * i, p = e >> 2, q = e & 3;
+      const int e = tid + NT * i, p = e >> 2, q = e & 3;
       const int hr = p / HC, hc = p - hr * HC;
       const int f = f0 + hr - PF, t = t0 + hc - 1;
       const bool ok = e < HP * 4 && f >= 0 && f < a.F && t >= 0 && t < a.T;
       const int64_t off = ok ? (((int64_t)b * a.F + f) * a.T + t) * C + kc * 16 + 4 * q : 0;
       xr[i] = ok ? *reinterpret_cast<const f32x4*>(a.x + off) : f32x4{0.f, 0.f, 0.f, 0.f};
-      sr[i] = ok ? *reinterpret_cast<const f32x4*>(a.skip + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      sr[i] = ok && a.skip ? *reinterpret_cast<const f32x4*>(a.skip + off) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   // the chunk's weight image straight into LDS (global_load_lds: 1 KiB per wave instruction, lane-linear)
   auto dma_w = [&](int kc, char* stg) {
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
-      const int pc = w + 4 * i;
+      const int pc = w + NWV * i;
       if (pc >= NPC) continue;   // (wave-uniform)
       const uint16_t* src = wsrc + (int64_t)kc * (W_BYTES / 2) + pc * 512 + lane * 8;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stg + X_BYTES + pc * 1024), 16,
@@ -1220,7 +1226,7 @@ __global__ void __launch_bounds__(256, 2) htd_rw3_kernel(RwArgs a) {
   auto store = [&](char* stg) {
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const int e = tid + 256 * i, p = e >> 2, q = e & 3;
+      const int e = tid + NT * i, p = e >> 2, q = e & 3;
       if (e >= HP * 4) continue;
       const f32x4 v = xr[i] + sr[i];
       const auto h2 = [](float x, float y) {
@@ -1237,8 +1243,8 @@ __global__ void __launch_bounds__(256, 2) htd_rw3_kernel(RwArgs a) {
     for (int j = 0; j < NI; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  // this wave's halo origin: row (FR 4: w), column offset of its 64 positions
-  const int wr0 = FR == 4 ? w : 0, wc0 = FR == 4 ? 0 : 64 * w;
+  // this wave's halo origin: row, column offset of its 64 positions
+  const int wr0 = w / WPR, wc0 = 64 * (w % WPR);
   load(0);
   dma_w(0, smem);
   store(smem);
@@ -1252,7 +1258,7 @@ __global__ void __launch_bounds__(256, 2) htd_rw3_kernel(RwArgs a) {
     const char* stg = smem + (kc & 1) * STAGE;
 #pragma unroll
     for (int tap = 0; tap < NTAP; ++tap) {
-      const int df = NTAP == 9 ? tap / 3 : 0, dt = NTAP == 9 ? tap % 3 : tap;   // halo offsets (0..2)
+      const int df = NTAP == 9 ? tap / 3 : 0, dt = NTAP == 9 ? tap % 3 : NTAP == 3 ? tap : 1;   // halo offsets (0..2)
       f16x8 af[MI], bf[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
@@ -1274,22 +1280,33 @@ __global__ void __launch_bounds__(256, 2) htd_rw3_kernel(RwArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the weight DMA landed
     __syncthreads();
   }
-  // epilogue: bias, GLU across lane pairs (l32 ^ 16: the block's gate half), lanes l32 < 16 store
-  const int f = f0 + wr0;
+  // epilogue: bias, GLU across lane pairs (l32 ^ 16: the block's gate half); lanes l32 < 16 put the 48 channels of
+  // each position into an LDS tile (row stride 52 floats: the h = 0 / 1 rows, 4 apart, land on different banks),
+  // then all threads store it as 16-B pieces of the positions' 192-B channel runs (4-B scattered stores before)
+  float* os = reinterpret_cast<float*>(smem);   // [NT / 64 * 64 positions][kRwOS]  (the ring is free: barrier above)
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int ch = cg * 48 + 16 * j + (l32 & 15);
-    const float bv = a.bias[(l32 < 16 ? 0 : C) + ch];
+    const int cl = 16 * j + (l32 & 15);
+    const float bv = a.bias[(l32 < 16 ? 0 : C) + cg * 48 + cl];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float v = acc[i][j][r] + bv;
         const float g = __shfl_xor(v, 16);
-        const int t = t0 + wc0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (l32 < 16 && f < a.F && t < a.T)
-          a.out[(((int64_t)b * a.F + f) * a.T + t) * C + ch] = v * (1.0f / (1.0f + __expf(-g)));
+        const int pl = 64 * w + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;   // wave w's positions 64 w .. 64 w + 63
+        if (l32 < 16) os[pl * kRwOS + cl] = v * (1.0f / (1.0f + __expf(-g)));
       }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < (64 * NWV * 12 + NT - 1) / NT; ++i) {
+    const int e = tid + NT * i, pl = e / 12, q = e - 12 * pl;
+    if (pl >= 64 * NWV) continue;
+    const int wv = pl >> 6, f = f0 + wv / WPR, t = t0 + 64 * (wv % WPR) + (pl & 63);
+    if (f < a.F && t < a.T)
+      *reinterpret_cast<f32x4*>(a.out + (((int64_t)b * a.F + f) * a.T + t) * C + cg * 48 + 4 * q) =
+          *reinterpret_cast<const f32x4*>(os + pl * kRwOS + 4 * q);
   }
 }
 
@@ -1416,6 +1433,26 @@ __global__ void htd_gn_apply_kernel(float* __restrict__ X, int64_t n_item, int D
   X[i] = (X[i] - mean) * rstd * g[c] + be[c];
 }
 
+// htd_gn_apply_kernel over 16-B quads with the item on blockIdx.y (no 64-bit division / modulo per element; D % 4 == 0,
+// n_item % 4 == 0): same arithmetic per element
+__global__ void __launch_bounds__(kT) htd_gn_apply4_kernel(float* __restrict__ X, int64_t n_item, int D,
+                                                           const double* __restrict__ stats, const float* __restrict__ g,
+                                                           const float* __restrict__ be) {
+  const int b = blockIdx.y;
+  float mean, rstd;
+  gn_stats(stats + 2 * b, (double)n_item, mean, rstd);
+  f32x4* xb = reinterpret_cast<f32x4*>(X + (int64_t)b * n_item);
+  const int64_t nq = n_item >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * kT + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kT) {
+    const int c = (int)((q << 2) % D);
+    const f32x4 v = xb[q], gv = *reinterpret_cast<const f32x4*>(g + c), bv = *reinterpret_cast<const f32x4*>(be + c);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[e] - mean) * rstd * gv[e] + bv[e];
+    xb[q] = o;
+  }
+}
+
 // ---- spectral back end ----------------------------------------------------------------------
 // _mask (cac) + _ispec frames: spectrum of signal sig = (b, s, c) at cropped frame tc from the decoder's
 // [B][2048][T][Cz] output, channel s * 2 ach + 2 c + (re, im), de-normalised (x * std + mean, :670),
@@ -1517,6 +1554,7 @@ struct Branch {   // one encoder / decoder level of one branch
   std::vector<DcLayer> edc, ddc;
   int h;          // DConv hidden channels
   int64_t rw_img = -1, rw_bias = -1;   // decoder rewrite for htd_rw3_kernel (fp16mix): d_w / d_f32 offsets
+  int64_t erw_img = -1, erw_bias = -1; // encoder 1x1 rewrite, same kernel (NTAP 1)
 };
 
 struct TLayer {
@@ -1954,6 +1992,29 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                    },
                    true, [&](int n) { return Bv[(n & 1) ? (n >> 1) + C : (n >> 1)]; }, blob, bias, f16w));
   };
+  // htd_rw3_kernel image: [C / 48][C / 16][taps][96][16] fp16, halves swizzled; bias [2C] as stored
+  auto pack_rw3 = [&](int64_t& img, int64_t& boff, const std::string& p, int C, int taps) {
+    const auto& W = P(m, p + ".rewrite.weight");   // [2C][C][taps]
+    while (blob.size() % 8) blob.push_back(0);
+    img = (int64_t)blob.size();
+    for (int cg = 0; cg < C / 48; ++cg)
+      for (int kc = 0; kc < C / 16; ++kc)
+        for (int tap = 0; tap < taps; ++tap)
+          for (int col = 0; col < kRwCols; ++col) {
+            const int q = tap * kRwCols + col;
+            const int jb = col / 32, cc = col % 32;
+            const int co = cg * 48 + 16 * jb + (cc & 15) + (cc < 16 ? 0 : C);   // a (cc < 16) or gate row
+            uint16_t v16[16];
+            for (int e = 0; e < 16; ++e) {
+              const int ci = kc * 16 + e;
+              v16[e] = __builtin_bit_cast(uint16_t, (_Float16)W[((size_t)co * C + ci) * taps + tap]);
+            }
+            const int sw = (q >> 3) & 1;   // 16-B half h of the row lands at half h ^ sw
+            for (int hh = 0; hh < 2; ++hh)
+              for (int e = 0; e < 8; ++e) blob.push_back(v16[8 * (hh ^ sw) + e]);
+          }
+    boff = put(P(m, p + ".rewrite.bias"));
+  };
   for (int i = 0; i < c.depth; ++i) {
     for (int br = 0; br < 2; ++br) {
       Branch& B = br ? m->tm[i] : m->fq[i];
@@ -1972,34 +2033,10 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                            true, [&](int n) { return Bv[n]; }, blob, bias, f16w));
       }
       pack_rewrite(B.rewrite, ep, B.Cout, 1);
+      if (f16w && B.Cout % 48 == 0) pack_rw3(B.erw_img, B.erw_bias, ep, B.Cout, 1);
       if (c.dconv_mode & 1) pack_dconv(B.edc, ep, B.Cout, B.h);
       pack_rewrite(B.drewrite, dp, B.Cout, br ? 3 : 9);
-      if (f16w && B.Cout % 48 == 0) {   // htd_rw3_kernel image: [C / 48][C / 16][taps][96][16] fp16, halves swizzled
-        const auto& W = P(m, dp + ".rewrite.weight");   // [2C][C][taps]
-        const int C = B.Cout, taps = br ? 3 : 9;
-        while (blob.size() % 8) blob.push_back(0);
-        B.rw_img = (int64_t)blob.size();
-        for (int cg = 0; cg < C / 48; ++cg)
-          for (int kc = 0; kc < C / 16; ++kc) {
-            const size_t img0 = blob.size();
-            for (int tap = 0; tap < taps; ++tap)
-              for (int col = 0; col < kRwCols; ++col) {
-                const int q = tap * kRwCols + col;
-                const int jb = col / 32, cc = col % 32;
-                const int co = cg * 48 + 16 * jb + (cc & 15) + (cc < 16 ? 0 : C);   // a (cc < 16) or gate row
-                uint16_t v16[16];
-                for (int e = 0; e < 16; ++e) {
-                  const int ci = kc * 16 + e;
-                  v16[e] = __builtin_bit_cast(uint16_t, (_Float16)W[((size_t)co * C + ci) * taps + tap]);
-                }
-                const int sw = (q >> 3) & 1;   // 16-B half h of the row lands at half h ^ sw
-                for (int hh = 0; hh < 2; ++hh)
-                  for (int e = 0; e < 8; ++e) blob.push_back(v16[8 * (hh ^ sw) + e]);
-              }
-            (void)img0;
-          }
-        B.rw_bias = put(P(m, dp + ".rewrite.bias"));
-      }
+      if (f16w && B.Cout % 48 == 0) pack_rw3(B.rw_img, B.rw_bias, dp, B.Cout, br ? 3 : 9);
       if (c.dconv_mode & 2) pack_dconv(B.ddc, dp, B.Cout, B.h);
       {  // transposed conv: column n = r * Cdec + co (phase r), k = u * Cout + ci reads x[q - u], kernel tap r + S u
         const auto& W = P(m, dp + ".conv_tr.weight");   // [Cout(in)][Cdec][K](1)
@@ -2306,6 +2343,35 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   // 1x1 rewrite + GLU (:114-118 of HEncLayer): the plain token GEMM (2 % faster end to end than the
   // one-tap conv-mode GEMM, profiles/r03_htd_rw_*.json; SESA_HTD_REWRITE_CONV=1 selects the latter)
   static const bool rw_conv = getenv("SESA_HTD_REWRITE_CONV") && std::string(getenv("SESA_HTD_REWRITE_CONV")) == "1";
+  // the halo-tile rewrite kernel (fp16mix images present; SESA_HTD_RW3=0: tok_gemm_kernel<conv> for A/B).  Returns
+  // false when it does not apply, and the caller runs the implicit GEMM.
+  auto rw3 = [&](const Branch& br, const float* x, const float* skip, float* o, int F, int Tn, int taps) -> bool {
+    static const bool on = !(getenv("SESA_HTD_RW3") && std::string(getenv("SESA_HTD_RW3")) == "0");
+    const int64_t img = taps == 1 ? br.erw_img : br.rw_img, boff = taps == 1 ? br.erw_bias : br.rw_bias;
+    if (!on || img < 0 || rc) return false;
+    const int Bk = taps == 1 ? 1 : B;
+    RwArgs ra{x, skip, m->d_w + img, Wb + boff, o, Bk, F, Tn, br.Cout};
+    // SESA_HTD_RW_NW=8: 512-thread workgroups (8 rows x 64 / 512 positions; one per CU) instead of 256 (two per CU)
+    static const int nw = getenv("SESA_HTD_RW_NW") && atoi(getenv("SESA_HTD_RW_NW")) == 8 ? 8 : 4;
+    const int FR = taps == 9 ? nw : 1, TT = 64 * nw / FR;   // (taps 1: B = F = 1, Tn = all positions)
+    const dim3 g((unsigned)((int64_t)Bk * ((F + FR - 1) / FR) * ((Tn + TT - 1) / TT)), (unsigned)(br.Cout / 48));
+    void* t0 = profile_begin(st);
+    if (nw == 8) {
+      if (taps == 9) hipLaunchKernelGGL((htd_rw3_kernel<8, 9, 8>), g, dim3(512), 0, st, ra);
+      else if (taps == 3) hipLaunchKernelGGL((htd_rw3_kernel<1, 3, 8>), g, dim3(512), 0, st, ra);
+      else hipLaunchKernelGGL((htd_rw3_kernel<1, 1, 8>), g, dim3(512), 0, st, ra);
+    } else if (taps == 9) hipLaunchKernelGGL((htd_rw3_kernel<4, 9>), g, dim3(256), 0, st, ra);
+    else if (taps == 3) hipLaunchKernelGGL((htd_rw3_kernel<1, 3>), g, dim3(256), 0, st, ra);
+    else hipLaunchKernelGGL((htd_rw3_kernel<1, 1>), g, dim3(256), 0, st, ra);
+    if (hipGetLastError() != hipSuccess) {
+      rc = SESA_ERR_HIP;
+      set_error("htdemucs: rewrite kernel launch failed");
+      return true;
+    }
+    const double M = (double)Bk * F * Tn, N = 2.0 * br.Cout, K = (double)taps * br.Cout;
+    profile_end(t0, st, SESA_KCLASS_HCONV, 2.0 * M * N * K, M * br.Cout * 4.0 * (skip ? 3.0 : 2.0));
+    return true;
+  };
   auto rewrite_glu = [&](const Gemm& gm, const float* xin, float* o, int64_t M, int C) {
     if (rw_conv) {
       conv_gemm(gm, xin, C, nullptr, o, C, (int)(M / B), 1, (int)(M / B), 1, 1, C, {0}, {}, TOK_ACT_NONE, 1, 1, 0, 0);
@@ -2472,8 +2538,12 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       const dim3 gq((unsigned)((Tn + kDcPQ - 1) / kDcPQ), (unsigned)rows);
       // per-kernel rocprofv3 on MI355X (profiles/r05_htd_dconv_*_kernel_stats.txt): the channel-group form wins at
       // 8 < h <= 16 (level 1: 251 -> 227 ms per 3 passes) and loses at h <= 8 (455 -> 498) and h <= 32 (135 -> 141)
+      // SESA_HTD_DCAPPLY8=1: the channel-pair streaming form at h <= 8 too (A/B; the time branch's long rows)
+      static const bool apq8 = getenv("SESA_HTD_DCAPPLY8") && std::string(getenv("SESA_HTD_DCAPPLY8")) == "1";
       if (apq && h > 8 && h <= 16 && C % 2 == 0 && C / 2 <= kT)
         hipLaunchKernelGGL((htd_dc_apply_q_kernel<16, 2>), gq, dim3(kT), 0, st, a);
+      else if (apq8 && h <= 8 && C % 2 == 0 && C / 2 <= kT)
+        hipLaunchKernelGGL((htd_dc_apply_q_kernel<8, 2>), gq, dim3(kT), 0, st, a);
       else if (h <= 8) hipLaunchKernelGGL(htd_dc_apply_kernel<8>, ga, dim3(kT), 0, st, a);
       else if (h <= 16) hipLaunchKernelGGL(htd_dc_apply_kernel<16>, ga, dim3(kT), 0, st, a);
       else if (h <= 32) hipLaunchKernelGGL(htd_dc_apply_kernel<32>, ga, dim3(kT), 0, st, a);
@@ -2505,7 +2575,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
               0, 0);
     if (c.dconv_mode & 1) dconv(t.edc, E, B, t.Fout, t.Cout, t.h);
     float* skt = F32(pl.st[i]);
-    rewrite_glu(t.rewrite, E, skt, (int64_t)B * t.Fout, t.Cout);
+    if (!rw3(t, E, nullptr, skt, 1, (int)((int64_t)B * t.Fout), 1))
+      rewrite_glu(t.rewrite, E, skt, (int64_t)B * t.Fout, t.Cout);
     xtm = skt;
     xt_ld = t.Cout;
     // frequency branch: conv (k x 1, stride s x 1) over F + GELU
@@ -2513,7 +2584,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
               0, 0);
     if (c.dconv_mode & 1) dconv(f.edc, E, B * f.Fout, T, f.Cout, f.h);
     float* skf = F32(pl.sf[i]);
-    rewrite_glu(f.rewrite, E, skf, (int64_t)B * f.Fout * T, f.Cout);
+    if (!rw3(f, E, nullptr, skf, 1, (int)((int64_t)B * f.Fout * T), 1))
+      rewrite_glu(f.rewrite, E, skf, (int64_t)B * f.Fout * T, f.Cout);
     if (i == 0 && c.freq_emb != 0.0 && !rc) {
       const int64_t n = (int64_t)B * f.Fout * T * f.Cout;
       SESA_REQUIRE(f.Cout % 4 == 0 && (int64_t)T * f.Cout < (1ll << 31) && f.Fout < 65536 && B < 65536,
@@ -2675,8 +2747,14 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
         return;
       }
       launch_item_stats(Xs, n_item, B, sts, st);
-      hipLaunchKernelGGL(htd_gn_apply_kernel, blocks(B * n_item), dim3(kT), 0, st, Xs, n_item, D, sts, Wb + g, Wb + b,
-                         (int64_t)B * n_item);
+      static const bool gn4 = !(getenv("SESA_HTD_STATS4") && std::string(getenv("SESA_HTD_STATS4")) == "0");
+      if (gn4 && D % 4 == 0 && n_item % 4 == 0)
+        hipLaunchKernelGGL(htd_gn_apply4_kernel,
+                           dim3((unsigned)std::min<int64_t>((n_item / 4 + kT - 1) / kT, 2048), (unsigned)B), dim3(kT), 0,
+                           st, Xs, n_item, D, sts, Wb + g, Wb + b);
+      else
+        hipLaunchKernelGGL(htd_gn_apply_kernel, blocks(B * n_item), dim3(kT), 0, st, Xs, n_item, D, sts, Wb + g, Wb + b,
+                           (int64_t)B * n_item);
       profile_end(tok, st, SESA_KCLASS_SIMT, 8.0 * (double)B * n_item, 8.0 * (double)B * n_item);
     };
     const int act = c.t_gelu ? TOK_ACT_GELU : TOK_ACT_RELU;
@@ -2742,26 +2820,6 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   if (rc) return rc;
 
   // ---- 4. decoders (:636-654): x + skip -> rewrite (3x3 / k3) + GLU -> DConv -> conv_tr -> trim -> GELU ----
-  // the halo-tile rewrite kernel (fp16mix images present; SESA_HTD_RW3=0: tok_gemm_kernel<conv> for A/B).  Returns
-  // false when it does not apply, and the caller runs the implicit GEMM.
-  auto rw3 = [&](const Branch& br, const float* x, const float* skip, float* o, int F, int Tn, int taps) -> bool {
-    static const bool on = !(getenv("SESA_HTD_RW3") && std::string(getenv("SESA_HTD_RW3")) == "0");
-    if (!on || br.rw_img < 0 || rc) return false;
-    RwArgs ra{x, skip, m->d_w + br.rw_img, Wb + br.rw_bias, o, B, F, Tn, br.Cout};
-    const int FR = taps == 9 ? 4 : 1, TT = 256 / FR;
-    const dim3 g((unsigned)((int64_t)B * ((F + FR - 1) / FR) * ((Tn + TT - 1) / TT)), (unsigned)(br.Cout / 48));
-    void* t0 = profile_begin(st);
-    if (taps == 9) hipLaunchKernelGGL((htd_rw3_kernel<4, 9>), g, dim3(256), 0, st, ra);
-    else hipLaunchKernelGGL((htd_rw3_kernel<1, 3>), g, dim3(256), 0, st, ra);
-    if (hipGetLastError() != hipSuccess) {
-      rc = SESA_ERR_HIP;
-      set_error("htdemucs: rewrite kernel launch failed");
-      return true;
-    }
-    const double M = (double)B * F * Tn, N = 2.0 * br.Cout, K = (double)taps * br.Cout;
-    profile_end(t0, st, SESA_KCLASS_HCONV, 2.0 * M * N * K, M * br.Cout * 4.0 * 3.0);
-    return true;
-  };
   const std::vector<int> r9a = {-1, -1, -1, 0, 0, 0, 1, 1, 1}, r9b = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
   const std::vector<int> r3 = {-1, 0, 1};
   std::vector<int> tr_d1(Kk / St);
