@@ -1310,6 +1310,140 @@ __global__ void __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) htd_rw3_kernel(RwA
   }
 }
 
+// ---- decoder transposed convs (fp16mix): ConvTranspose (K 8, stride S 4) along F (frequency branch, per (b, t)) or
+// along the length (time branch) as S output phases of a 2-tap conv -- GEMM row q, taps u = 0, 1 read x[q - u], column
+// n = r Cdec + co (phase r), kernel tap r + S u; output row q S + r - pad, trimmed to [0, O1) (demucs4ht.py HDecLayer
+// conv_tr + the [pad : pad + length] crop), bias + optional GELU.  The halo-tile structure of htd_rw3_kernel: per
+// 16-channel chunk the input tile (+ one halo row / column for tap 1) staged once as fp16 (32-B positions, 16-B halves
+// swizzled by position bit 3), the chunk's pre-swizzled fp16 weight image [2][96][16] by LDS-DMA; 96 GEMM columns per
+// workgroup (L0: N = 64, one group).  TWO_D: 4 q-rows x 64 t per workgroup; else 256 consecutive q.
+struct CtrArgs {
+  const float* x;      // [B][Q][T][Cin] (time branch: T = 1)
+  const uint16_t* w;   // [ceil(N / 96)][Cin / 16][2][96][16] fp16, pre-swizzled
+  const float* bias;   // [Cdec]
+  float* out;          // [B][O1][T][Cdec]
+  int B, Q, T, Cin, Cdec, S, O1, opad, act;
+};
+template <bool TWO_D>
+__global__ void __launch_bounds__(256, 2) htd_ctr_kernel(CtrArgs a) {
+  constexpr int FR = TWO_D ? 4 : 1, TT = TWO_D ? 64 : 256;
+  constexpr int HR = TWO_D ? FR + 1 : 1, HC = TWO_D ? TT : TT + 1, HP = HR * HC;
+  constexpr int X_BYTES = HP * 32, W_BYTES = rw_image_bytes(2), STAGE = X_BYTES + W_BYTES;
+  constexpr int XI = (HP * 4 + 255) / 256, NPC = W_BYTES / 1024, WPW = (NPC + 3) / 4;
+  constexpr int MI = 2, NI = 3;
+  static_assert(4 * STAGE <= 163840 && W_BYTES % 1024 == 0, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int cg = blockIdx.y, Cin = a.Cin, N = a.S * a.Cdec;
+  const int nq = a.Q + 1;                                   // GEMM rows q = 0 .. Q (tap 1 reads q - 1)
+  const int ntt = TWO_D ? (a.T + TT - 1) / TT : 1, nfr = TWO_D ? (nq + FR - 1) / FR : (nq + TT - 1) / TT;
+  int tile = blockIdx.x;
+  const int ti = tile % ntt;
+  tile /= ntt;
+  const int fi = tile % nfr, b = tile / nfr;
+  const int t0 = TWO_D ? ti * TT : 0, q0 = TWO_D ? fi * FR : fi * TT;
+  const int nk = Cin / 16;
+  const uint16_t* wsrc = a.w + (int64_t)cg * nk * (W_BYTES / 2);
+  f32x4 xr[XI];
+  auto load = [&](int kc) {
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 256 * i, p = e >> 2, qd = e & 3;
+      const int hr = p / HC, hc = p - hr * HC;
+      // halo row hr / column hc -> input row q, position t
+      const int q = TWO_D ? q0 - 1 + hr : q0 - 1 + hc, t = TWO_D ? t0 + hc : 0;
+      const bool ok = e < HP * 4 && q >= 0 && q < a.Q && t < a.T;
+      const int64_t off = ok ? (((int64_t)b * a.Q + q) * a.T + t) * Cin + kc * 16 + 4 * qd : 0;
+      xr[i] = ok ? *reinterpret_cast<const f32x4*>(a.x + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto dma_w = [&](int kc, char* stg) {
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      const int pc = w + 4 * i;
+      if (pc >= NPC) continue;
+      const uint16_t* src = wsrc + (int64_t)kc * (W_BYTES / 2) + pc * 512 + lane * 8;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stg + X_BYTES + pc * 1024), 16,
+                                       0, 0);
+    }
+  };
+  auto store = [&](char* stg) {
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 256 * i, p = e >> 2, qd = e & 3;
+      if (e >= HP * 4) continue;
+      const f32x4 v = xr[i];
+      const auto h2 = [](float x, float y) {
+        return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)y) << 16);
+      };
+      const int off = p * 32 + ((((qd >> 1) ^ (p >> 3)) & 1) << 4) + ((qd & 1) << 3);
+      *reinterpret_cast<uint2*>(stg + off) = make_uint2(h2(v[0], v[1]), h2(v[2], v[3]));
+    }
+  };
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int wr0 = TWO_D ? w : 0, wc0 = TWO_D ? 0 : 64 * w;
+  load(0);
+  dma_w(0, smem);
+  store(smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    if (kc + 1 < nk) {
+      load(kc + 1);
+      dma_w(kc + 1, smem + ((kc + 1) & 1) * STAGE);
+    }
+    const char* stg = smem + (kc & 1) * STAGE;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f16x8 af[MI], bf[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        // GEMM row (q, t) reads input q - u: halo row wr0 + 1 - u (TWO_D) / halo column c + 1 - u
+        const int p = TWO_D ? (wr0 + 1 - u) * HC + wc0 + 32 * i + l32 : wc0 + 32 * i + l32 + 1 - u;
+        af[i] = *reinterpret_cast<const f16x8*>(stg + p * 32 + (((h ^ (p >> 3)) & 1) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int qq = u * kRwCols + 32 * j + l32;
+        bf[j] = *reinterpret_cast<const f16x8*>(stg + X_BYTES + qq * 32 + (((h ^ (qq >> 3)) & 1) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (kc + 1 < nk) store(smem + ((kc + 1) & 1) * STAGE);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = cg * kRwCols + 32 * j + l32;
+    if (n >= N) continue;
+    const int r = n / a.Cdec, co = n - r * a.Cdec;
+    const float bv = a.bias[co];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int pos = wc0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * h;   // position within the wave's 64
+        const int q = TWO_D ? q0 + wr0 : q0 + pos, t = TWO_D ? t0 + pos : 0;
+        const int f = q * a.S + r - a.opad;
+        if (q >= nq || t >= a.T || f < 0 || f >= a.O1) continue;
+        float v = acc[i][j][rr] + bv;
+        if (a.act) v = gelu_erf(v);
+        a.out[(((int64_t)b * a.O1 + f) * a.T + t) * a.Cdec + co] = v;
+      }
+  }
+}
+
 // ---- transformer norms ------------------------------------------------------------------------
 // One wave per row: out = LayerNorm(in) * g + b (+ tab[row % n_tok]) (eps 1e-5, biased variance)
 __global__ void __launch_bounds__(kT) htd_layernorm_kernel(const float* __restrict__ in, float* __restrict__ out,
@@ -1555,6 +1689,7 @@ struct Branch {   // one encoder / decoder level of one branch
   int h;          // DConv hidden channels
   int64_t rw_img = -1, rw_bias = -1;   // decoder rewrite for htd_rw3_kernel (fp16mix): d_w / d_f32 offsets
   int64_t erw_img = -1, erw_bias = -1; // encoder 1x1 rewrite, same kernel (NTAP 1)
+  int64_t ctr_img = -1, ctr_bias = -1; // decoder transposed conv for htd_ctr_kernel (fp16mix)
 };
 
 struct TLayer {
@@ -2050,6 +2185,30 @@ extern "C" int sesa_htdemucs_finalize(sesa_htdemucs* m, void* stream) {
                                return W[((size_t)ci * Co + co) * K + r + St * u];
                              },
                              true, [&](int n) { return Bv[n % Co]; }, blob, bias, f16w));
+        if (f16w && Ci % 16 == 0 && K == 2 * St) {   // htd_ctr_kernel image: [ceil(N / 96)][Ci / 16][2][96][16] fp16
+          const int N = St * Co, ng = (N + kRwCols - 1) / kRwCols;
+          while (blob.size() % 8) blob.push_back(0);
+          B.ctr_img = (int64_t)blob.size();
+          for (int cg = 0; cg < ng; ++cg)
+            for (int kc = 0; kc < Ci / 16; ++kc)
+              for (int u = 0; u < 2; ++u)
+                for (int col = 0; col < kRwCols; ++col) {
+                  const int q = u * kRwCols + col, n = cg * kRwCols + col;
+                  uint16_t v16[16];
+                  for (int e = 0; e < 16; ++e) {
+                    float v = 0.f;
+                    if (n < N) {
+                      const int r = n / Co, co = n - r * Co, ci = kc * 16 + e;
+                      v = W[((size_t)ci * Co + co) * K + r + St * u];
+                    }
+                    v16[e] = __builtin_bit_cast(uint16_t, (_Float16)v);
+                  }
+                  const int sw = (q >> 3) & 1;
+                  for (int hh = 0; hh < 2; ++hh)
+                    for (int e = 0; e < 8; ++e) blob.push_back(v16[8 * (hh ^ sw) + e]);
+                }
+          B.ctr_bias = put(Bv);
+        }
       }
     }
   }
@@ -2820,6 +2979,29 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   if (rc) return rc;
 
   // ---- 4. decoders (:636-654): x + skip -> rewrite (3x3 / k3) + GLU -> DConv -> conv_tr -> trim -> GELU ----
+  // the halo-tile transposed conv (fp16mix images present; SESA_HTD_CTR=0: tok_gemm_kernel<conv> phases for A/B)
+  auto ctr = [&](const Branch& br, const float* x, float* o, int Q, int Tn, int act) -> bool {
+    static const bool on = !(getenv("SESA_HTD_CTR") && std::string(getenv("SESA_HTD_CTR")) == "0");
+    if (!on || br.ctr_img < 0 || rc) return false;
+    CtrArgs ca{x, m->d_w + br.ctr_img, Wb + br.ctr_bias, o, B, Q, Tn, br.Cout, br.Cdec, St, br.Fin, pad,
+               act == TOK_ACT_GELU ? 1 : 0};
+    const bool two_d = Tn > 1;
+    const int nq = Q + 1, N = St * br.Cdec;
+    const int64_t tiles = two_d ? (int64_t)B * ((nq + 3) / 4) * ((Tn + 63) / 64) : (int64_t)B * ((nq + 255) / 256);
+    const dim3 g((unsigned)tiles, (unsigned)((N + kRwCols - 1) / kRwCols));
+    void* t0 = profile_begin(st);
+    if (two_d) hipLaunchKernelGGL(htd_ctr_kernel<true>, g, dim3(256), 0, st, ca);
+    else hipLaunchKernelGGL(htd_ctr_kernel<false>, g, dim3(256), 0, st, ca);
+    if (hipGetLastError() != hipSuccess) {
+      rc = SESA_ERR_HIP;
+      set_error("htdemucs: transposed conv launch failed");
+      return true;
+    }
+    const double M = (double)B * nq * Tn;
+    profile_end(t0, st, SESA_KCLASS_HCONV, 2.0 * M * N * 2.0 * br.Cout,
+                4.0 * ((double)B * Q * Tn * br.Cout + (double)B * br.Fin * Tn * br.Cdec));
+    return true;
+  };
   const std::vector<int> r9a = {-1, -1, -1, 0, 0, 0, 1, 1, 1}, r9b = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
   const std::vector<int> r3 = {-1, 0, 1};
   std::vector<int> tr_d1(Kk / St);
@@ -2839,8 +3021,9 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     if (c.dconv_mode & 2) dconv(f.ddc, dB, B * f.Fout, T, f.Cout, f.h);
     // ConvTranspose2d (K x 1, stride S x 1), trim pad rows at both ends (:178-179)
     float* nxt_f = F32(pl.dA);   // cur_f (also dA) was consumed by the rewrite above (stream order)
-    conv_gemm(f.convtr, dB, f.Cout, nullptr, nxt_f, f.Cdec, f.Fout + 1, T, f.Fout, T, 1, f.Cout, tr_d1, {}, act, 0, St,
-              f.Fin, pad);
+    if (!ctr(f, dB, nxt_f, f.Fout, T, act))
+      conv_gemm(f.convtr, dB, f.Cout, nullptr, nxt_f, f.Cdec, f.Fout + 1, T, f.Fout, T, 1, f.Cout, tr_d1, {}, act, 0, St,
+                f.Fin, pad);
     cur_f = nxt_f;
     // time branch: rewrite conv1d k3 (skip on load) + GLU, DConv, ConvTranspose1d, trim [pad, pad + length)
     if (!rw3(t, cur_t, F32(pl.st[i]), tB, 1, t.Fout, 3))
@@ -2848,8 +3031,9 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
                 TOK_ACT_NONE, 1, 1, 0, 0);
     if (c.dconv_mode & 2) dconv(t.ddc, tB, B, t.Fout, t.Cout, t.h);
     float* nxt_t = F32(pl.tA);
-    conv_gemm(t.convtr, tB, t.Cout, nullptr, nxt_t, t.Cdec, t.Fout + 1, 1, t.Fout, 1, 1, t.Cout, tr_d1, {}, act, 0, St,
-              t.Fin, pad);
+    if (!ctr(t, tB, nxt_t, t.Fout, 1, act))
+      conv_gemm(t.convtr, tB, t.Cout, nullptr, nxt_t, t.Cdec, t.Fout + 1, 1, t.Fout, 1, 1, t.Cout, tr_d1, {}, act, 0, St,
+                t.Fin, pad);
     cur_t = nxt_t;
     if (rc) return rc;
   }

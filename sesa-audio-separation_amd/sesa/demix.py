@@ -60,7 +60,11 @@ def chunk_plan(L, chunk_size, num_overlap, batch_size):
 
 # Chunks per native forward, per model class (measured on MI355X, profiles/r01_bench_*): larger
 # batches amortise per-launch tails until the workspace or the gain runs out.
-EXEC_CAP = {"TFC_TDF_net": 64, "BSRoformer": 4, "MelBandRoformer": 4, "SCNet": 48, "HTDemucs": 32}
+# chunks per forward at most (288 GB of HBM: the workspace check in plan_exec_batch still halves these where memory is
+# short).  Round 5 same-box sweep (profiles/r05_n_bench_*.json): BS-Roformer 4 -> 16 +1.9 %, SCNet 48 -> 96 +3.9 %,
+# HTDemucs 32 -> 48 +1.7 % (64: the same); MDX23C 57 -> 85 per forward +0.75 % (noise level; an explicit cap of 96
+# would trip the half-free-HBM check at the vocals config's 1.7 GB per chunk), so it stays 64.
+EXEC_CAP = {"TFC_TDF_net": 64, "BSRoformer": 16, "MelBandRoformer": 16, "SCNet": 96, "HTDemucs": 48}
 
 
 def unwrap_model(model):
