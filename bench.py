@@ -195,14 +195,15 @@ def class_precision(kclass, precision, model="mdx23c", members=None):
             return p
         # the fp16 modes: conv3x3 = the one-pass (fp16w2: two-pass) fp16 direct convs; act = MDX23C's own mode
         # (its PMC stamp); fp16mix's TDF Linears mix fp16 (decoder) and bf16x3 stacks, priced at the fp16 peak (the
-        # conservative choice); the opt-in fp16 up-convs (SESA_MDX_UP16=1); everything else stays bf16x3
+        # conservative choice); the fp16 up-convs (default since round 5; SESA_MDX_UP16=0 keeps them bf16x3); everything
+        # else stays bf16x3
         if kclass == "conv3x3":
             return "fp16w2" if p == "fp16w2" else "fp16"
         if kclass == "act":
             return p
         if kclass == "tdf" and p == "fp16mix":
             return "fp16"
-        if kclass == "up" and p == "fp16mix" and os.environ.get("SESA_MDX_UP16") == "1":
+        if kclass == "up" and p == "fp16mix" and os.environ.get("SESA_MDX_UP16") != "0":
             return "fp16"
         return "bf16x3"
     if kclass == "simt":

@@ -168,8 +168,9 @@ int sesa_mdx23c_set_wino(int mode);
  * (env SESA_F16_PLAN overrides it at first use). */
 int sesa_mdx23c_set_f16_plan(const char* plan, char* prev);
 /* SESA_PREC_F16MIX plan of the TDF Linears (same layout; '1' = one fp16 pass, '3' = bf16x3; only Linears of
- * the LDS-DMA kernel's shapes run fp16).  Default "3333311111111111": the decoder stacks in fp16 (env
- * SESA_TDF_PLAN overrides it at first use). */
+ * the LDS-DMA kernel's shapes run fp16).  Default "1333111111111111": encoder levels 1-3 bf16x3, the other stacks
+ * in fp16 (env SESA_TDF_PLAN overrides it at first use).  In fp16mix the transposed up-convs also run one fp16
+ * pass (env SESA_MDX_UP16=0: bf16x3). */
 int sesa_mdx23c_set_tdf_plan(const char* plan, char* prev);
 
 /* ---------------------------------------------------------------------------------------

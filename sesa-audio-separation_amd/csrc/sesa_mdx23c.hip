@@ -348,13 +348,14 @@ std::mutex g_plan_mu;
 char g_f16_plan[17] = {0};
 
 // The TDF Linears' plan for SESA_PREC_F16MIX, same layout, digits '1' (fp16) / '3' (bf16x3); only Linears the
-// LDS-DMA kernel takes (tdf_dma_eligible) go fp16.  Default from the emulation's per-stack scan on the 0.3-RMS
-// golden with the conv plan above: the decoder stacks in fp16 add 2.7e-6 (5.235 -> 5.262e-5), encoder level 0
-// 1.05e-5, levels 1 / 2 / 3 6.1 / 3.0 / 1.8e-5 (kept bf16x3).  Encoder level 0 in fp16 too (plan
-// 1333111111111111, opt-in): worst fixture 5.25 -> 5.50e-5, same box 267.2 / 267.1x -> 270.6 / 270.5x
-// (profiles/r04_tdf0_ab_*.json) -- but with the fp16 up-convs it took the full-width ensemble's median_fft
-// blend to 1.04e-4 (profiles/r04_final_gputest_attempt1.txt), so the default keeps the encoder stacks bf16x3.
-constexpr char kTdfPlanDefault[17] = "3333311111111111";
+// LDS-DMA kernel takes (tdf_dma_eligible) go fp16.  From the emulation's per-stack scan on the 0.3-RMS golden with the
+// conv plan above: the decoder stacks in fp16 add 2.7e-6 (5.235 -> 5.262e-5), encoder level 0 1.05e-5, levels 1 / 2 / 3
+// 6.1 / 3.0 / 1.8e-5 (kept bf16x3).  Round 5 default: encoder level 0 in fp16 too (worst fixture 5.25 -> 5.50e-5, same
+// box 267.2 / 267.1x -> 270.6 / 270.5x, profiles/r04_tdf0_ab_*.json).  Round 4 had kept it opt-in because, with the
+// fp16 up-convs, the full-width ensemble's median_fft blend passed the gate (1.04e-4); the ensemble now runs its
+// MDX23C member in bf16x3 (sesa.ensemble.ENSEMBLE_PRECISIONS), so the fp16mix plan no longer reaches a blend.
+// SESA_TDF_PLAN=3333311111111111 restores the round-4 default.
+constexpr char kTdfPlanDefault[17] = "1333111111111111";
 char g_tdf_plan[17] = {0};
 
 bool tdf_plan_f16(int precision, bool enc, int level) {
@@ -837,10 +838,9 @@ extern "C" int sesa_mdx23c_finalize(sesa_mdx23c* m, void* stream) {
     pack_norm(m, m->down_norm[i], aff);
   }
   pstack(m->bottleneck, true, (int)m->enc.size());
-  // SESA_MDX_UP16=1 (opt-in): the transposed 2x2 up-convs of fp16mix on one fp16 pass (+0.55 % same box,
-  // profiles/r04_up16_ab_*.json; with the level-0 fp16 TDF it took the full-width ensemble's median_fft blend
-  // over the gate, see kTdfPlanDefault)
-  static const bool up16 = getenv("SESA_MDX_UP16") && std::string(getenv("SESA_MDX_UP16")) == "1";
+  // the transposed 2x2 up-convs of fp16mix on one fp16 pass (+0.55 % same box, worst fixture 5.50 -> 5.52e-5,
+  // profiles/r04_up16_ab_*.json; the default since round 5, see kTdfPlanDefault); SESA_MDX_UP16=0: bf16x3
+  static const bool up16 = !(getenv("SESA_MDX_UP16") && std::string(getenv("SESA_MDX_UP16")) == "0");
   for (size_t i = 0; i < m->dec.size(); ++i) {
     m->up[i].f16 = up16 && m->cfg.precision == SESA_PREC_F16MIX;
     m->up[i].f16c = 3;
