@@ -135,10 +135,21 @@ KSRC = {"conv3x3": _MDX_SRC, "tdf": _MDX_SRC, "act": _MDX_SRC, "conv1x1": _MDX_S
         "ola": ("sesa_ola.hip", "sesa_common.hpp")}
 
 
-def kernel_sources_sha16(kclass):
+# each model's own source joins its classes' stamps (a class such as simt / tokgemm / attn has launches in several
+# models, and their per-launch traffic differs): profiles/pmc_<class>_<model>.json
+MODEL_SRC = {"mdx23c": ("sesa_mdx23c.hip",), "bs_roformer": ("sesa_bsroformer.hip",), "scnet": ("sesa_scnet.hip",),
+             "htdemucs": ("sesa_htdemucs.hip",),
+             "ensemble": ("sesa_mdx23c.hip", "sesa_bsroformer.hip", "sesa_scnet.hip")}
+
+
+def kernel_sources_sha16(kclass, model=None):
     import hashlib
     h = hashlib.sha256()
-    for fn in KSRC[kclass]:
+    files = list(KSRC[kclass])
+    for fn in MODEL_SRC.get(model, ()):
+        if fn not in files:
+            files.append(fn)
+    for fn in files:
         with open(os.path.join(_CSRC, fn), "rb") as f:
             h.update(fn.encode() + b"\0" + f.read())
     return h.hexdigest()[:16]
@@ -228,23 +239,24 @@ def class_precision(kclass, precision, model="mdx23c", members=None):
     return "fp16" if "fp16" in modes else (modes.pop() if len(modes) == 1 else "bf16x3")
 
 
-def pmc_traffic(kclass, precision="bf16x3"):
-    """(HBM bytes per launch, provenance) from profiles/pmc_<class>.json when its ``src_sha16`` matches
-    the kernel sources in this tree and it was measured in the same precision mode; (None, reason)
-    otherwise -- a stale counter figure is not reported."""
-    pmc = os.path.join(REPO, "profiles", f"pmc_{kclass}.json")
+def pmc_traffic(kclass, precision="bf16x3", model=None):
+    """(HBM bytes per launch, provenance) from profiles/pmc_<class>_<model>.json when its ``src_sha16`` matches
+    the kernel sources in this tree (the class's sources + the model's own) and it was measured in the same
+    precision mode; (None, reason) otherwise -- a stale counter figure is not reported."""
+    name = f"pmc_{kclass}_{model}.json" if model else f"pmc_{kclass}.json"
+    pmc = os.path.join(REPO, "profiles", name)
     if not os.path.exists(pmc):
-        return None, f"no profiles/pmc_{kclass}.json"
+        return None, f"no profiles/{name}"
     with open(pmc) as f:
         d = json.load(f)
-    cur = kernel_sources_sha16(kclass)
+    cur = kernel_sources_sha16(kclass, model)
     if d.get("src_sha16") != cur:
-        return None, (f"profiles/pmc_{kclass}.json measured on sources {d.get('src_sha16')} (git "
+        return None, (f"profiles/{name} measured on sources {d.get('src_sha16')} (git "
                       f"{d.get('git_sha', '?')}), this tree has {cur}: stale, not reported")
     if d.get("precision", "bf16x3") != precision:
-        return None, (f"profiles/pmc_{kclass}.json measured in precision {d.get('precision', 'bf16x3')}, this run "
+        return None, (f"profiles/{name} measured in precision {d.get('precision', 'bf16x3')}, this run "
                       f"is {precision}: not reported")
-    return d.get("hbm_bytes_per_launch"), {"file": f"profiles/pmc_{kclass}.json", "src_sha16": cur,
+    return d.get("hbm_bytes_per_launch"), {"file": f"profiles/{name}", "src_sha16": cur,
                                            "git_sha": d.get("git_sha"), "precision": precision,
                                            "algorithmic_bytes_per_launch": d.get("algorithmic_bytes_per_launch")}
 
@@ -727,7 +739,8 @@ def main():
     # dominant kernel class: the model's own, or the class with the most kernel time
     kclass = MODELS[args.model][2] or max(roofs, key=lambda k: roofs[k]["ms_per_step"])
     roof = dict(roofs[kclass])
-    traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model, member_prec))
+    traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model, member_prec),
+                                       args.model)
     if isinstance(traffic_src, dict):   # one algorithmic figure: this run's (the PMC file's own is for its run)
         traffic_src.pop("algorithmic_bytes_per_launch", None)
     alg_bytes = roof["algorithmic_bytes_per_launch"]
@@ -793,7 +806,7 @@ def main():
                 # rocprofv3 counter bytes of one step of this workload (profiles/pmc_<class>.json, tools/pmc_stream.py);
                 # act: the per-launch summary of tools/pmc_traffic.py (same sha / precision rules)
                 if kc == "act":   # (measured on MDX23C's act_split / act_f16 launches: that model only)
-                    bpl, src = (pmc_traffic("act", class_precision("act", args.precision, args.model))
+                    bpl, src = (pmc_traffic("act", class_precision("act", args.precision, args.model), "mdx23c")
                                 if args.model == "mdx23c" else (None, "act counters: measured for mdx23c only"))
                     cb = bpl * kn / args.steps if bpl else None
                 else:

@@ -4,7 +4,7 @@
 # One bench step of the real workload (same exec batch as the timed run) under two separate rocprofv3 --pmc
 # passes (FETCH_SIZE, then WRITE_SIZE: MI355X_MICROARCH.md HBM section; FETCH_SIZE doubled for gfx950 in
 # tools/pmc_traffic.py), each under its own time limit; the summaries are stamped with the kernel sources'
-# sha (bench.py KSRC) and written to gpurun_out/pmc_<class>.json.
+# sha (bench.py KSRC + the model's own source) and written to gpurun_out/pmc_<class>_<model>.json.
 set -e
 M=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -18,6 +18,6 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_${M}_w -o run -- $B > $
 for spec in "$@"; do
   K=${spec%%=*}; S=${spec#*=}
   # stamped with the precision that class's kernels ran in (bench.py class_precision)
-  SESA_PMC_PRECISION=$(python3 -c "import bench; print(bench.class_precision('$K', '$P', '$M'))") \
-    python3 tools/pmc_traffic.py $O/pmc_${M}_f $O/pmc_${M}_w "$S" $O/pmc_${K}.json $K
+  SESA_PMC_PRECISION=$(python3 -c "import bench; print(bench.class_precision('$K', '$P', '$M'))") SESA_PMC_MODEL=$M \
+    python3 tools/pmc_traffic.py $O/pmc_${M}_f $O/pmc_${M}_w "$S" $O/pmc_${K}_${M}.json $K
 done

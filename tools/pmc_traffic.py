@@ -72,7 +72,9 @@ def main(fetch_dir, write_dir, substr, out=None, kclass=None):
         bench = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(bench)
         res["kernel_class"] = kclass
-        res["src_sha16"] = bench.kernel_sources_sha16(kclass)
+        model = os.environ.get("SESA_PMC_MODEL") or None
+        res["model"] = model
+        res["src_sha16"] = bench.kernel_sources_sha16(kclass, model)
         res["git_sha"] = os.environ.get("GIT_SHA", "unknown")
         res["precision"] = os.environ.get("SESA_PMC_PRECISION", "bf16x3")
     print(json.dumps(res, indent=1))

@@ -28,8 +28,8 @@ timeout -k 10 120 python3 tools/pmc_stream.py gpurun_out/pmc_mdx23c_f gpurun_out
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step pmc htdemucs
 timeout -k 10 700 bash tools/pmc_refresh.sh htdemucs \
-  "hconv=2, false, true, false|1, false, true, false|htd_rw3" \
-  "simt=htd_dc_|htd_layernorm|htd_item_stats|htd_gn_apply|htd_norm_" \
+  "hconv=2, false, true, false|1, false, true, false|htd_rw3|htd_ctr" \
+  "simt=htd_dc_|htd_item_stats|htd_gn_apply|htd_norm_freq|htd_norm_time" \
   "attn=attn_kernel|attn_f16_kernel" > $O/pmc_htdemucs.log 2>&1
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step pmc bs_roformer
@@ -37,7 +37,10 @@ timeout -k 10 700 bash tools/pmc_refresh.sh bs_roformer "tokgemm=tok_gemm" > $O/
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step pmc scnet
 timeout -k 10 700 bash tools/pmc_refresh.sh scnet "lstm=scn_lstm_mfma" \
-  "simt=scn_cm_in|scn_cm_out|scn_sdconv|scn_convtr|scn_gn_" "dft=scn_dft_mfma" > $O/pmc_scnet.log 2>&1
+  "simt=scn_cm_in|scn_cm_out|scn_sdconv|scn_convtr|scn_gelu_rows|scn_conv3x3" "dft=scn_dft_mfma" > $O/pmc_scnet.log 2>&1
+rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
+step pmc ensemble
+timeout -k 10 900 bash tools/pmc_refresh.sh ensemble "tokgemm=tok_gemm" > $O/pmc_ensemble.log 2>&1
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 mkdir -p $O/pmc
 cp gpurun_out/pmc_*.json $O/pmc/ 2>/dev/null || true
