@@ -58,6 +58,14 @@ class HTDemucs(NativeModule):
             refuse.append("group-norm transformer variants")
         if refuse:
             raise NotImplementedError("HTDemucs native engine: unsupported configuration: " + ", ".join(refuse))
+        if not k["t_gelu"]:
+            # the native fp16mix transformer writes its FF1 output through a GELU-only fp16 epilogue: a ReLU
+            # transformer (t_gelu=False) runs bf16x3 / bf16 only, and --enable_amp maps it to bf16x3
+            self._precisions = ("bf16x3", "bf16")
+            self._amp_precision = "bf16x3"
+            if self.precision == "fp16mix":
+                raise ValueError("HTDemucs: precision 'fp16mix' needs t_gelu=True (the fp16 FF1 epilogue is GELU "
+                                 "only); use 'bf16x3'")
         self.sources = list(sources)
         self.audio_channels = int(audio_channels)
         self.samplerate = samplerate

@@ -76,6 +76,19 @@ def test_load_state_dict_strict_and_errors():
     assert res.missing_keys == ["encoder.0.conv.bias"]
 
 
+def test_relu_transformer_has_no_fp16mix():
+    """The native fp16mix transformer writes FF1 through a GELU-only fp16 epilogue: a t_gelu=False model refuses
+    fp16mix at construction / set_precision, and --enable_amp (the backend's _amp_precision) maps it to bf16x3."""
+    from sesa.models.htdemucs import HTDemucs
+    with pytest.raises(ValueError, match="t_gelu"):
+        HTDemucs(["a", "b"], t_gelu=False, precision="fp16mix")
+    m = HTDemucs(["a", "b"], t_gelu=False)
+    assert m._amp_precision == "bf16x3"
+    with pytest.raises(ValueError):
+        m.set_precision("fp16mix")
+    assert HTDemucs(["a", "b"])._amp_precision == "fp16mix"
+
+
 def test_create_rejects_unsupported():
     from sesa.models.htdemucs import HTDemucs
     with pytest.raises(NotImplementedError):
