@@ -40,7 +40,7 @@ timeout -k 10 700 bash tools/pmc_refresh.sh scnet "lstm=scn_lstm_mfma" \
   "simt=scn_cm_in|scn_cm_out|scn_sdconv|scn_convtr|scn_gelu_rows|scn_conv3x3" "dft=scn_dft_mfma" > $O/pmc_scnet.log 2>&1
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step pmc ensemble
-timeout -k 10 900 bash tools/pmc_refresh.sh ensemble "tokgemm=tok_gemm" > $O/pmc_ensemble.log 2>&1
+timeout -k 10 900 bash tools/pmc_refresh.sh ensemble "conv3x3=conv3x3_db_kernel|tap_gemm_kernel<3, 3" "tokgemm=tok_gemm" > $O/pmc_ensemble.log 2>&1
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 mkdir -p $O/pmc
 cp gpurun_out/pmc_*.json $O/pmc/ 2>/dev/null || true
