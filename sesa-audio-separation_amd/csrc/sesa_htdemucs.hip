@@ -1175,7 +1175,11 @@ constexpr int kRwOS = 52;   // epilogue LDS tile row stride (floats)
 __host__ __device__ constexpr int rw_image_bytes(int ntap) { return ntap * kRwCols * 32; }   // whole 1 KiB pieces
 // NWV waves (256 or 512 threads): wave w covers halo row w / WPR, positions 64 (w % WPR) .. + 63, WPR = NWV / FR waves
 // per row; the 8-wave form halves the per-position weight-image traffic and halo overhead at one workgroup per CU.
-template <int FR, int NTAP, int NWV = 4>
+// PERS: persistent workgroups (grid.x < tiles): each walks tiles blockIdx.x, + gridDim.x, ...; the next tile's first
+// chunk (halo loads + weight DMA) is issued under the current tile's last chunk, so no tile starts on an exposed
+// load (level 0 has only C / 16 = 3 chunks per tile); its epilogue stores straight from registers (the LDS holds the
+// next tile's first stage).
+template <int FR, int NTAP, int NWV = 4, bool PERS = false>
 __global__ void __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) htd_rw3_kernel(RwArgs a) {
   static_assert(NTAP == 9 || NTAP == 3 || NTAP == 1, "3x3, k3 or 1x1");
   constexpr int NT = 64 * NWV, WPR = NWV / FR, TT = 64 * WPR, PF = NTAP == 9 ? 1 : 0;
@@ -1192,15 +1196,20 @@ __global__ void __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) htd_rw3_kernel(RwA
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int cg = blockIdx.y, C = a.C;
   const int ntt = (a.T + TT - 1) / TT, nfr = (a.F + FR - 1) / FR;
+  const int ntiles = a.B * nfr * ntt;
   int tile = blockIdx.x;
-  const int ti = tile % ntt;
-  tile /= ntt;
-  const int fi = tile % nfr, b = tile / nfr;
-  const int t0 = ti * TT, f0 = fi * FR;
+  auto decode = [&](int tl, int& bb, int& ff0, int& tt0) {   // (workgroup-uniform: scalar registers)
+    const int ti = tl % ntt, rest = tl / ntt;
+    tt0 = __builtin_amdgcn_readfirstlane(ti * TT);
+    ff0 = __builtin_amdgcn_readfirstlane((rest % nfr) * FR);
+    bb = __builtin_amdgcn_readfirstlane(rest / nfr);
+  };
+  int b, f0, t0;
+  decode(tile, b, f0, t0);
   const int nk = C / 16;
   const uint16_t* wsrc = a.w + (int64_t)cg * nk * (W_BYTES / 2);
   f32x4 xr[XI], sr[XI];
-  auto load = [&](int kc) {
+  auto load_t = [&](int b, int f0, int t0, int kc) {
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int e = tid + NT * i, p = e >> 2, q = e & 3;
@@ -1245,17 +1254,7 @@ __global__ void __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) htd_rw3_kernel(RwA
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   // this wave's halo origin: row, column offset of its 64 positions
   const int wr0 = w / WPR, wc0 = 64 * (w % WPR);
-  load(0);
-  dma_w(0, smem);
-  store(smem);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kc = 0; kc < nk; ++kc) {
-    if (kc + 1 < nk) {
-      load(kc + 1);
-      dma_w(kc + 1, smem + ((kc + 1) & 1) * STAGE);   // that buffer's readers (chunk kc - 1) are behind the barrier
-    }
-    const char* stg = smem + (kc & 1) * STAGE;
+  auto compute = [&](const char* stg) {
 #pragma unroll
     for (int tap = 0; tap < NTAP; ++tap) {
       const int df = NTAP == 9 ? tap / 3 : 0, dt = NTAP == 9 ? tap % 3 : NTAP == 3 ? tap : 1;   // halo offsets (0..2)
@@ -1276,6 +1275,64 @@ __global__ void __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) htd_rw3_kernel(RwA
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
+  };
+  load_t(b, f0, t0, 0);
+  dma_w(0, smem);
+  store(smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (PERS) {
+    int g = 0;   // chunks consumed by this workgroup: stage g & 1
+    for (;;) {
+      const int ntile = tile + (int)gridDim.x;
+      const bool more = ntile < ntiles;
+      for (int kc = 0; kc < nk; ++kc, ++g) {
+        const bool last = kc + 1 == nk, pre = !last || more;
+        char* nxt = smem + ((g + 1) & 1) * STAGE;
+        if (pre) {   // the next chunk of this tile, or the next tile's first chunk
+          if (!last) {
+            load_t(b, f0, t0, kc + 1);
+          } else {
+            int nb, nf0, nt0;
+            decode(ntile, nb, nf0, nt0);
+            load_t(nb, nf0, nt0, 0);
+          }
+          dma_w(last ? 0 : kc + 1, nxt);
+        }
+        compute(smem + (g & 1) * STAGE);
+        if (pre) store(nxt);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      // epilogue straight from registers: bias, GLU across lane pairs (l32 ^ 16), lanes l32 < 16 store
+      const int f = f0 + wr0;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int ch = cg * 48 + 16 * j + (l32 & 15);
+        const float bv = a.bias[(l32 < 16 ? 0 : C) + ch];
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = acc[i][j][r] + bv;
+            const float gt = __shfl_xor(v, 16);
+            const int t = t0 + wc0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (l32 < 16 && f < a.F && t < a.T)
+              a.out[(((int64_t)b * a.F + f) * a.T + t) * C + ch] = v * (1.0f / (1.0f + __expf(-gt)));
+            acc[i][j][r] = 0.f;
+          }
+      }
+      if (!more) return;
+      tile = ntile;
+      decode(tile, b, f0, t0);
+    }
+  }
+  for (int kc = 0; kc < nk; ++kc) {
+    if (kc + 1 < nk) {
+      load_t(b, f0, t0, kc + 1);
+      dma_w(kc + 1, smem + ((kc + 1) & 1) * STAGE);   // that buffer's readers (chunk kc - 1) are behind the barrier
+    }
+    compute(smem + (kc & 1) * STAGE);
     if (kc + 1 < nk) store(smem + ((kc + 1) & 1) * STAGE);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the weight DMA landed
     __syncthreads();
@@ -1660,6 +1717,103 @@ __global__ void htd_istft_ola_kernel(const float* __restrict__ fw, int T, int L,
   mean_std(tstats + 2 * b, (int64_t)ach * L, mt, st);
   const float xt = XT[((int64_t)b * L + i) * (nsrc * ach) + rem] * st + mt;
   out[(int64_t)sig * L + i] = xt + acc / env;
+}
+
+// Round 5: _mask + _ispec frames + the istft overlap-add in ONE kernel (htd_istft_frames_kernel + htd_istft_ola_kernel
+// wrote every windowed 4096-sample frame to HBM and read it back four times: ~12 GB per forward at exec batch 48).  A
+// workgroup owns one signal and a segment of kIstSeg padded frames: it walks frames tp = seg start - 3 .. seg end - 1
+// (the three before the segment only feed its first samples), accumulates each windowed inverse FFT into a 4096-sample
+// LDS ring (sample n at n mod 4096), and after frame tp emits the hop of samples [tp hop, tp hop + hop) -- no later
+// frame reaches them -- as out = xt + acc / env (the same envelope and time-branch sum as the OLA kernel), zeroing
+// those ring slots for n + 4096.  Grid ids put the nsrc * ach signals of one (item, segment) 8 apart (one XCD), so
+// the spectrum lines they share ([b][k][t][Cz]: bin k of frames t, t + 1 for every signal) are fetched once per XCD.
+constexpr int kIstSeg = 32;
+__global__ void __launch_bounds__(kT) htd_istft_fused_kernel(const float* __restrict__ Z, int T, int Cz, int ach,
+                                                             int nsrc, int n_items, int nseg,
+                                                             const double* __restrict__ stats, int64_t n_item,
+                                                             const float* __restrict__ win, Fft2048Tables tb, int L,
+                                                             const float* __restrict__ XT,
+                                                             const double* __restrict__ tstats,
+                                                             float* __restrict__ out) {
+  __shared__ float2 bufA[kFft2048];
+  __shared__ float2 bufB[kFft2048 + 1];
+  __shared__ float ring[kFft4096];
+  const int nper = nsrc * ach;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int gi = xcd + 8 * (slot / nper), j = slot % nper;
+  const int b = gi / nseg, seg = gi - b * nseg;
+  if (b >= n_items) return;   // (whole workgroup: grid padding)
+  const int n0 = kPadSpec + kCenter, n1 = n0 + L;   // output samples i = n - n0
+  const int tpa = n0 / kHop + seg * kIstSeg, tpb = min((n1 - 1) / kHop + 1, tpa + kIstSeg);
+  if (tpa >= tpb) return;
+  const int sig = b * nper + j, s = j / ach, c = j - s * ach;
+  const int ch = s * 2 * ach + 2 * c;
+  float mean, sd, mt, st;
+  mean_std(stats + 2 * b, n_item, mean, sd);
+  mean_std(tstats + 2 * b, (int64_t)ach * L, mt, st);
+  const float sc = 2.0f / 64.0f;
+  for (int i = threadIdx.x; i < kFft4096; i += kT) ring[i] = 0.f;
+  // spectrum bins of the next real frame in registers: loaded under the current frame's FFT
+  constexpr int KPT = (kFft2048 + 1 + kT - 1) / kT;   // bins per thread (9)
+  float2 xs[KPT];
+  auto load_frame = [&](int tc) {
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int k = threadIdx.x + u * kT;
+      float2 X = make_float2(0.f, 0.f);
+      if (k < kF0) {
+        const float2 v = *reinterpret_cast<const float2*>(Z + (((int64_t)b * kF0 + k) * T + tc) * Cz + ch);
+        X = make_float2(v.x * sd + mean, v.y * sd + mean);
+      }
+      if (k == 0) X.y = 0.f;
+      xs[u] = X;
+    }
+  };
+  auto real = [&](int tp) { return tp >= 0 && tp - 2 >= 0 && tp - 2 < T; };
+  {
+    int tp = tpa - 3;
+    while (tp < tpb && !real(tp)) ++tp;
+    if (tp < tpb) load_frame(tp - 2);
+  }
+  for (int tp = tpa - 3; tp < tpb; ++tp) {
+    if (real(tp)) {   // (uniform)
+      __syncthreads();   // the previous frame's ring add (reads of z) and emit are done
+#pragma unroll
+      for (int u = 0; u < KPT; ++u) {
+        const int k = threadIdx.x + u * kT;
+        if (k <= kFft2048) bufB[k] = xs[u];
+      }
+      int nx = tp + 1;   // the next real frame: its loads fly under this frame's FFT
+      while (nx < tpb && !real(nx)) ++nx;
+      if (nx < tpb) load_frame(nx - 2);
+      __syncthreads();
+      for (int k = threadIdx.x; k < kFft2048; k += kT) bufA[k] = irfft_pack(bufB, tb.twN, k);
+      const float2* z = fft2048<true>(bufA, bufB, tb.tw);   // (returns after a barrier)
+      for (int k = threadIdx.x; k < kFft2048; k += kT) {
+        const float2 v = z[k];
+        const int pos = (tp * kHop + 2 * k) & (kFft4096 - 1);
+        ring[pos] += v.x * sc * win[2 * k];
+        ring[pos + 1] += v.y * sc * win[2 * k + 1];
+      }
+    }
+    __syncthreads();
+    // samples [tp hop, tp hop + hop) are complete: emit the segment's, then clear their slots
+    for (int mm = threadIdx.x; mm < kHop; mm += kT) {
+      const int n = tp * kHop + mm, idx = n & (kFft4096 - 1);
+      if (tp >= tpa && n >= n0 && n < n1) {
+        const int tq_lo = max(0, (n - kFft4096 + kHop) / kHop), tq_hi = min(T + 3, n / kHop);
+        float env = 0.f;
+        for (int tq = tq_lo; tq <= tq_hi; ++tq) {
+          const float w = win[n - tq * kHop];
+          env = fmaf(w, w, env);
+        }
+        const int i = n - n0;
+        const float xt = XT[((int64_t)b * L + i) * nper + j] * st + mt;
+        out[(int64_t)sig * L + i] = xt + ring[idx] / env;
+      }
+      ring[idx] = 0.f;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2512,6 +2666,8 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     RwArgs ra{x, skip, m->d_w + img, Wb + boff, o, Bk, F, Tn, br.Cout};
     // SESA_HTD_RW_NW=8: 512-thread workgroups (8 rows x 64 / 512 positions; one per CU) instead of 256 (two per CU)
     static const int nw = getenv("SESA_HTD_RW_NW") && atoi(getenv("SESA_HTD_RW_NW")) == 8 ? 8 : 4;
+    // SESA_HTD_RW_PERS=1: persistent workgroups with the next tile's first chunk prefetched (A/B)
+    static const bool pers = getenv("SESA_HTD_RW_PERS") && std::string(getenv("SESA_HTD_RW_PERS")) == "1";
     const int FR = taps == 9 ? nw : 1, TT = 64 * nw / FR;   // (taps 1: B = F = 1, Tn = all positions)
     const dim3 g((unsigned)((int64_t)Bk * ((F + FR - 1) / FR) * ((Tn + TT - 1) / TT)), (unsigned)(br.Cout / 48));
     void* t0 = profile_begin(st);
@@ -2519,6 +2675,12 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       if (taps == 9) hipLaunchKernelGGL((htd_rw3_kernel<8, 9, 8>), g, dim3(512), 0, st, ra);
       else if (taps == 3) hipLaunchKernelGGL((htd_rw3_kernel<1, 3, 8>), g, dim3(512), 0, st, ra);
       else hipLaunchKernelGGL((htd_rw3_kernel<1, 1, 8>), g, dim3(512), 0, st, ra);
+    } else if (pers) {
+      // persistent: two workgroups per CU (256 CUs), each walking its share of the position tiles
+      const dim3 gp((unsigned)std::min<int64_t>(g.x, 512), g.y);
+      if (taps == 9) hipLaunchKernelGGL((htd_rw3_kernel<4, 9, 4, true>), gp, dim3(256), 0, st, ra);
+      else if (taps == 3) hipLaunchKernelGGL((htd_rw3_kernel<1, 3, 4, true>), gp, dim3(256), 0, st, ra);
+      else hipLaunchKernelGGL((htd_rw3_kernel<1, 1, 4, true>), gp, dim3(256), 0, st, ra);
     } else if (taps == 9) hipLaunchKernelGGL((htd_rw3_kernel<4, 9>), g, dim3(256), 0, st, ra);
     else if (taps == 3) hipLaunchKernelGGL((htd_rw3_kernel<1, 3>), g, dim3(256), 0, st, ra);
     else hipLaunchKernelGGL((htd_rw3_kernel<1, 1>), g, dim3(256), 0, st, ra);
@@ -3046,13 +3208,29 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     const int64_t n_groups = (int64_t)B * ((T + 1) / 2);
     const int64_t n_ids = 8 * (int64_t)(2 * m->nsrc * ach) * ((n_groups + 7) / 8);
     SESA_REQUIRE(n_ids < (1ll << 31), SESA_ERR_INVALID, "htdemucs forward: iSTFT grid too large");
-    hipLaunchKernelGGL(htd_istft_frames_kernel, dim3((unsigned)n_ids), dim3(kT), 0, st, cur_f, T, m->fq[0].Cdec, ach,
-                       m->nsrc, B, st_f, (int64_t)kF0 * T * 2 * ach, win, tb, FR);
-    SESA_CHECK_LAUNCH();
-    hipLaunchKernelGGL(htd_istft_ola_kernel, dim3((L + kT - 1) / kT, nsig), dim3(kT), 0, st, FR, T, L, ach, m->nsrc, win,
-                       cur_t, st_t, out);
-    SESA_CHECK_LAUNCH();
-    profile_end(tok, st, SESA_KCLASS_ISTFT, 4.0 * nsig * ((double)T * kF0 * 2 + 2.0 * (double)T * kFft4096 + 2.0 * L));
+    // frames + overlap-add in one kernel (iSTFT class 70.2 -> 61.3 ms per step same box, profiles/r05_s_bench_htd_*.json;
+    // no 4096-sample frame buffer in HBM); SESA_HTD_ISTFT_FUSED=0: the two-kernel form (A/B)
+    static const bool fused = !(getenv("SESA_HTD_ISTFT_FUSED") && std::string(getenv("SESA_HTD_ISTFT_FUSED")) == "0");
+    if (fused) {
+      const int nper = m->nsrc * ach;
+      const int tp_n = (kPadSpec + kCenter + L - 1) / kHop - (kPadSpec + kCenter) / kHop + 1;
+      const int nseg = (tp_n + kIstSeg - 1) / kIstSeg;
+      const int64_t groups = (int64_t)B * nseg;
+      const int64_t ids = 8 * (int64_t)nper * ((groups + 7) / 8);
+      SESA_REQUIRE(ids < (1ll << 31), SESA_ERR_INVALID, "htdemucs forward: iSTFT grid too large");
+      hipLaunchKernelGGL(htd_istft_fused_kernel, dim3((unsigned)ids), dim3(kT), 0, st, cur_f, T, m->fq[0].Cdec, ach,
+                         m->nsrc, B, nseg, st_f, (int64_t)kF0 * T * 2 * ach, win, tb, L, cur_t, st_t, out);
+      SESA_CHECK_LAUNCH();
+      profile_end(tok, st, SESA_KCLASS_ISTFT, 4.0 * nsig * ((double)T * kF0 * 2 + 2.0 * L));
+    } else {
+      hipLaunchKernelGGL(htd_istft_frames_kernel, dim3((unsigned)n_ids), dim3(kT), 0, st, cur_f, T, m->fq[0].Cdec, ach,
+                         m->nsrc, B, st_f, (int64_t)kF0 * T * 2 * ach, win, tb, FR);
+      SESA_CHECK_LAUNCH();
+      hipLaunchKernelGGL(htd_istft_ola_kernel, dim3((L + kT - 1) / kT, nsig), dim3(kT), 0, st, FR, T, L, ach, m->nsrc,
+                         win, cur_t, st_t, out);
+      SESA_CHECK_LAUNCH();
+      profile_end(tok, st, SESA_KCLASS_ISTFT, 4.0 * nsig * ((double)T * kF0 * 2 + 2.0 * (double)T * kFft4096 + 2.0 * L));
+    }
   }
   return SESA_OK;
 }
