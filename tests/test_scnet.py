@@ -195,3 +195,35 @@ def test_forward_odd_lengths_match_oracle(dev, L):
     y = m(torch.from_numpy(x).to(dev)).cpu().numpy()
     assert y.shape == ref.shape == (1, 4, 2, L)
     assert rms(y, ref) <= RMS_GATE
+
+
+def test_feature_conversion_dft_matrices_match_numpy_fft():
+    """scn_dft_mfma_kernel's formulation (sesa_scnet.hip finalize): FeatureConversion (separation.py:20-34, norm
+    "ortho") as out = D @ in with rfft D = [s cos; -s sin] (2K x T, real parts then imaginary parts) and irfft
+    D = [s w cos | -s w sin] (T x 2K, w = 1 at DC / Nyquist else 2, the imaginary DC / Nyquist columns zero).
+    Checked here in float64 against numpy's FFTs -- the matrices the kernel packs (bf16 hi / lo) are these."""
+    rng = np.random.default_rng(0)
+    T, C = 18, 5
+    K = T // 2 + 1
+    s = 1.0 / np.sqrt(T)
+    k = np.arange(K)[:, None]
+    t = np.arange(T)[None, :]
+    ang = 2 * np.pi * ((k * t) % T) / T
+    Dr = np.concatenate([s * np.cos(ang), -s * np.sin(ang)], axis=0)          # [2K][T]
+    x = rng.standard_normal((T, C))
+    y = Dr @ x
+    ref = np.fft.rfft(x, axis=0, norm="ortho")
+    assert np.allclose(y[:K], ref.real, atol=1e-12) and np.allclose(y[K:], ref.imag, atol=1e-12)
+    w = np.where((np.arange(K) == 0) | (np.arange(K) == K - 1), 1.0, 2.0)[None, :]
+    edge = ((np.arange(K) == 0) | (np.arange(K) == K - 1))[None, :]
+    angi = ang.T                                                                # [T][K]
+    Di = np.concatenate([s * w * np.cos(angi), np.where(edge, 0.0, -s * w * np.sin(angi))], axis=1)   # [T][2K]
+    spec_in = np.concatenate([ref.real, ref.imag], axis=0)                     # [2K][C]
+    assert np.allclose(Di @ spec_in, x, atol=1e-12)
+    # irfft ignores the imaginary parts of DC and Nyquist: so do the zero columns
+    noisy = ref.copy()
+    noisy[0] += 1j * rng.standard_normal(C)
+    noisy[K - 1] += 1j * rng.standard_normal(C)
+    noisy[1:K - 1] += rng.standard_normal((K - 2, C)) + 1j * rng.standard_normal((K - 2, C))
+    back = Di @ np.concatenate([noisy.real, noisy.imag], axis=0)
+    assert np.allclose(back, np.fft.irfft(noisy, n=T, axis=0, norm="ortho"), atol=1e-12)
