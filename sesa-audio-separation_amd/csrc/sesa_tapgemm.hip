@@ -490,6 +490,12 @@ constexpr int kActMaxC = 1024;
 // buffer resource base (SALU), and one counted wait + barrier per chunk replaces the register staging
 // (load_item / store_main: ~200 VALU and 7 ds_write_b128 per thread per chunk).  The A image is padded to whole
 // 1-KiB DMA pieces (37 KiB), so a stage is 55 KiB and two stages sit in the same LDS as before.
+// SCR = 3 (MDMA only): the fused 1x1 shortcut INTERLEAVED with the main chunks -- shortcut chunk kc rides in main
+// iteration kc: its W1 image (hi + lo, 4 KiB) is DMA'd into the main stage beside W, and each lane loads its own
+// A fragments (4 rows x 32 B of the raw fp32 block input, 32 VGPRs) one iteration ahead, so the HBM stream of the
+// raw input runs under the MFMA-bound main loop instead of in a phase of its own after it (where it was bound by
+// the bytes a CU keeps in flight).  Shortcut chunks beyond n_main (decoder blocks: the block input has 2 C
+// channels) run on the per-wave DMA ring afterwards, as SCR = 2.
 template <bool X3, bool XTRA, int EPI = 0, bool ACT = false, int F16 = 0, bool MI4 = false, int SCR = 0,
           int SCD = 2, bool ORD = false, int MDMA = 0>
 __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
@@ -497,7 +503,9 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   static_assert(!MDMA || (MI4 && F16 == 1 && !ACT), "MDMA: the fp16 32-row tile on pre-activated planes");
   static_assert(!MI4 || (F16 == 1 && !ACT), "MI4: fp16 single pass on pre-activated planes");
   static_assert(!SCR || (XTRA && X3), "SCR: the bf16x3 fused shortcut from registers / per-wave LDS-DMA");
-  static_assert(SCR != 2 || MI4, "SCR 2: the 32-row tile (one wave = 4 rows of 32 positions)");
+  static_assert(SCR < 2 || MI4, "SCR 2 / 3: the 32-row tile (one wave = 4 rows of 32 positions)");
+  static_assert(SCR != 3 || MDMA, "SCR 3: the interleaved shortcut rides the LDS-DMA main loop");
+  constexpr bool SCI = SCR == 3;
   constexpr bool ALO = X3 && F16 == 0;  // main chunks read an A lo image
   constexpr bool WLO = X3 && F16 != 1;  // main chunks read a W lo image
   constexpr int NT = 512;
@@ -511,14 +519,15 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   constexpr int A_IMG_M = MDMA ? (A_BYTES + 1023) / 1024 * 1024 : A_BYTES;   // MDMA: whole 1-KiB pieces
   constexpr int WOFF_M = MDMA ? A_IMG_M : (ALO ? 2 : 1) * A_BYTES;
   constexpr int WOFF_X = 2 * A_BYTES;
-  constexpr int STAGE_M = WOFF_M + (WLO ? 2 : 1) * W_BYTES;
+  constexpr int W1OFF_M = WOFF_M + (WLO ? 2 : 1) * W_BYTES;   // SCI: the shortcut chunk's W1 image (hi + lo)
+  constexpr int STAGE_M = W1OFF_M + (SCI ? 2 * W1_BYTES : 0);
   constexpr int STAGE_X = XTRA ? WOFF_X + 2 * W1_BYTES : 0;
   constexpr int STAGE = MI4 ? (STAGE_M > STAGE_X ? STAGE_M : STAGE_X) : 2 * A_BYTES + 2 * W_BYTES;
   // (one LDS array: the ACT affine table sits past the two stages)
   // SCR 2: the shortcut phase's per-wave rings take the whole 160 KiB (8 waves x kScrWave)
   constexpr int kScrWave = 2 * 8192 + 4096;
   constexpr int SMEM_B = 2 * STAGE + (ACT ? 2 * kActMaxC * 4 : 0);
-  __shared__ __attribute__((aligned(16))) char smem[SCR == 2 && 8 * kScrWave > SMEM_B ? 8 * kScrWave : SMEM_B];
+  __shared__ __attribute__((aligned(16))) char smem[SCR >= 2 && 8 * kScrWave > SMEM_B ? 8 * kScrWave : SMEM_B];
   float* act_sc = reinterpret_cast<float*>(smem + 2 * STAGE);
   float* act_sh = act_sc + kActMaxC;
 
@@ -779,9 +788,12 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
 
   // ---- main chunks: straight-line pipelined body, clamped (redundant) prefetch at the tail ----
   // MDMA: this wave's DMA pieces per chunk (A pieces first, then the W image's), wave-uniform piece index
-  constexpr int MD_A_PC = A_IMG_M / 1024, MD_PC = MD_A_PC + W_BYTES / 1024, MD_PPW = (MD_PC + 7) / 8;
-  uint32_t mdo[MDMA ? MD_PPW : 1];   // per-lane source byte offsets (A: from the chunk-0 plane base; W: image)
+  constexpr int MD_A_PC = A_IMG_M / 1024, MD_W_END = MD_A_PC + W_BYTES / 1024;
+  constexpr int MD_PC = MD_W_END + (SCI ? 2 * W1_BYTES / 1024 : 0), MD_PPW = (MD_PC + 7) / 8;
+  uint32_t mdo[MDMA ? MD_PPW : 1];   // per-lane source byte offsets (A: from the chunk-0 plane base; W / W1: image)
   const int wv = __builtin_amdgcn_readfirstlane(wm);
+  // SCI: shortcut chunks 0 .. n_sci - 1 interleaved with the main chunks, the rest on the ring afterwards
+  const int n_sci = SCI ? min(a.x_chunks, n_main) : 0;
   auto md_issue = [&](int kc, char* stg) {
     if constexpr (MDMA) {
       const uint32_t plane_bytes = (uint32_t)((int64_t)a.T_in * a.F_in * C * 2);
@@ -791,6 +803,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
           __builtin_amdgcn_make_buffer_rsrc((void*)const_cast<char*>(abase), (short)0, (int)(plane_bytes - kc * 32), 0x00020000);
       const __amdgpu_buffer_rsrc_t rw =
           __builtin_amdgcn_make_buffer_rsrc((void*)const_cast<char*>(wbase), (short)0, W_BYTES, 0x00020000);
+      // SCI: shortcut chunk kc's W1 image (hi + lo), stored after the main chunks' images
+      const char* w1base = reinterpret_cast<const char*>(wblk + (int64_t)n_main * W_BYTES) + (int64_t)kc * 2 * W1_BYTES;
+      const __amdgpu_buffer_rsrc_t rw1 =
+          __builtin_amdgcn_make_buffer_rsrc((void*)const_cast<char*>(w1base), (short)0, 2 * W1_BYTES, 0x00020000);
 #pragma unroll
       for (int i = 0; i < MD_PPW; ++i) {
         // (the voffset as int: an unsigned lvalue here made the host pass silently drop this kernel's launch stub)
@@ -798,9 +814,61 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
         if (pc < MD_A_PC)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(stg + pc * 1024), 16,
                                                    (int)mdo[i], 0, 0, 0);
-        else if (pc < MD_PC)
+        else if (pc < MD_W_END)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               rw, (__attribute__((address_space(3))) void*)(stg + WOFF_M + (pc - MD_A_PC) * 1024), 16, (int)mdo[i], 0, 0, 0);
+        else if (pc < MD_PC && kc < n_sci)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rw1, (__attribute__((address_space(3))) void*)(stg + W1OFF_M + (pc - MD_W_END) * 1024), 16, (int)mdo[i], 0, 0,
+              0);
+      }
+    }
+  };
+  // SCI: this lane's A fragments of shortcut chunk kx -- rows wm MI + i, position f0 + l32, channels 8 h .. 8 h + 7
+  // of the chunk (32 contiguous bytes of the raw fp32 input; rows past T_in clamped here, zeroed at the split)
+  f32x4 xa[SCI ? MI : 1][2];
+  auto sci_load = [&](int kx) {
+    if constexpr (SCI) {
+      const int k0 = kx * kConvBK;
+      const int sx = k0 < a.xin.C_split ? 0 : 1;
+      const Src xs = pick_src(a.xin, sx);
+      const int cl0 = k0 - (sx ? a.xin.C_split : 0) + 8 * h;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int t = min(t0 + wm * MI + i, a.T_in - 1);
+        const f32x4* q =
+            reinterpret_cast<const f32x4*>(xs.ptr + (((int64_t)b * a.T_in + t) * a.F_in + f0 + l32) * xs.C + cl0);
+        xa[i][0] = q[0];
+        xa[i][1] = q[1];
+      }
+    }
+  };
+  // SCI: the bf16x3 MFMAs of the shortcut chunk in xa against the W1 image of stage stg (the ring's arithmetic)
+  auto sci_mma = [&](const char* stg) {
+    if constexpr (SCI) {
+      const char* wimg = stg + W1OFF_M;
+      bf16x8 bh[NI], bl[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int p = j * 32 + l32;
+        const int off = p * 32 + ((h ^ ((p >> 3) & 1)) << 4);
+        bh[j] = *reinterpret_cast<const bf16x8*>(wimg + off);
+        bl[j] = *reinterpret_cast<const bf16x8*>(wimg + W1_BYTES + off);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const bool ok = t0 + wm * MI + i < a.T_in;
+        __bf16 hv[8], lv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) split_bf16(ok ? xa[i][q >> 2][q & 3] : 0.f, hv[q], lv[q]);
+        const bf16x8 ah = bf16x8{hv[0], hv[1], hv[2], hv[3], hv[4], hv[5], hv[6], hv[7]};
+        const bf16x8 al = bf16x8{lv[0], lv[1], lv[2], lv[3], lv[4], lv[5], lv[6], lv[7]};
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          acc[i][j] = mfma32(al, bh[j], acc[i][j]);
+          acc[i][j] = mfma32(ah, bl[j], acc[i][j]);
+          acc[i][j] = mfma32(ah, bh[j], acc[i][j]);
+        }
       }
     }
   };
@@ -820,12 +888,15 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
           const int hf = (lane & 1) ^ ((p >> 3) & 1);
           if (p < NPOS && ti >= 0 && ti < a.T_in && fi >= 0 && fi < a.F_in)
             v = (uint32_t)((((int64_t)ti * a.F_in + fi) * C + 8 * hf) * 2);
-        } else if (pc < MD_PC) {
+        } else if (pc < MD_W_END) {
           v = (uint32_t)((pc - MD_A_PC) * 1024 + lane * 16);
+        } else if (pc < MD_PC) {
+          v = (uint32_t)((pc - MD_W_END) * 1024 + lane * 16);
         }
         mdo[i] = v;
       }
       md_issue(0, smem);
+      if (SCI && n_sci > 0) sci_load(0);
     } else {
       load_main(0);
       if constexpr (ACT) __syncthreads();   // the LDS affine table, before the first staging step reads it
@@ -842,7 +913,11 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        // SCI: shortcut chunk kc (its fragments landed with the wait above) before the next DMA is in flight, so a
+        // compiler-inserted wait for xa cannot hold up on chunk kc + 1's pieces; then its successor's loads
+        if (SCI && kc < n_sci) sci_mma(cur);
         if (kc + 1 < n_main) md_issue(kc + 1, nxt);
+        if (SCI && kc + 1 < n_sci) sci_load(kc + 1);
       }
       Frags fr[2];
       if constexpr (MI4) {
@@ -938,7 +1013,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
   };
   // ---- fused 1x1 shortcut chunks (centre tap) ----
   auto shortcut_phase = [&]() __attribute__((always_inline)) {
-    if constexpr (XTRA && SCR == 2) {
+    if constexpr (XTRA && (SCR == 2 || SCR == 3)) {
       // Per-wave LDS-DMA ring: each wave streams only its own 4 rows x 32 positions x 16 channels of the raw
       // fp32 block input (8 KiB = eight 1-KiB buffer_load ... lds pieces per chunk) into a private 2-slot ring
       // and the chunk's W1 image (hi + lo, 4 KiB = four pieces) into a private slot: 20 KiB per wave, the whole
@@ -948,6 +1023,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       // x image per slot: position p = 32 row + f holds 16 channels in 64 B, its 16-B quads permuted by
       // (f >> 2) & 3 (conflict-free ds_read_b128 groups).
       const int nx = a.x_chunks;
+      const int kb = n_sci;   // SCR 3: the chunks the main loop did not take (nx - kb even: host check)
       const char* w1 = reinterpret_cast<const char*>(wblk + (int64_t)n_main * W_BYTES);
       char* ring = smem + wm * kScrWave;
       char* wimg = ring + 2 * 8192;
@@ -983,11 +1059,12 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
       // Straight-line loop unrolled by the two slots; every step issues its refills (clamped to the last chunk
       // at the tail: harmless repeats), so the count of transfers behind a chunk's is the same on every path:
       // issue order x(k) W1(k) x(k+1) | W1(k+1) x(k+2) | ..., and chunk k is complete once only x(k+1)'s 8
-      // pieces remain.  nx is even (host check).
-      issue_x(0, 0);
-      issue_w(0);
-      issue_x(min(1, nx - 1), 1);
-      for (int kx0 = 0; kx0 < nx; kx0 += 2) {
+      // pieces remain.  nx - kb is even (host check).
+      if (kb < nx) {
+      issue_x(kb, 0);
+      issue_w(kb);
+      issue_x(min(kb + 1, nx - 1), 1);
+      for (int kx0 = kb; kx0 < nx; kx0 += 2) {
         Unroll<0, 2>::run([&](auto S) {
           constexpr int slot = decltype(S)::value;
           const int kx = kx0 + slot;
@@ -1027,6 +1104,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_db_kernel(ConvArgs a) {
         });
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // the tail's repeat refills landed
+      }
       __syncthreads();   // the epilogue's statistics reduction reuses the LDS
     } else if constexpr (XTRA && SCR == 1) {
       // Register-direct form: every lane loads its own A fragments straight from the raw fp32 block input
@@ -2965,6 +3043,15 @@ bool conv3x3_mdma_enabled() {
   return v;
 }
 
+// The fused 1x1 shortcut interleaved with the LDS-DMA main loop (conv3x3_db_kernel<SCR = 3>), opt-in SESA_CONV_SCI=1:
+// measured SLOWER than the ring after the main loop -- per level +0 (L1 enc) ... +37 % (L3 enc), the headline 270.5 ->
+// 266.8x same box (profiles/r05_u_*): the main loop does not leave the raw-input stream idle issue slots to hide in,
+// the shortcut's MFMAs, splits and loads simply add to it.
+bool conv3x3_sci_enabled() {
+  static const bool v = getenv("SESA_CONV_SCI") && std::string(getenv("SESA_CONV_SCI")) == "1";
+  return v;
+}
+
 bool tap_bn128_enabled() {
   static const bool v = !(getenv("SESA_TAP_BN128") && std::string(getenv("SESA_TAP_BN128")) == "0");
   return v;
@@ -3121,7 +3208,13 @@ int launch_conv(int kind, int bn, int x3, const ConvArgs& a, int batch, hipStrea
                             (int64_t)a.T_in * a.F_in * std::max(a.xin.src[0].C, a.xin.src[1].C) * 4 < (1ll << 31);
           // MDMA: the batch item's fp16 plane addressed with 32-bit offsets
           const bool mdma = conv3x3_mdma_enabled() && (int64_t)a.T_in * a.F_in * a.in.src[0].C * 2 < (1ll << 31);
-          if (ring && mdma)
+          // SCI: the shortcut chunks past the main loop's (a.x_chunks - a.n_chunks of them) go to the ring in pairs
+          const bool sci = ring && mdma && conv3x3_sci_enabled() &&
+                           (a.x_chunks - std::min(a.x_chunks, a.n_chunks)) % 2 == 0;
+          if (sci)
+            hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, 3, 2, false, 1>), g32, dim3(512), 0, st,
+                               a);
+          else if (ring && mdma)
             hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, 2, 2, false, 1>), g32, dim3(512), 0, st,
                                a);
           else if (ring)

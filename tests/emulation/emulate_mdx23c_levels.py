@@ -58,13 +58,16 @@ def make(per_conv, tdf=None):
 
     def conv2d(inp, w, *a, **k):
         # OTHER (env, comma list): also round these operands to fp16 -- down (2x2 s2 downscale), sc (fused 1x1
-        # shortcuts, every level), scw (the T >= 32 shortcuts' weights only), c33 (3x3 convs of the T < 32 levels)
+        # shortcuts, every level), scw (the T >= 32 shortcuts' weights only), sca (their
+        # activation only), c33 (3x3 convs of the T < 32 levels)
         if w.shape[-1] == 2 and "down" in OTHER:
             return F.conv2d(f16(inp), f16(w), *a, **k)
         if w.shape[-1] == 1 and w.shape[0] != w.shape[1] and "sc" in OTHER and inp.shape[1] > 4:
             return F.conv2d(f16(inp), f16(w), *a, **k)
         if w.shape[-1] == 1 and w.shape[0] != w.shape[1] and "scw" in OTHER and inp.shape[1] > 4 and inp.shape[2] >= 32:
             return F.conv2d(inp, f16(w), *a, **k)   # shortcut of the fp16 convs: fp16 weights x exact activation
+        if w.shape[-1] == 1 and w.shape[0] != w.shape[1] and "sca" in OTHER and inp.shape[1] > 4 and inp.shape[2] >= 32:
+            return F.conv2d(f16(inp), w_f16x2(w), *a, **k)   # fp16 activation x fp16 hi + lo weights
         if w.shape[-1] == 3 and inp.shape[2] < 32 and "c33" in OTHER:
             return F.conv2d(f16(inp), f16(w), *a, **k)
         if w.shape[-1] == 3 and inp.shape[2] >= 32:

@@ -91,6 +91,81 @@ int main(int argc, char** argv) {
   const bool only_wino = argc > 2 && strcmp(argv[2], "wino") == 0;  // ./tools/conv_bench 57 wino
   const bool only_f16 = argc > 2 && strcmp(argv[2], "f16") == 0;    // ./tools/conv_bench 57 f16
   const bool only_mdma = argc > 2 && strcmp(argv[2], "mdma") == 0;  // ./tools/conv_bench 57 mdma
+  const bool only_sci = argc > 2 && strcmp(argv[2], "sci") == 0;    // ./tools/conv_bench 57 sci
+  if (only_sci) {
+    // fp16 MI4 MDMA TFC conv with the fused shortcut: per-wave DMA ring after the main loop (SCR = 2, the default) vs
+    // interleaved with the main loop (SCR = 3); same operands, different fp32 summation order
+    for (int lvl = 0; lvl < 4; ++lvl)
+      for (int dec = 0; dec < 2; ++dec) {
+        const int C = 128 * (lvl + 1), Cx = dec ? 2 * C : C, T = 256 >> lvl, F = 1024 >> lvl;
+        const int64_t n_act = (int64_t)B * T * F * C, n_x = (int64_t)B * T * F * Cx;
+        float *x, *out, *out2;
+        uint16_t *hi, *w;
+        double* stats;
+        const int nblk = C / 64, nch = C / kConvBK, xch = Cx / kConvBK;
+        const int64_t w_elems = (int64_t)nblk * (nch * 9 * 64 * 32 + xch * 64 * 32);
+        CK(hipMalloc(&x, n_x * 4));
+        CK(hipMalloc(&hi, n_act * 2));
+        CK(hipMalloc(&w, w_elems * 2));
+        CK(hipMalloc(&out, n_act * 4));
+        CK(hipMalloc(&out2, n_act * 4));
+        CK(hipMalloc(&stats, (size_t)B * C * 2 * 8));
+        hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint16_t*>(x), n_x * 2, 4u, 1.f);
+        hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, hi, n_act, 1u, 1.f);
+        hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, w, w_elems, 3u, 0.03f);
+        CK(hipDeviceSynchronize());
+        ConvArgs a{};
+        a.in.src[0] = Src{nullptr, nullptr, nullptr, C, SRC_PRE, hi, nullptr};
+        a.in.src[1] = a.in.src[0];
+        a.in.C_split = a.in.C_in = C;
+        a.out.ptr = out;
+        a.out.stats = stats;
+        a.out.C_out = C;
+        a.w = w;
+        a.T_in = a.T_out = T;
+        a.F_in = a.F_out = F;
+        a.n_cols = C;
+        a.n_chunks = nch;
+        a.xin.src[0] = Src{x, nullptr, nullptr, Cx, SRC_RAW, nullptr, nullptr};
+        a.xin.src[1] = a.xin.src[0];
+        a.xin.C_split = a.xin.C_in = Cx;
+        a.x_chunks = xch;
+        const double flop_x = 2.0 * B * T * F * (double)C * C * 9 + 2.0 * B * T * F * (double)C * Cx;
+        const dim3 g32((unsigned)(((T + 31) / 32) * (F / kTF) * ((C + 63) / 64)), 1u, (unsigned)B);
+        auto rep = [&](const char* v, float ms, double fl) {
+          printf("L%d%s %-34s %9.3f %9.1f\n", lvl, dec ? "dec" : "enc", v, ms, fl / ms * 1e-9);
+        };
+        rep("ring shortcut (SCR 2)", time_ms([&] {
+              hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, 2, 2, false, 1>), g32, dim3(512), 0, 0, a);
+            }), flop_x);
+        rep("interleaved shortcut (SCR 3)", time_ms([&] {
+              hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, 3, 2, false, 1>), g32, dim3(512), 0, 0, a);
+            }), flop_x);
+        unsigned int* dm;
+        CK(hipMalloc(&dm, 8));
+        CK(hipMemset(dm, 0, 8));
+        ConvArgs q = a;
+        q.out.ptr = out2;
+        hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, 2, 2, false, 1>), g32, dim3(512), 0, 0, a);
+        hipLaunchKernelGGL((conv3x3_db_kernel<true, true, 0, false, 1, true, 3, 2, false, 1>), g32, dim3(512), 0, 0, q);
+        hipLaunchKernelGGL(max_diff, dim3(2048), dim3(256), 0, 0, out, out2, n_act, dm);
+        unsigned int hh[2];
+        CK(hipMemcpy(hh, dm, 8, hipMemcpyDeviceToHost));
+        float d, mm;
+        memcpy(&d, &hh[0], 4);
+        memcpy(&mm, &hh[1], 4);
+        printf("L%d%s SCR 3 vs SCR 2: max|diff| %.3e max|out| %.3e rel %.2e %s\n", lvl, dec ? "dec" : "enc", d, mm,
+               d / mm, d / mm < 1e-5f ? "OK" : "MISMATCH");
+        CK(hipFree(dm));
+        CK(hipFree(x));
+        CK(hipFree(hi));
+        CK(hipFree(w));
+        CK(hipFree(out));
+        CK(hipFree(out2));
+        CK(hipFree(stats));
+      }
+    return 0;
+  }
   if (only_mdma) {
     // fp16 MI4 TFC conv: register-staged main chunks vs LDS-DMA staged (MDMA), without and with the per-wave DMA ring
     // shortcut; outputs must be bit-identical (same operands, same MFMA order)
