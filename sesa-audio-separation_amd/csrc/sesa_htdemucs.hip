@@ -1816,6 +1816,246 @@ __global__ void __launch_bounds__(kT) htd_istft_fused_kernel(const float* __rest
   }
 }
 
+// Round 5: the same _mask + _ispec + overlap-add, one WAVE per signal and no workgroup barrier in the frame loop.
+// htd_istft_fused_kernel runs each 2048-point complex FFT with the whole workgroup (six barrier-separated radix-4 /
+// radix-2 stages, twiddles from global memory) and measured ~1 GB/s-class rates (iSTFT class 12 % of HBM).  Here a
+// workgroup owns one (item, segment) and kIwWaves of its signals, one wave per signal (an item's signals read the same
+// spectrum lines: its workgroups are adjacent in the grid), and each wave transforms its frames alone: 32 complex values per lane,
+// four Stockham stages (radix 8, 8, 8, 4; tools/istft_wave_fft_model.py is the index model, checked against numpy)
+// through the wave's private 16-KiB LDS buffer -- a wave's LDS operations complete in order, so no barrier -- with the
+// twiddles from one LDS table.  The last stage leaves lane L holding complex positions L + 64 u + 512 j (u < 8, j < 4),
+// a set closed under the hop (512 complex = 1024 samples), so the overlap-add ring lives in registers: R[j] is the
+// 1024-sample block tp + j; after frame tp block tp is complete and emitted as out = xt + acc / env (the OLA kernel's
+// formula), and the ring shifts by one block.  Four waves per workgroup and one workgroup per CU (84 KiB of LDS): each
+// wave may hold 512 registers -- its ring (64), the transform (64) and the next frame's bins in flight (64) -- where two
+// waves per SIMD (256 each) spilled.
+constexpr int kIwSeg = 32;
+constexpr int kIwWaves = 4;
+// float2 through two b32 buffer loads (merged into one buffer_load_dwordx2): this toolchain lowers
+// __builtin_amdgcn_raw_buffer_load_b64 to a single buffer_load_dword (the high dword is never loaded)
+__device__ __forceinline__ float2 buf_ld2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return make_float2(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0)),
+                     __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff + 4, soff, 0)));
+}   // signals (waves) per workgroup: nsrc * ach
+
+__device__ __forceinline__ void idft4(float2& a, float2& b, float2& c, float2& d) {   // inverse: e^{+2 pi i / 4} = i
+  const float2 apc = cadd(a, c), amc = csub(a, c), bpd = cadd(b, d), bmd = csub(b, d);
+  const float2 jbmd = make_float2(-bmd.y, bmd.x);
+  a = cadd(apc, bpd);
+  b = cadd(amc, jbmd);
+  c = csub(apc, bpd);
+  d = csub(amc, jbmd);
+}
+__device__ __forceinline__ void idft8(float2* x) {   // inverse 8-point DFT in place
+  float2 e0 = x[0], e1 = x[2], e2 = x[4], e3 = x[6], o0 = x[1], o1 = x[3], o2 = x[5], o3 = x[7];
+  idft4(e0, e1, e2, e3);
+  idft4(o0, o1, o2, o3);
+  const float h = 0.70710678118654752f;
+  o1 = make_float2(h * (o1.x - o1.y), h * (o1.x + o1.y));      // x e^{+2 pi i / 8}
+  o2 = make_float2(-o2.y, o2.x);                                // x e^{+2 pi i 2 / 8}
+  o3 = make_float2(-h * (o3.x + o3.y), h * (o3.x - o3.y));     // x e^{+2 pi i 3 / 8}
+  x[0] = cadd(e0, o0);
+  x[4] = csub(e0, o0);
+  x[1] = cadd(e1, o1);
+  x[5] = csub(e1, o1);
+  x[2] = cadd(e2, o2);
+  x[6] = csub(e2, o2);
+  x[3] = cadd(e3, o3);
+  x[7] = csub(e3, o3);
+}
+
+__global__ void __launch_bounds__(64 * kIwWaves, 1) htd_istft_wave_kernel(
+    const float* __restrict__ Z, int T, int Cz, int ach, int nsrc, int nseg, const double* __restrict__ stats,
+    int64_t n_item, const float* __restrict__ win, Fft2048Tables tb, int L, const float* __restrict__ XT,
+    const double* __restrict__ tstats, float* __restrict__ out) {
+  __shared__ float2 wbuf[kIwWaves][kFft2048];    // per-wave exchange buffers (64 KiB)
+  __shared__ float2 twl[kFft2048 + 1];           // exp(-2 pi i k / 4096), k <= 2048
+  __shared__ float envI[kHop];                   // window envelope of an interior sample, by n mod hop
+  const int nper = nsrc * ach;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wpi = (nper + kIwWaves - 1) / kIwWaves;   // workgroups per (item, segment)
+  const int g = blockIdx.x / wpi, part = blockIdx.x - g * wpi;
+  const int b = g / nseg, seg = g - b * nseg;
+  for (int i = threadIdx.x; i <= kFft2048; i += blockDim.x) twl[i] = tb.twN[i];
+  for (int m = threadIdx.x; m < kHop; m += blockDim.x) {
+    // the OLA kernel's envelope loop for n with all four frames present: tq ascending = window offset descending
+    float env = 0.f;
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+      const float w = win[m + q * kHop];
+      env = fmaf(w, w, env);
+    }
+    envI[m] = env;
+  }
+  __syncthreads();   // the only workgroup barrier
+  const int j = part * kIwWaves + wv;   // this wave's signal
+  if (j >= nper) return;
+  const int n0 = kPadSpec + kCenter, n1 = n0 + L;   // output samples i = n - n0
+  const int tpa = n0 / kHop + seg * kIwSeg, tpb = min((n1 - 1) / kHop + 1, tpa + kIwSeg);
+  if (tpa >= tpb) return;
+  const int sig = b * nper + j, s = j / ach, c = j - s * ach;
+  const int ch = s * 2 * ach + 2 * c;
+  float mean, sd, mt, st;
+  mean_std(stats + 2 * b, n_item, mean, sd);
+  mean_std(tstats + 2 * b, (int64_t)ach * L, mt, st);
+  const float sc = 2.0f / 64.0f;
+  float2* B = wbuf[wv];
+  // conj(exp(-2 pi i e / 2048)) for e in [0, 2048) from the 4096-point table: tw[e] = twN[2 e] (e < 1024), -twN[2 e - 2048]
+  auto twi = [&](int e) -> float2 {
+    const float2 v = twl[2 * (e & 1023)];
+    return (e & 1024) ? make_float2(-v.x, v.y) : make_float2(v.x, -v.y);
+  };
+  auto twmul = [&](float2* x, int e) {   // x[q] *= W^(q e), W = exp(+2 pi i / 2048), q = 1..7
+    const float2 w1 = twi(e & 2047);
+    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
+    const float2 w5 = cmul(w4, w1), w6 = cmul(w4, w2), w7 = cmul(w4, w3);
+    x[1] = cmul(x[1], w1);
+    x[2] = cmul(x[2], w2);
+    x[3] = cmul(x[3], w3);
+    x[4] = cmul(x[4], w4);
+    x[5] = cmul(x[5], w5);
+    x[6] = cmul(x[6], w6);
+    x[7] = cmul(x[7], w7);
+  };
+  // spectrum bins X[k], k = lane + 64 u + 256 r, of frame tc: stage 1's butterfly inputs.  Buffer loads over the
+  // item's [kF0][T][Cz] plane: one per-lane offset, the (u, r) part in the scalar offset (64-bit addresses per load
+  // would take 64 VGPRs across the frame loop)
+  const int rowb = T * Cz * 4;   // bytes per bin row (host check: the plane < 2^31 bytes)
+  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)const_cast<float*>(Z + (int64_t)b * kF0 * T * Cz), (short)0, kF0 * rowb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rwin =
+      __builtin_amdgcn_make_buffer_rsrc((void*)const_cast<float*>(win), (short)0, kFft4096 * 4, 0x00020000);
+  float2 xs[4][8];
+  auto load_frame = [&](int tc) {
+    const int vo = lane * rowb + (tc * Cz + ch) * 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float2 v = buf_ld2(rz, vo, (64 * u + 256 * r) * rowb);
+        const bool dc = lane == 0 && u == 0 && r == 0;
+        xs[u][r] = make_float2(v.x * sd + mean, dc ? 0.f : v.y * sd + mean);   // C2R ignores DC's imaginary part
+      }
+  };
+  auto real = [&](int tp) { return tp - 2 >= 0 && tp - 2 < T; };
+  float2 R[4][8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) R[q][u] = make_float2(0.f, 0.f);
+  {
+    int tp = tpa - 3;
+    while (tp < tpb && !real(tp)) ++tp;
+    if (tp < tpb) load_frame(tp - 2);
+  }
+  for (int tp = tpa - 3; tp < tpb; ++tp) {
+    if (real(tp)) {   // (wave-uniform)
+      float2 d[4][8];
+      // pack (irfft_pack): X[2048 - k] from the wave's buffer; k = 0 pairs with the zeroed Nyquist bin
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) B[lane + 64 * u + 256 * r] = xs[u][r];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int k = lane + 64 * u + 256 * r;
+          const float2 xk = xs[u][r];
+          const float2 xm = k ? cconj(B[kFft2048 - k]) : make_float2(0.f, 0.f);
+          const float2 E = make_float2(0.5f * (xk.x + xm.x), 0.5f * (xk.y + xm.y));
+          const float2 D = csub(xk, xm);
+          const float2 O = cmul(make_float2(0.5f * D.x, 0.5f * D.y), cconj(twl[k]));
+          d[u][r] = make_float2(E.x - O.y, E.y + O.x);
+        }
+      // the next real frame's bins fly under this frame's transform
+      if (tp + 1 < tpb && real(tp + 1)) load_frame(tp - 1);
+      // stage 1 (s = 1): butterfly p = lane + 64 u reads A[p + 256 r] (in registers), writes y[8 p + q]
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = lane + 64 * u;
+        idft8(d[u]);
+        twmul(d[u], p);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) B[8 * p + q] = d[u][q];
+      }
+      // stage 2 (s = 8): bf = lane + 64 u, q0 = bf % 8, p = bf / 8; reads x[bf + 256 r], writes y[q0 + 64 p + 8 q]
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) d[u][r] = B[lane + 64 * u + 256 * r];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int bf = lane + 64 * u, q0 = bf & 7, p = bf >> 3;
+        idft8(d[u]);
+        twmul(d[u], 8 * p);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) B[q0 + 64 * p + 8 * q] = d[u][q];
+      }
+      // stage 3 (s = 64): q0 = lane, p = u; reads x[lane + 64 u + 256 r], writes y[lane + 64 (8 u + q)]
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) d[u][r] = B[lane + 64 * u + 256 * r];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        idft8(d[u]);
+        twmul(d[u], 64 * u);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) B[lane + 64 * (8 * u + q)] = d[u][q];
+      }
+      // stage 4 (radix 4, s = 512): position k = lane + 64 u + 512 q, windowed into ring block q
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float2 e0 = B[lane + 64 * u], e1 = B[lane + 64 * u + 512], e2 = B[lane + 64 * u + 1024],
+               e3 = B[lane + 64 * u + 1536];
+        idft4(e0, e1, e2, e3);
+        const float2 zq[4] = {e0, e1, e2, e3};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float2 w = buf_ld2(rwin, lane * 8, (64 * u + 512 * q) * 8);
+          R[q][u].x += zq[q].x * sc * w.x;
+          R[q][u].y += zq[q].y * sc * w.y;
+        }
+      }
+    }
+    // samples [tp hop, tp hop + hop) are complete: ring block 0
+    if (tp >= tpa) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int nb = tp * kHop + 2 * (lane + 64 * u);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int n = nb + e;
+          if (n >= n0 && n < n1) {
+            float env;
+            const int th = n / kHop;
+            if (th <= T + 3) {
+              env = envI[n & (kHop - 1)];
+            } else {   // frames past the padded spectrogram's last: the OLA kernel's loop
+              env = 0.f;
+              for (int tq = th - 3; tq <= T + 3; ++tq) {
+                const float w = win[n - tq * kHop];
+                env = fmaf(w, w, env);
+              }
+            }
+            const int i = n - n0;
+            const float xt = XT[((int64_t)b * L + i) * nper + j] * st + mt;
+            out[(int64_t)sig * L + i] = xt + (e ? R[0][u].y : R[0][u].x) / env;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      R[0][u] = R[1][u];
+      R[1][u] = R[2][u];
+      R[2][u] = R[3][u];
+      R[3][u] = make_float2(0.f, 0.f);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 struct Param {
   std::string name;
@@ -3211,7 +3451,25 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     // frames + overlap-add in one kernel (iSTFT class 70.2 -> 61.3 ms per step same box, profiles/r05_s_bench_htd_*.json;
     // no 4096-sample frame buffer in HBM); SESA_HTD_ISTFT_FUSED=0: the two-kernel form (A/B)
     static const bool fused = !(getenv("SESA_HTD_ISTFT_FUSED") && std::string(getenv("SESA_HTD_ISTFT_FUSED")) == "0");
-    if (fused) {
+    // one wave per signal, no barrier in the frame loop (htd_istft_wave_kernel), opt-in SESA_HTD_ISTFT_WAVE=1: measured
+    // slower -- iSTFT class 61.5 -> 77.5 ms per step, configs[3] 1250 -> 1240x (profiles/r05_v_*), parity 5.87e-6.  A
+    // wave gathers its frame's 2048 bins from 2048 different lines of the [b][k][t][Cz] spectrum (one 8-B value each)
+    // with one wave per SIMD to cover the latency; the fused kernel's XCD grouping lets 16 (signal, frame) consumers
+    // share each line in L2 instead.
+    static const bool wave = getenv("SESA_HTD_ISTFT_WAVE") && std::string(getenv("SESA_HTD_ISTFT_WAVE")) == "1";
+    const int nper_w = m->nsrc * ach;
+    if (fused && wave) {
+      const int tp_n = (kPadSpec + kCenter + L - 1) / kHop - (kPadSpec + kCenter) / kHop + 1;
+      const int nseg = (tp_n + kIwSeg - 1) / kIwSeg;
+      const int64_t groups = (int64_t)B * nseg * ((nper_w + kIwWaves - 1) / kIwWaves);
+      SESA_REQUIRE(groups < (1ll << 31) && (int64_t)kF0 * T * m->fq[0].Cdec * 4 < (1ll << 31), SESA_ERR_INVALID,
+                   "htdemucs forward: iSTFT grid / spectrum plane too large");
+      hipLaunchKernelGGL(htd_istft_wave_kernel, dim3((unsigned)groups), dim3(64 * kIwWaves), 0, st, cur_f, T,
+                         m->fq[0].Cdec, ach, m->nsrc, nseg, st_f, (int64_t)kF0 * T * 2 * ach, win, tb, L, cur_t, st_t,
+                         out);
+      SESA_CHECK_LAUNCH();
+      profile_end(tok, st, SESA_KCLASS_ISTFT, 4.0 * nsig * ((double)T * kF0 * 2 + 2.0 * L));
+    } else if (fused) {
       const int nper = m->nsrc * ach;
       const int tp_n = (kPadSpec + kCenter + L - 1) / kHop - (kPadSpec + kCenter) / kHop + 1;
       const int nseg = (tp_n + kIstSeg - 1) / kIstSeg;

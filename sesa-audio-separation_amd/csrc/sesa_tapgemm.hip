@@ -2556,10 +2556,14 @@ __global__ void __launch_bounds__(512) tdf_u_split_kernel(TdfArgs a) {
 //     last chunk) are written as full 128-B lines; per-column statistics (fp32 over 16-value runs, fp64
 //     beyond) reduced through LDS.
 // F16 (X3 = false): W and B images in fp16, one v_mfma_f32_32x32x16_f16 pass (SESA_PREC_F16MIX TDF plan).
-template <bool X3, bool U_IN, bool U_OUT, int BM, bool PRE = false, bool F16 = false>
+// DEEP (F16 only; round 5): the fp16 images free LDS for deeper rings -- W two chunks ahead (3 stages), X five ahead
+// (6 stages, 96 KiB of the input in flight per CU instead of 48) -- and the PRE input DMAs only the fp16 image of each
+// 16-KiB block (tdf_u_split_kernel<F16> writes no lo image: the plain ring fetched 8 KiB of unwritten bytes per chunk).
+template <bool X3, bool U_IN, bool U_OUT, int BM, bool PRE = false, bool F16 = false, bool DEEP = false>
 __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   static_assert(!PRE || U_IN, "pre-split B images exist for the tiled U input only");
   static_assert(!F16 || !X3, "fp16: one pass");
+  static_assert(!DEEP || F16, "deep rings: the fp16 images");
   constexpr int BN = 128;
   constexpr int WM = BM / 64, WN = 8 / WM;
   constexpr int MI = 2, NI = BN / WN / 32;
@@ -2569,16 +2573,21 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   constexpr int W_STAGE = (X3 ? 2 : 1) * W_PLANE;
   constexpr int X_STAGE = kTdfBK * BN * 4;         // 16 KiB fp32
   constexpr int B_PLANE = BN * ROWB;                // 8 KiB
-  constexpr int NWS = 2, NXS = 4;                   // W ring (one chunk ahead), X ring (three ahead)
+  constexpr int NWS = DEEP ? 3 : 2, NXS = DEEP ? 6 : 4;   // W ring (one / two chunks ahead), X ring (three / five)
   constexpr int W_OFF = 0, X_OFF = NWS * W_STAGE, B_OFF = X_OFF + NXS * X_STAGE;
   constexpr int B_IMG = (X3 ? 2 : 1) * B_PLANE;      // two B images: chunk kc's MFMAs / chunk kc+1's conversion
   constexpr int SMEM = B_OFF + 2 * B_IMG;
   static_assert(SMEM <= 163840 && WM * BN * 2 * 8 <= SMEM, "LDS budget");
-  constexpr int W_PC = W_STAGE / 1024, X_PC = X_STAGE / 1024;
+  constexpr int X_DMA = DEEP && PRE ? X_STAGE / 2 : X_STAGE;   // bytes DMA'd per X chunk
+  constexpr int W_PC = W_STAGE / 1024, X_PC = X_DMA / 1024;
   static_assert(W_PC % 8 == 0 && X_PC % 8 == 0, "uniform DMA pieces per wave");
   // s_waitcnt: all but the X_PC / 8 youngest vector-memory ops (the X DMA issued last), lgkmcnt(0)
-  constexpr int VMN = X_PC / 8;
+  constexpr int VMN = X_PC / 8, WPW = W_PC / 8;
   constexpr int WAIT_ONE = (VMN & 15) | ((VMN >> 4) << 14) | (7 << 4);
+  // DEEP: vmcnt(n) (expcnt not waited, lgkmcnt(0))
+  constexpr int WAIT_D2 = ((2 * VMN + WPW) & 15) | (((2 * VMN + WPW) >> 4) << 14) | (7 << 4);
+  constexpr int WAIT_D1 = ((VMN + WPW) & 15) | (((VMN + WPW) >> 4) << 14) | (7 << 4);
+  constexpr int WAIT_D0 = (WPW & 15) | ((WPW >> 4) << 14) | (7 << 4);
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x;
@@ -2718,8 +2727,9 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
     }
   };
 
-  // prologue: W(0), X(0..2) landed; chunk 0 converted
+  // prologue: W(0) (DEEP: and W(1)), X(0 .. NXS - 2) landed; chunk 0 converted
   issue_w(0);
+  if (DEEP && nk > 1) issue_w(1);
 #pragma unroll
   for (int d = 0; d < NXS - 1; ++d)
     if (d < nk) issue_x(d);
@@ -2735,7 +2745,11 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
   // (iteration kc - 1's MFMAs, iteration kc - 2's conversion) are behind a barrier; one barrier per chunk
   for (int kc = 0; kc < nk; ++kc) {
     const bool more_w = kc + 1 < nk, more_x = kc + NXS - 1 < nk;
-    if (more_w) issue_w(kc + 1);
+    if (DEEP) {
+      if (kc + 2 < nk) issue_w(kc + 2);
+    } else if (more_w) {
+      issue_w(kc + 1);
+    }
     if (more_x) issue_x(kc + NXS - 1);
     if (!U_OUT && kc + 1 == nk) load_res();
     const char* W = smem + W_OFF + (kc % NWS) * W_STAGE;
@@ -2772,8 +2786,15 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
         }
     }
     // W(kc + 1) and X(kc + 2) landed (only X(kc + 3), issued last, may stay in flight; the residual
-    // prefetch of the last iteration is waited for at its use)
-    if (more_x) __builtin_amdgcn_s_waitcnt(WAIT_ONE);
+    // prefetch of the last iteration is waited for at its use).  DEEP: the ops younger than W(kc + 1) -- X(kc + 4),
+    // W(kc + 2), X(kc + 5), as far as they were issued -- may stay in flight
+    if (DEEP) {
+      if (kc + 5 < nk) __builtin_amdgcn_s_waitcnt(WAIT_D2);
+      else if (kc + 4 < nk) __builtin_amdgcn_s_waitcnt(WAIT_D1);
+      else if (kc + 2 < nk) __builtin_amdgcn_s_waitcnt(WAIT_D0);
+      else if (more_w) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else if (more_x) __builtin_amdgcn_s_waitcnt(WAIT_ONE);
     else if (more_w) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     asm volatile("" ::: "memory");
@@ -3341,6 +3362,14 @@ int tdf_variant() {  // SESA_TDF_VARIANT=old: the round-1 register-staged tdf_ke
 }
 }  // namespace
 
+// The fp16 TDF Linears on the deep rings (tdf_dma_kernel<..., DEEP>): the pre-split second Linear 3.61 -> 3.21 ms at
+// level 0, the tdf class 142 -> 138 ms per step, configs[1] 270.5 -> 272.6x same box, bit-identical output
+// (profiles/r05_w_*).  SESA_TDF_DEEP=0: the round-4 rings (A/B).
+bool tdf_deep_enabled() {
+  static const bool v = !(getenv("SESA_TDF_DEEP") && std::string(getenv("SESA_TDF_DEEP")) == "0");
+  return v;
+}
+
 // the LDS-DMA TDF kernel takes this Linear (and so may run it in fp16, x3 == 2; the host packs those
 // weights as fp16 images): C % 128 == 0, K % 32 == 0, 128 or 256 row blocks, one normalised / raw source
 bool tdf_dma_eligible(int C, int K, int M) {
@@ -3364,9 +3393,11 @@ int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transpos
       const int64_t grid = (n_tiles + 7) / 8 * 8 * ((a.M + bm - 1) / bm);
       SESA_REQUIRE(grid < (1ll << 31), SESA_ERR_INVALID, "tdf: grid too large");
       const dim3 g((unsigned)grid), blk(512);
+      const bool deep = tdf_deep_enabled();
 #define SESA_TDF_DMA(UI, UO, BMV)                                                                     \
   do {                                                                                                \
-    if (x3 == 2) hipLaunchKernelGGL((tdf_dma_kernel<false, UI, UO, BMV, false, true>), g, blk, 0, st, b); \
+    if (x3 == 2 && deep) hipLaunchKernelGGL((tdf_dma_kernel<false, UI, UO, BMV, false, true, true>), g, blk, 0, st, b); \
+    else if (x3 == 2) hipLaunchKernelGGL((tdf_dma_kernel<false, UI, UO, BMV, false, true>), g, blk, 0, st, b); \
     else if (x3) hipLaunchKernelGGL((tdf_dma_kernel<true, UI, UO, BMV>), g, blk, 0, st, b);            \
     else hipLaunchKernelGGL((tdf_dma_kernel<false, UI, UO, BMV>), g, blk, 0, st, b);                  \
   } while (0)
@@ -3383,7 +3414,8 @@ int launch_tdf(int x3, const TdfArgs& a, int batch, hipStream_t st, int transpos
         SESA_CHECK_LAUNCH();
 #define SESA_TDF_PRE(BMV)                                                                               \
   do {                                                                                                  \
-    if (x3 == 2) hipLaunchKernelGGL((tdf_dma_kernel<false, true, false, BMV, true, true>), g, blk, 0, st, b); \
+    if (x3 == 2 && deep) hipLaunchKernelGGL((tdf_dma_kernel<false, true, false, BMV, true, true, true>), g, blk, 0, st, b); \
+    else if (x3 == 2) hipLaunchKernelGGL((tdf_dma_kernel<false, true, false, BMV, true, true>), g, blk, 0, st, b); \
     else if (x3) hipLaunchKernelGGL((tdf_dma_kernel<true, true, false, BMV, true>), g, blk, 0, st, b);        \
     else hipLaunchKernelGGL((tdf_dma_kernel<false, true, false, BMV, true>), g, blk, 0, st, b);              \
   } while (0)
