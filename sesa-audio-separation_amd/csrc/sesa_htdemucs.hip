@@ -1169,6 +1169,10 @@ struct RwArgs {
   const float* bias;   // [2C]: a then gate (the Conv bias as stored)
   float* out;          // [B][F][T][C]
   int B, F, T, C;
+  // (nullable) a [tab_F][C] table added to the output row of flattened position p: row (p / tab_T) % tab_F -- the
+  // frequency embedding after the first frequency encoder (demucs4ht.py:606-611), fused into the store
+  const float* rowtab = nullptr;
+  int tab_T = 1, tab_F = 1;
 };
 constexpr int kRwCols = 96;
 constexpr int kRwOS = 52;   // epilogue LDS tile row stride (floats)
@@ -1361,9 +1365,13 @@ __global__ void __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) htd_rw3_kernel(RwA
     const int e = tid + NT * i, pl = e / 12, q = e - 12 * pl;
     if (pl >= 64 * NWV) continue;
     const int wv = pl >> 6, f = f0 + wv / WPR, t = t0 + 64 * (wv % WPR) + (pl & 63);
-    if (f < a.F && t < a.T)
-      *reinterpret_cast<f32x4*>(a.out + (((int64_t)b * a.F + f) * a.T + t) * C + cg * 48 + 4 * q) =
-          *reinterpret_cast<const f32x4*>(os + pl * kRwOS + 4 * q);
+    if (f < a.F && t < a.T) {
+      const int64_t pos = ((int64_t)b * a.F + f) * a.T + t;
+      f32x4 v = *reinterpret_cast<const f32x4*>(os + pl * kRwOS + 4 * q);
+      if (a.rowtab)
+        v += *reinterpret_cast<const f32x4*>(a.rowtab + (((int)pos / a.tab_T) % a.tab_F) * C + cg * 48 + 4 * q);
+      *reinterpret_cast<f32x4*>(a.out + pos * C + cg * 48 + 4 * q) = v;
+    }
   }
 }
 
@@ -2898,16 +2906,19 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   static const bool rw_conv = getenv("SESA_HTD_REWRITE_CONV") && std::string(getenv("SESA_HTD_REWRITE_CONV")) == "1";
   // the halo-tile rewrite kernel (fp16mix images present; SESA_HTD_RW3=0: tok_gemm_kernel<conv> for A/B).  Returns
   // false when it does not apply, and the caller runs the implicit GEMM.
-  auto rw3 = [&](const Branch& br, const float* x, const float* skip, float* o, int F, int Tn, int taps) -> bool {
+  auto rw3 = [&](const Branch& br, const float* x, const float* skip, float* o, int F, int Tn, int taps,
+                 const float* rowtab = nullptr, int tab_T = 1, int tab_F = 1) -> bool {
     static const bool on = !(getenv("SESA_HTD_RW3") && std::string(getenv("SESA_HTD_RW3")) == "0");
     const int64_t img = taps == 1 ? br.erw_img : br.rw_img, boff = taps == 1 ? br.erw_bias : br.rw_bias;
     if (!on || img < 0 || rc) return false;
     const int Bk = taps == 1 ? 1 : B;
-    RwArgs ra{x, skip, m->d_w + img, Wb + boff, o, Bk, F, Tn, br.Cout};
+    RwArgs ra{x, skip, m->d_w + img, Wb + boff, o, Bk, F, Tn, br.Cout, rowtab, tab_T, tab_F};
     // SESA_HTD_RW_NW=8: 512-thread workgroups (8 rows x 64 / 512 positions; one per CU) instead of 256 (two per CU)
     static const int nw = getenv("SESA_HTD_RW_NW") && atoi(getenv("SESA_HTD_RW_NW")) == 8 ? 8 : 4;
     // SESA_HTD_RW_PERS=1: persistent workgroups with the next tile's first chunk prefetched (A/B)
     static const bool pers = getenv("SESA_HTD_RW_PERS") && std::string(getenv("SESA_HTD_RW_PERS")) == "1";
+    // (the persistent epilogue has no table add; the table row comes from a 32-bit position)
+    if (rowtab && (pers || (int64_t)Bk * F * Tn >= (1ll << 31))) return false;
     const int FR = taps == 9 ? nw : 1, TT = 64 * nw / FR;   // (taps 1: B = F = 1, Tn = all positions)
     const dim3 g((unsigned)((int64_t)Bk * ((F + FR - 1) / FR) * ((Tn + TT - 1) / TT)), (unsigned)(br.Cout / 48));
     void* t0 = profile_begin(st);
@@ -3145,9 +3156,14 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
               0, 0);
     if (c.dconv_mode & 1) dconv(f.edc, E, B * f.Fout, T, f.Cout, f.h);
     float* skf = F32(pl.sf[i]);
-    if (!rw3(f, E, nullptr, skf, 1, (int)((int64_t)B * f.Fout * T), 1))
+    // the frequency embedding (i == 0) rides in the rewrite's store when the halo-tile kernel runs it
+    const bool emb = i == 0 && c.freq_emb != 0.0;
+    bool emb_done = false;
+    if (rw3(f, E, nullptr, skf, 1, (int)((int64_t)B * f.Fout * T), 1, emb ? Wb + m->emb_tab : nullptr, T, f.Fout))
+      emb_done = emb;
+    else
       rewrite_glu(f.rewrite, E, skf, (int64_t)B * f.Fout * T, f.Cout);
-    if (i == 0 && c.freq_emb != 0.0 && !rc) {
+    if (emb && !emb_done && !rc) {
       const int64_t n = (int64_t)B * f.Fout * T * f.Cout;
       SESA_REQUIRE(f.Cout % 4 == 0 && (int64_t)T * f.Cout < (1ll << 31) && f.Fout < 65536 && B < 65536,
                    SESA_ERR_INVALID, "htdemucs: frequency embedding rows");
