@@ -4,8 +4,11 @@
 #   dominant classes + the streaming classes, one bench line per BASELINE config (+ rank-share rehearsals), rocprofv3
 #   kernel stats.  Every GPU step has its own time limit; the script stops at the first crash or time limit.
 #   PART=t|p|b|c splits it over calls (t: GPU tests + smoke, p: PMC passes, b: bench lines, c: rocprof).
+#   Second pass (final5b) after the round's last source changes: the PMC step re-measures only the classes whose
+#   sha stamps the changes invalidated (MDX23C conv3x3 / tdf / act, HTDemucs hconv / simt / attn, the ensemble's
+#   conv3x3); the BS-Roformer, SCNet and streaming-class summaries still match the tree.
 set -e
-O=gpurun_out/final5
+O=gpurun_out/final5b
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 step() { echo "[final] $(date +%T) $*"; }
@@ -23,8 +26,6 @@ step pmc mdx23c
 timeout -k 10 700 bash tools/pmc_refresh.sh mdx23c \
   "conv3x3=conv3x3_db_kernel<true, true, 0, false, 1, true|conv3x3_db_kernel<true, false, 0, false, 1, true" \
   "tdf=tdf_dma_kernel|tdf_kernel|tdf_u_split" "act=act_split_kernel|act_f16" > $O/pmc_mdx23c.log 2>&1
-timeout -k 10 120 python3 tools/pmc_stream.py gpurun_out/pmc_mdx23c_f gpurun_out/pmc_mdx23c_w mdx23c \
-  "$(python3 -c 'import bench; print(bench.default_precision("mdx23c"))')" gpurun_out > $O/pmc_stream.log 2>&1
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step pmc htdemucs
 timeout -k 10 700 bash tools/pmc_refresh.sh htdemucs \
@@ -32,15 +33,8 @@ timeout -k 10 700 bash tools/pmc_refresh.sh htdemucs \
   "simt=htd_dc_|htd_item_stats|htd_gn_apply|htd_norm_freq|htd_norm_time" \
   "attn=attn_kernel|attn_f16_kernel" > $O/pmc_htdemucs.log 2>&1
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
-step pmc bs_roformer
-timeout -k 10 700 bash tools/pmc_refresh.sh bs_roformer "tokgemm=tok_gemm" > $O/pmc_bsr.log 2>&1
-rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
-step pmc scnet
-timeout -k 10 700 bash tools/pmc_refresh.sh scnet "lstm=scn_lstm_mfma" \
-  "simt=scn_cm_in|scn_cm_out|scn_sdconv|scn_convtr|scn_gelu_rows|scn_conv3x3" "dft=scn_dft_mfma" > $O/pmc_scnet.log 2>&1
-rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 step pmc ensemble
-timeout -k 10 900 bash tools/pmc_refresh.sh ensemble "conv3x3=conv3x3_db_kernel|tap_gemm_kernel<3, 3" "tokgemm=tok_gemm" > $O/pmc_ensemble.log 2>&1
+timeout -k 10 900 bash tools/pmc_refresh.sh ensemble "conv3x3=conv3x3_db_kernel|tap_gemm_kernel<3, 3" > $O/pmc_ensemble.log 2>&1
 rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
 mkdir -p $O/pmc
 cp gpurun_out/pmc_*.json $O/pmc/ 2>/dev/null || true
@@ -69,13 +63,13 @@ timeout -k 10 900 python bench.py --model ensemble --steps 2 --warmup 1 > $O/ben
 fi
 if [[ $PART == *c* ]]; then
 step rocprof mdx23c
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_mdx23c -o run -- python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-parity > $O/prof_mdx23c.json 2> $O/prof_mdx23c.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_mdx23c -o run -- python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-parity --no-pcie > $O/prof_mdx23c.json 2> $O/prof_mdx23c.err
 step rocprof htdemucs
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_htdemucs -o run -- python3 bench.py --model htdemucs --steps 1 --warmup 1 --no-cpu-baseline --no-parity > $O/prof_htdemucs.json 2> $O/prof_htdemucs.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_htdemucs -o run -- python3 bench.py --model htdemucs --steps 1 --warmup 1 --no-cpu-baseline --no-parity --no-pcie > $O/prof_htdemucs.json 2> $O/prof_htdemucs.err
 step rocprof bs_roformer
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_bsr -o run -- python3 bench.py --model bs_roformer --steps 1 --warmup 1 --no-cpu-baseline --no-parity > $O/prof_bsr.json 2> $O/prof_bsr.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_bsr -o run -- python3 bench.py --model bs_roformer --steps 1 --warmup 1 --no-cpu-baseline --no-parity --no-pcie > $O/prof_bsr.json 2> $O/prof_bsr.err
 step rocprof scnet
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_scnet -o run -- python3 bench.py --model scnet --steps 1 --warmup 1 --no-cpu-baseline --no-parity > $O/prof_scnet.json 2> $O/prof_scnet.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_scnet -o run -- python3 bench.py --model scnet --steps 1 --warmup 1 --no-cpu-baseline --no-parity --no-pcie > $O/prof_scnet.json 2> $O/prof_scnet.err
 step summarize
 for r in mdx23c htdemucs bsr scnet; do
   python3 tools/rocprof_summary.py $O/prof_$r $O/kernel_stats_$r.txt > /dev/null
