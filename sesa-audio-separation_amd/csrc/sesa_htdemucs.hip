@@ -1386,8 +1386,9 @@ struct CtrArgs {
   const float* x;      // [B][Q][T][Cin] (time branch: T = 1)
   const uint16_t* w;   // [ceil(N / 96)][Cin / 16][2][96][16] fp16, pre-swizzled
   const float* bias;   // [Cdec]
-  float* out;          // [B][O1][T][Cdec]
+  float* out;          // [B][O1][T][Cdec], or (fmajor) [B][T][O1][Cdec]
   int B, Q, T, Cin, Cdec, S, O1, opad, act;
+  int fmajor = 0;      // frame-major output: the spectrum the one-wave iSTFT reads (one frame's bins contiguous)
 };
 template <bool TWO_D>
 __global__ void __launch_bounds__(256, 2) htd_ctr_kernel(CtrArgs a) {
@@ -1504,7 +1505,8 @@ __global__ void __launch_bounds__(256, 2) htd_ctr_kernel(CtrArgs a) {
         if (q >= nq || t >= a.T || f < 0 || f >= a.O1) continue;
         float v = acc[i][j][rr] + bv;
         if (a.act) v = gelu_erf(v);
-        a.out[(((int64_t)b * a.O1 + f) * a.T + t) * a.Cdec + co] = v;
+        const int64_t orow = a.fmajor ? ((int64_t)b * a.T + t) * a.O1 + f : ((int64_t)b * a.O1 + f) * a.T + t;
+        a.out[orow * a.Cdec + co] = v;
       }
   }
 }
@@ -1925,22 +1927,24 @@ __global__ void __launch_bounds__(64 * kIwWaves, 1) htd_istft_wave_kernel(
     x[6] = cmul(x[6], w6);
     x[7] = cmul(x[7], w7);
   };
-  // spectrum bins X[k], k = lane + 64 u + 256 r, of frame tc: stage 1's butterfly inputs.  Buffer loads over the
-  // item's [kF0][T][Cz] plane: one per-lane offset, the (u, r) part in the scalar offset (64-bit addresses per load
-  // would take 64 VGPRs across the frame loop)
-  const int rowb = T * Cz * 4;   // bytes per bin row (host check: the plane < 2^31 bytes)
+  // spectrum bins X[k], k = lane + 64 u + 256 r, of frame tc: stage 1's butterfly inputs.  The spectrum is
+  // frame-major, [B][T][kF0][Cz] (the last decoder layer's htd_ctr_kernel<fmajor>): one frame's bins are contiguous,
+  // 64 B apart, so a wave's load touches 32 lines and the workgroup's four signals share them in L1.  Buffer loads
+  // over the item's plane: one per-lane offset, the (u, r) part in the scalar offset (64-bit addresses per load would
+  // take 64 VGPRs across the frame loop)
+  const int binb = Cz * 4;   // bytes per bin (host check: the item's plane < 2^31 bytes)
   const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)const_cast<float*>(Z + (int64_t)b * kF0 * T * Cz), (short)0, kF0 * rowb, 0x00020000);
+      (void*)const_cast<float*>(Z + (int64_t)b * T * kF0 * Cz), (short)0, T * kF0 * binb, 0x00020000);
   const __amdgpu_buffer_rsrc_t rwin =
       __builtin_amdgcn_make_buffer_rsrc((void*)const_cast<float*>(win), (short)0, kFft4096 * 4, 0x00020000);
   float2 xs[4][8];
   auto load_frame = [&](int tc) {
-    const int vo = lane * rowb + (tc * Cz + ch) * 4;
+    const int vo = (tc * kF0 + lane) * binb + ch * 4;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        const float2 v = buf_ld2(rz, vo, (64 * u + 256 * r) * rowb);
+        const float2 v = buf_ld2(rz, vo, (64 * u + 256 * r) * binb);
         const bool dc = lane == 0 && u == 0 && r == 0;
         xs[u][r] = make_float2(v.x * sd + mean, dc ? 0.f : v.y * sd + mean);   // C2R ignores DC's imaginary part
       }
@@ -3398,11 +3402,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
 
   // ---- 4. decoders (:636-654): x + skip -> rewrite (3x3 / k3) + GLU -> DConv -> conv_tr -> trim -> GELU ----
   // the halo-tile transposed conv (fp16mix images present; SESA_HTD_CTR=0: tok_gemm_kernel<conv> phases for A/B)
-  auto ctr = [&](const Branch& br, const float* x, float* o, int Q, int Tn, int act) -> bool {
+  auto ctr = [&](const Branch& br, const float* x, float* o, int Q, int Tn, int act, bool fmajor = false) -> bool {
     static const bool on = !(getenv("SESA_HTD_CTR") && std::string(getenv("SESA_HTD_CTR")) == "0");
     if (!on || br.ctr_img < 0 || rc) return false;
     CtrArgs ca{x, m->d_w + br.ctr_img, Wb + br.ctr_bias, o, B, Q, Tn, br.Cout, br.Cdec, St, br.Fin, pad,
-               act == TOK_ACT_GELU ? 1 : 0};
+               act == TOK_ACT_GELU ? 1 : 0, fmajor ? 1 : 0};
     const bool two_d = Tn > 1;
     const int nq = Q + 1, N = St * br.Cdec;
     const int64_t tiles = two_d ? (int64_t)B * ((nq + 3) / 4) * ((Tn + 63) / 64) : (int64_t)B * ((nq + 255) / 256);
@@ -3428,6 +3432,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
   float* tB = F32(pl.tB);
   float* cur_f = xdec;
   float* cur_t = tdec;
+  // the one-wave iSTFT on a frame-major spectrum (htd_istft_wave_kernel; the last transposed conv writes [B][T][2048][Cz]):
+  // iSTFT class 61.5 -> 45.5 ms per step, configs[3] 1313 -> 1328x same box, parity unchanged (profiles/r05_z_*).
+  // SESA_HTD_ISTFT_WAVE=0: the workgroup-FFT fused kernel on the [B][2048][T][Cz] spectrum (A/B)
+  static const bool istft_wave = !(getenv("SESA_HTD_ISTFT_WAVE") && std::string(getenv("SESA_HTD_ISTFT_WAVE")) == "0");
+  bool spec_fmajor = false;   // cur_f after the loop is [B][T][2048][Cz] (else [B][2048][T][Cz])
   for (int i = c.depth - 1; i >= 0; --i) {
     const Branch& f = m->fq[i];
     const Branch& t = m->tm[i];
@@ -3439,7 +3448,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     if (c.dconv_mode & 2) dconv(f.ddc, dB, B * f.Fout, T, f.Cout, f.h);
     // ConvTranspose2d (K x 1, stride S x 1), trim pad rows at both ends (:178-179)
     float* nxt_f = F32(pl.dA);   // cur_f (also dA) was consumed by the rewrite above (stream order)
-    if (!ctr(f, dB, nxt_f, f.Fout, T, act))
+    // the last layer writes the spectrum frame-major when the one-wave iSTFT consumes it
+    const bool fm = i == 0 && istft_wave && f.Fin == kF0;
+    if (ctr(f, dB, nxt_f, f.Fout, T, act, fm))
+      spec_fmajor = fm;
+    else
       conv_gemm(f.convtr, dB, f.Cout, nullptr, nxt_f, f.Cdec, f.Fout + 1, T, f.Fout, T, 1, f.Cout, tr_d1, {}, act, 0, St,
                 f.Fin, pad);
     cur_f = nxt_f;
@@ -3467,14 +3480,11 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
     // frames + overlap-add in one kernel (iSTFT class 70.2 -> 61.3 ms per step same box, profiles/r05_s_bench_htd_*.json;
     // no 4096-sample frame buffer in HBM); SESA_HTD_ISTFT_FUSED=0: the two-kernel form (A/B)
     static const bool fused = !(getenv("SESA_HTD_ISTFT_FUSED") && std::string(getenv("SESA_HTD_ISTFT_FUSED")) == "0");
-    // one wave per signal, no barrier in the frame loop (htd_istft_wave_kernel), opt-in SESA_HTD_ISTFT_WAVE=1: measured
-    // slower -- iSTFT class 61.5 -> 77.5 ms per step, configs[3] 1250 -> 1240x (profiles/r05_v_*), parity 5.87e-6.  A
-    // wave gathers its frame's 2048 bins from 2048 different lines of the [b][k][t][Cz] spectrum (one 8-B value each)
-    // with one wave per SIMD to cover the latency; the fused kernel's XCD grouping lets 16 (signal, frame) consumers
-    // share each line in L2 instead.
-    static const bool wave = getenv("SESA_HTD_ISTFT_WAVE") && std::string(getenv("SESA_HTD_ISTFT_WAVE")) == "1";
+    // one wave per signal, no barrier in the frame loop (htd_istft_wave_kernel) on the frame-major spectrum.  (On the
+    // [b][k][t][Cz] layout it measured slower than the fused kernel -- 61.5 -> 77.5 ms per step, profiles/r05_v_*: a
+    // wave gathered its frame's 2048 bins from 2048 different lines.)
     const int nper_w = m->nsrc * ach;
-    if (fused && wave) {
+    if (spec_fmajor) {
       const int tp_n = (kPadSpec + kCenter + L - 1) / kHop - (kPadSpec + kCenter) / kHop + 1;
       const int nseg = (tp_n + kIwSeg - 1) / kIwSeg;
       const int64_t groups = (int64_t)B * nseg * ((nper_w + kIwWaves - 1) / kIwWaves);
