@@ -1874,6 +1874,10 @@ __device__ __forceinline__ void idft8(float2* x) {   // inverse 8-point DFT in p
   x[7] = csub(e3, o3);
 }
 
+// PF: the window in LDS (read per frame from there), and the time-branch samples of frame tp's emitted block loaded at
+// the top of the iteration -- so no global load is issued and waited for inside the frame (in-order vmcnt made each
+// such wait also wait for the next frame's spectrum prefetch).
+template <bool PF = true>
 __global__ void __launch_bounds__(64 * kIwWaves, 1) htd_istft_wave_kernel(
     const float* __restrict__ Z, int T, int Cz, int ach, int nsrc, int nseg, const double* __restrict__ stats,
     int64_t n_item, const float* __restrict__ win, Fft2048Tables tb, int L, const float* __restrict__ XT,
@@ -1881,12 +1885,15 @@ __global__ void __launch_bounds__(64 * kIwWaves, 1) htd_istft_wave_kernel(
   __shared__ float2 wbuf[kIwWaves][kFft2048];    // per-wave exchange buffers (64 KiB)
   __shared__ float2 twl[kFft2048 + 1];           // exp(-2 pi i k / 4096), k <= 2048
   __shared__ float envI[kHop];                   // window envelope of an interior sample, by n mod hop
+  __shared__ float2 wlds[PF ? kFft2048 : 1];     // PF: the window as (w[2k], w[2k + 1]) pairs
   const int nper = nsrc * ach;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wpi = (nper + kIwWaves - 1) / kIwWaves;   // workgroups per (item, segment)
   const int g = blockIdx.x / wpi, part = blockIdx.x - g * wpi;
   const int b = g / nseg, seg = g - b * nseg;
   for (int i = threadIdx.x; i <= kFft2048; i += blockDim.x) twl[i] = tb.twN[i];
+  if constexpr (PF)
+    for (int i = threadIdx.x; i < kFft2048; i += blockDim.x) wlds[i] = *reinterpret_cast<const float2*>(win + 2 * i);
   for (int m = threadIdx.x; m < kHop; m += blockDim.x) {
     // the OLA kernel's envelope loop for n with all four frames present: tq ascending = window offset descending
     float env = 0.f;
@@ -1961,6 +1968,20 @@ __global__ void __launch_bounds__(64 * kIwWaves, 1) htd_istft_wave_kernel(
     if (tp < tpb) load_frame(tp - 2);
   }
   for (int tp = tpa - 3; tp < tpb; ++tp) {
+    // PF: the time-branch samples of this iteration's emitted block, in flight under the transform
+    float xtv[PF ? 8 : 1][PF ? 2 : 1];
+    if constexpr (PF) {
+      if (tp >= tpa) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int n = tp * kHop + 2 * (lane + 64 * u) + e;
+            const int i = min(max(n - n0, 0), L - 1);
+            xtv[u][e] = XT[((int64_t)b * L + i) * nper + j];
+          }
+      }
+    }
     if (real(tp)) {   // (wave-uniform)
       float2 d[4][8];
       // pack (irfft_pack): X[2048 - k] from the wave's buffer; k = 0 pairs with the zeroed Nyquist bin
@@ -2025,7 +2046,7 @@ __global__ void __launch_bounds__(64 * kIwWaves, 1) htd_istft_wave_kernel(
         const float2 zq[4] = {e0, e1, e2, e3};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float2 w = buf_ld2(rwin, lane * 8, (64 * u + 512 * q) * 8);
+          const float2 w = PF ? wlds[lane + 64 * u + 512 * q] : buf_ld2(rwin, lane * 8, (64 * u + 512 * q) * 8);
           R[q][u].x += zq[q].x * sc * w.x;
           R[q][u].y += zq[q].y * sc * w.y;
         }
@@ -2052,7 +2073,7 @@ __global__ void __launch_bounds__(64 * kIwWaves, 1) htd_istft_wave_kernel(
               }
             }
             const int i = n - n0;
-            const float xt = XT[((int64_t)b * L + i) * nper + j] * st + mt;
+            const float xt = (PF ? xtv[u][e] : XT[((int64_t)b * L + i) * nper + j]) * st + mt;
             out[(int64_t)sig * L + i] = xt + (e ? R[0][u].y : R[0][u].x) / env;
           }
         }
@@ -3490,9 +3511,17 @@ extern "C" int sesa_htdemucs_forward(sesa_htdemucs* m, const float* x, int B, fl
       const int64_t groups = (int64_t)B * nseg * ((nper_w + kIwWaves - 1) / kIwWaves);
       SESA_REQUIRE(groups < (1ll << 31) && (int64_t)kF0 * T * m->fq[0].Cdec * 4 < (1ll << 31), SESA_ERR_INVALID,
                    "htdemucs forward: iSTFT grid / spectrum plane too large");
-      hipLaunchKernelGGL(htd_istft_wave_kernel, dim3((unsigned)groups), dim3(64 * kIwWaves), 0, st, cur_f, T,
-                         m->fq[0].Cdec, ach, m->nsrc, nseg, st_f, (int64_t)kF0 * T * 2 * ach, win, tb, L, cur_t, st_t,
-                         out);
+      // window in LDS + time-branch prefetch (PF): iSTFT 45.5 -> 35.7 ms per step same box (profiles/r05_ac_*);
+      // SESA_HTD_IW_PF=0: the window and time-branch samples loaded where they are used (A/B)
+      static const bool pf = !(getenv("SESA_HTD_IW_PF") && std::string(getenv("SESA_HTD_IW_PF")) == "0");
+      if (pf)
+        hipLaunchKernelGGL(htd_istft_wave_kernel<true>, dim3((unsigned)groups), dim3(64 * kIwWaves), 0, st, cur_f, T,
+                           m->fq[0].Cdec, ach, m->nsrc, nseg, st_f, (int64_t)kF0 * T * 2 * ach, win, tb, L, cur_t, st_t,
+                           out);
+      else
+        hipLaunchKernelGGL(htd_istft_wave_kernel<false>, dim3((unsigned)groups), dim3(64 * kIwWaves), 0, st, cur_f, T,
+                           m->fq[0].Cdec, ach, m->nsrc, nseg, st_f, (int64_t)kF0 * T * 2 * ach, win, tb, L, cur_t, st_t,
+                           out);
       SESA_CHECK_LAUNCH();
       profile_end(tok, st, SESA_KCLASS_ISTFT, 4.0 * nsig * ((double)T * kF0 * 2 + 2.0 * L));
     } else if (fused) {
