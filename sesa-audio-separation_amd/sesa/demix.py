@@ -64,9 +64,10 @@ def chunk_plan(L, chunk_size, num_overlap, batch_size):
 # short).  Round 5 same-box sweep (profiles/r05_n_bench_*.json): BS-Roformer 4 -> 16 +1.9 %, SCNet 48 -> 96 +3.9 %,
 # HTDemucs 32 -> 48 +1.7 % (64: the same); MDX23C 57 -> 85 per forward +0.75 % (noise level; an explicit cap of 96
 # would trip the half-free-HBM check at the vocals config's 1.7 GB per chunk), so it stays 64.
-# (round 5, same-box A/B on the final kernels, profiles/r05_ad_*: MDX23C 3 x 57 -> 2 x 85 chunks per forward +0.8 %,
-# HTDemucs 14 x 48 -> 11 x 61 +1.8 %)
-EXEC_CAP = {"TFC_TDF_net": 96, "BSRoformer": 16, "MelBandRoformer": 16, "SCNet": 96, "HTDemucs": 64}
+# (round 5, same-box A/B on the final kernels: HTDemucs 14 x 48 -> 11 x 61 chunks per forward +1.8 %,
+# profiles/r05_ad_*.  MDX23C stays at 64: 2 x 85 measured +0.8 % over 3 x 57 with an explicit batch, but its workspace
+# is over the half-free-HBM guard below, which halves cap 96 to 4 x 43 -- 0.6 % slower than 3 x 57, profiles/r05_ae_*)
+EXEC_CAP = {"TFC_TDF_net": 64, "BSRoformer": 16, "MelBandRoformer": 16, "SCNet": 96, "HTDemucs": 64}
 
 
 def unwrap_model(model):
@@ -81,7 +82,7 @@ def unwrap_model(model):
 def plan_exec_batch(model, n_chunks, chunk, device=None, world=1, cap=None, streams=1):
     """Execution batch for ``n_chunks`` chunks of length ``chunk`` spread over ``world`` ranks: the
     model's cap (EXEC_CAP), halved while its workspace would exceed half the free HBM, then balanced
-    so a rank's last forward is not a small remainder (169 chunks at cap 96 -> 2 forwards of 85).
+    so a rank's last forward is not a small remainder (169 chunks at cap 64 -> 3 forwards of 57).
     ``model`` may be the network or a backend wrapping it (HipBackend: the CLI and utils.demix pass
     the backend), so the CLI plans the same batch as bench.py."""
     model = unwrap_model(model)
