@@ -351,6 +351,14 @@ int sesa_profile_read2(int kclass, double* total_ms, int64_t* launches, double* 
  * the roofline bound of each launch's own arithmetic intensity */
 int sesa_profile_floor(int kclass, double peak_tflops, double peak_gbs, double* floor_ms);
 
+/* Diagnostics (tools/streams_trace.py): while a trace is open on the calling host thread, every instrumented launch of
+ * the network forwards is followed, on its own stream, by a kernel that adds a 64-bit checksum of that launch's output
+ * bytes into the next slot of `buf` (device memory, `cap` zeroed uint64 slots), so two runs can be compared launch by
+ * launch.  sesa_debug_trace_end closes the trace, copies each traced launch's kernel class into `classes` (up to cap)
+ * and returns the number of traced launches. */
+int sesa_debug_trace_begin(void* buf, int cap);
+int sesa_debug_trace_end(int* classes, int cap);
+
 #ifdef __cplusplus
 }
 #endif

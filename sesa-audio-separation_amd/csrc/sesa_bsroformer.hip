@@ -697,6 +697,9 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
   BsrTables tb;
   int rc = get_tables(&tb);
   if (rc) return rc;
+  // (diagnostics: the input, then the whole workspace after every launch -- sesa_debug_trace_begin)
+  debug_trace(st, SESA_KCLASS_STFT, x, (size_t)B * ch * c.chunk_size * 4);
+  debug_trace_range(ws, pl.total);
 
   void* tok = profile_begin(st);
   hipLaunchKernelGGL(bsr_stft_kernel, dim3(T, B * ch), dim3(kFT), 0, st, x, ch, c.chunk_size, c.hop_length, T, tb, spec);
@@ -894,6 +897,8 @@ extern "C" int sesa_bsr_forward(sesa_bsr* m, const float* x, int B, float* out, 
                      c.hop_length, c.chunk_size, tb.win, out);
   SESA_CHECK_LAUNCH();
   profile_end(tok, st, SESA_KCLASS_ISTFT, 4.0 * n_sig * ((double)T * m->F * 4 + 2.0 * T * kN + c.chunk_size));
+  debug_trace_range(nullptr, 0);
+  debug_trace(st, SESA_KCLASS_ISTFT, out, (size_t)n_sig * c.chunk_size * 4);
   return SESA_OK;
 }
 

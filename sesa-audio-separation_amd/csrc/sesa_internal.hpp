@@ -21,4 +21,10 @@ void* profile_begin(hipStream_t st);
 // work: algorithmic FLOPs (compute classes) or bytes (streaming classes); bytes: the algorithmic HBM bytes of a
 // compute-class launch (0: not stated)
 void profile_end(void* token, hipStream_t st, int kclass, double work, double bytes = 0.0);
+// checksum of a launch's output bytes into the host thread's trace buffer, if one is set (sesa_debug_trace_begin)
+void debug_trace(hipStream_t st, int kclass, const void* p, size_t bytes);
+// the byte range every later profile_end checksums while a trace is open (nullptr: none)
+void debug_trace_range(const void* p, size_t bytes);
+// SESA_DEBUG_ONLY: true for a launch of a class other than the selected one (the forward skips it)
+bool debug_skip(int kclass);
 }  // namespace sesa

@@ -466,22 +466,23 @@ struct Fwd {
                        : w.kind == CONV1X1 ? SESA_KCLASS_CONV1X1
                        : w.kind == CONV2X2S2 ? SESA_KCLASS_DOWN : SESA_KCLASS_UP;
     void* tok = profile_begin(st);
-    rc = launch_conv(w.kind, w.bn, w.f16 ? w.f16c : x3, a, B, st);
+    if (!debug_skip(kclass)) rc = launch_conv(w.kind, w.bn, w.f16 ? w.f16c : x3, a, B, st);
+    double bytes = 0.0;
     if (tok) {
       // algorithmic HBM bytes: every input element read once in the form the kernel reads it, the output
       // (+ residual) once, the weight image once
       const int64_t pin = (int64_t)B * T_in * F_in;
       const bool one = w.f16 || x3 == 0;
-      double bytes = src_bytes(in.src[0], pin, in.C_split, one) + src_bytes(in.src[1], pin, in.C_in - in.C_split, one);
+      bytes = src_bytes(in.src[0], pin, in.C_split, one) + src_bytes(in.src[1], pin, in.C_in - in.C_split, one);
       if (xin)
         bytes += src_bytes(xin->src[0], pin, xin->C_split, x3 == 0) +
                  src_bytes(xin->src[1], pin, xin->C_in - xin->C_split, x3 == 0);
       bytes += (double)B * T_out * F_out * w.n_cols * 4.0 * (residual ? 2.0 : 1.0);
       const double wb = w.f16 ? (w.f16c == 3 ? 2.0 : 4.0) : (x3 ? 4.0 : 2.0);
       bytes += (double)w.n_cols * (w.C_in * taps * wb + (xin ? xin->C_in * (x3 ? 4.0 : 2.0) : 0.0));
-      profile_end(tok, st, kclass,
-                  2.0 * B * T_out * F_out * (double)w.n_cols * (w.C_in * taps + (xin ? xin->C_in : 0)), bytes);
     }
+    profile_end(tok, st, kclass,
+                2.0 * B * T_out * F_out * (double)w.n_cols * (w.C_in * taps + (xin ? xin->C_in : 0)), bytes);
   }
 
   // bytes of `ch` channels of one conv source over `pos` positions, read once: pre-split planes 2 B (one plane:
@@ -506,7 +507,7 @@ struct Fwd {
     a.n_chunks = (w.K + kTdfBK - 1) / kTdfBK;
     a.u_planes = u_planes;
     void* tok = profile_begin(st);
-    rc = launch_tdf(w.f16 ? 2 : x3, a, B, st, transposed_io);
+    if (!debug_skip(SESA_KCLASS_TDF)) rc = launch_tdf(w.f16 ? 2 : x3, a, B, st, transposed_io);
     // algorithmic bytes: the fp32 input rows (K features) read once, the fp32 output rows (M features) + residual
     // written / read once, the weight image once (fp16 2 B, bf16x3 4 B per coefficient)
     const double rows = (double)B * T * C;
@@ -529,7 +530,7 @@ struct Fwd {
     const GemmIn src = input(a, b, SRC_NORM_GELU, SRC_NORM_GELU, nrm, T, F);
     if (!dry && !rc) {
       void* tok = profile_begin(st);
-      rc = launch_act_split(src, (int64_t)T * F, B, hi, lo, st, rhi, rlo);
+      if (!debug_skip(SESA_KCLASS_ACT)) rc = launch_act_split(src, (int64_t)T * F, B, hi, lo, st, rhi, rlo);
       profile_end(tok, st, SESA_KCLASS_ACT, (raw ? 12.0 : 8.0) * n);
     }
     if (raw) {
@@ -557,7 +558,7 @@ struct Fwd {
     const GemmIn src = input(a, b, SRC_NORM_GELU, SRC_NORM_GELU, nrm, T, F);
     if (!dry && !rc) {
       void* tok = profile_begin(st);
-      rc = launch_act_f16(src, (int64_t)T * F, B, hi, st);
+      if (!debug_skip(SESA_KCLASS_ACT)) rc = launch_act_f16(src, (int64_t)T * F, B, hi, st);
       profile_end(tok, st, SESA_KCLASS_ACT, 6.0 * n);
     }
     GemmIn in{};
@@ -650,7 +651,7 @@ struct Fwd {
     Tensor mix{buf((int64_t)B * T * F * dc), nullptr, dc};
     if (!dry && !rc) {
       void* tok = profile_begin(st);
-      rc = stft_launch(x, B * 2, c.chunk_size, c.hop_length, c.dim_f, 1, c.num_subbands, mix.p, st);
+      if (!debug_skip(SESA_KCLASS_STFT)) rc = stft_launch(x, B * 2, c.chunk_size, c.hop_length, c.dim_f, 1, c.num_subbands, mix.p, st);
       profile_end(tok, st, SESA_KCLASS_STFT, 4.0 * B * (2.0 * c.chunk_size + (double)T * F * dc));
     }
     Tensor fco{buf((int64_t)B * T * F * c.num_channels), stats(c.num_channels), c.num_channels};
@@ -696,7 +697,9 @@ struct Fwd {
     float* frames = buf((int64_t)B * m->ni * 2 * T * c.n_fft);
     if (!dry && !rc) {
       void* tok = profile_begin(st);
-      rc = istft_launch(fin, B * m->ni * 2, c.dim_f, T, c.hop_length, 1, c.num_subbands, m->ni, out, frames, st);
+      if (!debug_skip(SESA_KCLASS_ISTFT))
+        rc = istft_launch(fin, B * m->ni * 2, c.dim_f, T, c.hop_length, 1, c.num_subbands, m->ni, out, frames, st);
+      debug_trace(st, SESA_KCLASS_ISTFT, out, (size_t)B * m->ni * 2 * c.chunk_size * 4);   // (diagnostics only)
       profile_end(tok, st, SESA_KCLASS_ISTFT,
                   4.0 * B * ((double)T * F * cf + m->ni * 2.0 * (2.0 * T * c.n_fft + c.chunk_size)));
     }
@@ -899,7 +902,12 @@ extern "C" int sesa_mdx23c_forward(sesa_mdx23c* m, const float* x, int batch, fl
   f.stats_base = ws + fb;
   f.stats_cap = sb;
   f.float_cap = fb;
+  // (diagnostics: the input, then the float region after every launch -- not the fp64 statistics, whose atomic
+  // summation order is not fixed)
+  debug_trace(st, SESA_KCLASS_STFT, x, (size_t)batch * 2 * m->cfg.chunk_size * 4);
+  debug_trace_range(ws, fb);
   f.run(x, out);
+  debug_trace_range(nullptr, 0);
   return f.rc;
 }
 

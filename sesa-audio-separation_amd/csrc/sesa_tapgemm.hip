@@ -2539,6 +2539,15 @@ __global__ void __launch_bounds__(512) tdf_u_split_kernel(TdfArgs a) {
   if constexpr (!F16) *reinterpret_cast<uint4*>(dst + BN * ROWB + off) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
 }
 
+// An LDS store hipcc's waitcnt pass does not see: it treats every plain store into a __shared__ array that an LDS-DMA
+// (buffer_load ... lds) also writes as possibly aliasing the DMA and waits vmcnt(0) before it (profiles/r06_isa_audit.txt).
+// The caller orders it: the store's data registers are ordinary compiler-tracked values, and its readers sit behind an
+// explicit lgkmcnt(0) + barrier.
+__device__ __forceinline__ void ds_write_b128_untracked(char* p, u32x4 v) {
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)p;
+  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
 // ---------------------------------------------------------------------------------------------
 // tdf_dma_kernel: the TDF Linears (mdx23c_tfc_tdf_v3.py:113-120) with every operand staged by LDS-DMA
 // so each chunk's HBM latency is covered by several chunks of MFMAs (tdf_kernel covers it with one).
@@ -2697,8 +2706,11 @@ __global__ void __launch_bounds__(512, 1) tdf_dma_kernel(TdfArgs a) {
       lw[e / 2] = pack2(l0, l1);
     }
     char* Bhi = smem + B_OFF + (kc & 1) * B_IMG;
-    *reinterpret_cast<uint4*>(Bhi + b_off) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-    if (X3) *reinterpret_cast<uint4*>(Bhi + B_PLANE + b_off) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+    // (inline-asm stores: hipcc treats a plain LDS store into this array as possibly aliasing the in-flight LDS-DMA
+    // and drains vmcnt(0) before it -- every chunk in flight, i.e. the whole ring -- each iteration; the B images are
+    // disjoint from the DMA rings, and the loop's lgkmcnt(0) + barrier orders these stores before their readers)
+    ds_write_b128_untracked(Bhi + b_off, u32x4{hw[0], hw[1], hw[2], hw[3]});
+    if (X3) ds_write_b128_untracked(Bhi + B_PLANE + b_off, u32x4{lw[0], lw[1], lw[2], lw[3]});
   };
 
   f32x16 acc[MI][NI];

@@ -115,6 +115,8 @@ SIGNATURES = {
     "sesa_profile_read2": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "sesa_profile_floor": (c_int, [c_int, ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
+    "sesa_debug_trace_begin": (c_int, [c_void_p, c_int]),
+    "sesa_debug_trace_end": (c_int, [ctypes.POINTER(c_int), c_int]),
 }
 
 KCLASS = {"conv3x3": 0, "conv1x1": 1, "down": 2, "up": 3, "tdf": 4, "stft": 5, "istft": 6, "act": 7, "tokgemm": 8,

@@ -14,6 +14,7 @@ reproduced only as the quantisation it causes (``requantize_special_paths=True``
 import argparse
 import os
 import sys
+import warnings
 
 import numpy as np
 import torch
@@ -72,19 +73,42 @@ def ensemble_separate(members, mix_d, stem="vocals", method="avg_wave", weights=
     from .config import prefer_target_instrument
     from .parallel import demix_sharded
     stems = []
-    for i, (cfg, model) in enumerate(members):
-        names = prefer_target_instrument(cfg)
-        if stem not in names:
-            raise ValueError(f"ensemble member {i} has no '{stem}' stem (instruments: {names})")
-        eb = exec_batch[i] if isinstance(exec_batch, (list, tuple)) else (exec_batch or 8)
-        est = demix_sharded(cfg, model, mix_d, mix_d.device, rank=rank, world=world, exec_batch=eb, group=group,
-                            gather_to=gather_to, simulate=simulate, **(demix_hooks or {}))
-        if est is not None:
-            stems.append(est[names.index(stem)])
+    restore = _spectral_blend_precisions(members, method)
+    try:
+        for i, (cfg, model) in enumerate(members):
+            names = prefer_target_instrument(cfg)
+            if stem not in names:
+                raise ValueError(f"ensemble member {i} has no '{stem}' stem (instruments: {names})")
+            eb = exec_batch[i] if isinstance(exec_batch, (list, tuple)) else (exec_batch or 8)
+            est = demix_sharded(cfg, model, mix_d, mix_d.device, rank=rank, world=world, exec_batch=eb, group=group,
+                                gather_to=gather_to, simulate=simulate, **(demix_hooks or {}))
+            if est is not None:
+                stems.append(est[names.index(stem)])
+    finally:
+        for model, prec in restore:
+            model.set_precision(prec)
     if not stems:
         return None, {}
     x = torch.stack(stems)
     return (blend_fn or blend_device)(x, method, weights, buffer), {i: s for i, s in enumerate(stems)}
+
+
+def _spectral_blend_precisions(members, method):
+    """The spectral blends (max_fft / min_fft / median_fft) take file 0's phase and another member's magnitude per bin,
+    so they amplify an MDX23C member's rounding error (fp16mix: 9.5e-4 max_fft on the full-width fixtures against
+    4.1e-5 in bf16x3, profiles/r05_ens_parity_scan.txt).  For those methods every MDX23C member not already in bf16x3
+    runs bf16x3 for this call (with a warning); returns [(model, precision to restore)]."""
+    if not method.endswith("_fft"):
+        return []
+    restore = []
+    for i, (_, model) in enumerate(members):
+        m = getattr(model, "module", model)   # nn.DataParallel
+        if getattr(m, "_prefix", None) == "mdx23c" and getattr(m, "precision", "bf16x3") != "bf16x3":
+            warnings.warn(f"ensemble member {i} (MDX23C, {m.precision}): the {method} blend amplifies its rounding "
+                          f"error past the 1e-4 parity gate; running it in bf16x3 for this ensemble")
+            restore.append((m, m.precision))
+            m.set_precision("bf16x3")
+    return restore
 
 
 class AudioEnsembleEngine:

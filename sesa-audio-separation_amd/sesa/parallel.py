@@ -215,6 +215,8 @@ def demix_sharded(config, model, mix_d, device=None, rank=None, world=None, exec
     n_ch, L = mix_d.shape
     rows = ni * n_ch
     if L == 0:
+        if world > 1 and not simulate and gather_to is not None and rank != gather_to:
+            return None   # (the gather contract: only rank gather_to holds the result)
         return torch.zeros(ni, n_ch, 0, device=mix_d.device, dtype=torch.float32)
     plan = shard_plan(config, L, world, mode)
     if local_fn is None:
