@@ -147,7 +147,7 @@ MODEL_SRC = {"mdx23c": ("sesa_mdx23c.hip",), "bs_roformer": ("sesa_bsroformer.hi
 def kernel_sources_sha16(kclass, model=None):
     import hashlib
     h = hashlib.sha256()
-    files = list(KSRC[kclass])
+    files = list(KSRC[kclass]) + ["Makefile"]   # (the build flags shape the code as much as the sources)
     for fn in MODEL_SRC.get(model, ()):
         if fn not in files:
             files.append(fn)
@@ -241,10 +241,14 @@ def class_precision(kclass, precision, model="mdx23c", members=None):
     return "fp16" if "fp16" in modes else (modes.pop() if len(modes) == 1 else "bf16x3")
 
 
-def pmc_traffic(kclass, precision="bf16x3", model=None):
+def pmc_traffic(kclass, precision="bf16x3", model=None, records_per_step=None):
     """(HBM bytes per launch, provenance) from profiles/pmc_<class>_<model>.json when its ``src_sha16`` matches
     the kernel sources in this tree (the class's sources + the model's own) and it was measured in the same
-    precision mode; (None, reason) otherwise -- a stale counter figure is not reported."""
+    precision mode; (None, reason) otherwise -- a stale counter figure is not reported.
+    A "launch" is one of libsesa's profile records -- the unit the algorithmic bytes are counted in.  Some records
+    cover several kernel dispatches (SCNet's `simt` band convs: 9 per record; HTDemucs' DConv: 2), so with
+    ``records_per_step`` (this run's records of the class per step) the counter bytes of one whole step are divided
+    by it: traffic and algorithmic bytes then share one unit."""
     name = f"pmc_{kclass}_{model}.json" if model else f"pmc_{kclass}.json"
     pmc = os.path.join(REPO, "profiles", name)
     if not os.path.exists(pmc):
@@ -258,9 +262,14 @@ def pmc_traffic(kclass, precision="bf16x3", model=None):
     if d.get("precision", "bf16x3") != precision:
         return None, (f"profiles/{name} measured in precision {d.get('precision', 'bf16x3')}, this run "
                       f"is {precision}: not reported")
-    return d.get("hbm_bytes_per_launch"), {"file": f"profiles/{name}", "src_sha16": cur,
-                                           "git_sha": d.get("git_sha"), "precision": precision,
-                                           "algorithmic_bytes_per_launch": d.get("algorithmic_bytes_per_launch")}
+    prov = {"file": f"profiles/{name}", "src_sha16": cur, "git_sha": d.get("git_sha"), "precision": precision,
+            "algorithmic_bytes_per_launch": d.get("algorithmic_bytes_per_launch")}
+    if records_per_step and d.get("hbm_bytes_per_step"):
+        prov.update(counter_bytes_per_step=d["hbm_bytes_per_step"], dispatches_per_step=d.get("dispatches_per_step"),
+                    records_per_step=round(records_per_step, 2),
+                    unit="counter bytes of one step / libsesa records of the class per step")
+        return round(d["hbm_bytes_per_step"] / records_per_step), prov
+    return d.get("hbm_bytes_per_launch"), prov
 
 
 def conv_plan_modes(precision, plan=None):
@@ -586,11 +595,13 @@ def main():
     ap.add_argument("--no-parity", action="store_true", help="skip the parity forward (PMC passes: one workload only)")
     ap.add_argument("--no-pcie", action="store_true",
                     help="skip the PCIe-inclusive timing (PMC / kernel-trace runs: the timed steps only)")
-    ap.add_argument("--streams", type=int, default=1, help="forwards in flight on separate HIP streams (> 1 is refused: "
-                    "not bit-consistent, sesa/parallel.py)")
+    ap.add_argument("--streams", type=int, default=1, help="forwards in flight on separate HIP streams (bit-identical "
+                    "to 1, sesa/parallel.py)")
     ap.add_argument("--rank-share", type=int, default=0, metavar="W",
                     help="one-GPU rehearsal of rank 0's share of a W-rank run (its chunks, its exec batch, local OLA + "
                          "finalise, no collective): value = the implied W-rank ceiling (track seconds / rank-0 time)")
+    ap.add_argument("--gather", action="store_true",
+                    help="multi-GPU: gather every rank's span to rank 0 (the round-5 form) instead of the owned form")
     ap.add_argument("--cpu-chunks-only", action="store_true",
                     help="mdx23c: time --cpu-sample-chunks forwards instead of the configs[0] 10 s end-to-end run")
     args = ap.parse_args()
@@ -656,20 +667,38 @@ def main():
     stems_host = None
 
     mix_dev = mix_host.to(dev)     # the track resident in HBM: `value`'s timed region starts from it
+    # Multi-GPU (and its one-GPU rehearsal): the OWNED form (sesa/parallel.py demix_owned) -- each rank uploads only
+    # the mix samples its chunks read, exchanges one seam with each neighbour and finalises its own output range,
+    # which it copies to the host itself; no rank gathers the track.  The ensemble (members with different chunk
+    # plans blended sample by sample) and plans with a rank shorter than one seam keep the gather to rank 0.
+    from sesa.parallel import demix_owned, input_span, owned_ranges
+    owned = (pworld > 1 and args.model != "ensemble" and not args.gather
+             and owned_ranges(shard_plan(members[0][1], n, pworld, modes[0])) is not None)
+    span = input_span(shard_plan(members[0][1], n, pworld, modes[0]), rank, n) if owned else (0, n)
+    mix_span_buf = torch.empty_like(mix_dev) if owned else None
 
     def step(pcie=False):
         """One pass of the hot path over the track.  pcie=False (`value`): from the mix resident in HBM to the stems
-        in HBM.  pcie=True (`pcie_inclusive`): pinned host mix -> H2D -> separation -> stems D2H."""
+        in HBM.  pcie=True (`pcie_inclusive`): pinned host mix -> H2D -> separation -> stems D2H (owned form: each
+        rank moves only its input span and its own output range over its own PCIe link)."""
         nonlocal stems_host
-        mix_d = mix_host.to(dev, non_blocking=True) if pcie else mix_dev
+        if pcie and owned:
+            mix_span_buf[:, span[0]:span[1]].copy_(mix_host[:, span[0]:span[1]], non_blocking=True)
+            mix_d = mix_span_buf
+        else:
+            mix_d = mix_host.to(dev, non_blocking=True) if pcie else mix_dev
         if args.model == "ensemble":
             est = ensemble_separate([(cfg, m) for m, cfg, _ in members], mix_d, "vocals", args.blend, rank=rank,
                                     world=pworld, exec_batch=batches, simulate=sim)[0]
+        elif owned:
+            m, cfg, _ = members[0]
+            est = demix_owned(cfg, m, mix_d, dev, rank=rank, world=pworld, exec_batch=batches[0], mode=modes[0],
+                              streams=args.streams, simulate=sim)[0]
         else:
             m, cfg, _ = members[0]
             est = demix_sharded(cfg, m, mix_d, dev, rank=rank, world=pworld, exec_batch=batches[0], mode=modes[0],
                                 streams=args.streams, simulate=sim)
-        if pcie and rank == 0:   # stems D2H (one copy of the result; the RCCL gather delivers it to rank 0 only)
+        if pcie and est is not None:   # stems D2H (gather form: rank 0's whole result; owned form: each rank's range)
             if stems_host is None or stems_host.shape != est.shape or stems_host.dtype != est.dtype:
                 stems_host = torch.empty(est.shape, dtype=est.dtype, pin_memory=True)
             stems_host.copy_(est, non_blocking=True)
@@ -709,8 +738,8 @@ def main():
         t = torch.tensor([elapsed, elapsed_pcie], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, elapsed_pcie = (float(v) for v in t.tolist())
-    assert (est is None) == (rank != 0)
-    if rank == 0:
+    assert owned or (est is None) == (rank != 0)
+    if est is not None:
         assert torch.isfinite(est).all().item()
         assert args.no_pcie or (torch.isfinite(stems_host).all().item() and stems_host.shape == est.shape)
 
@@ -762,7 +791,7 @@ def main():
     kclass = MODELS[args.model][2] or max(roofs, key=lambda k: roofs[k]["ms_per_step"])
     roof = dict(roofs[kclass])
     traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model, member_prec),
-                                       args.model)
+                                       args.model, roof["launches"] / args.steps)
     if isinstance(traffic_src, dict):   # one algorithmic figure: this run's (the PMC file's own is for its run)
         traffic_src.pop("algorithmic_bytes_per_launch", None)
     alg_bytes = roof["algorithmic_bytes_per_launch"]
@@ -793,16 +822,23 @@ def main():
             "metric": METRIC[args.model] + (f" -- rank-0 share of {pworld} ranks, one-GPU rehearsal" if sim else ""),
             "value": round(value, 3), "unit": "separated-audio sec/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
+            "scaling": "strong", "vs_baseline": None,
+            "dtype": args.precision if len(names) == 1 else "+".join(f"{nm}:{member_prec[nm]}" for nm in names),
+            # (rounds 1-4 and the first round-5 leases reported the PCIe-inclusive rate -- now `pcie_inclusive.value`
+            # -- as `value`; from the last round-5 lease on, `value` is the HBM-resident rate, the bench contract's
+            # "inputs already resident in HBM")
+            "value_basis": "hbm_resident", "bench_contract_version": 2,
             "data": "synthetic: 0.1*N(0,1) stereo mix (seed 0), name-keyed random-init weights",
             "config": {"workload": f"{desc[0]}, {track_seconds:.0f} s 44.1 kHz stereo track chunked; timed: the mix "
                                    f"resident in HBM -> gather -> forwards -> OLA -> finalise -> stems in HBM "
                                    f"(pcie_inclusive adds the pinned host mix H2D and the stems D2H)",
                        "model": args.model, "chunks": n_chunks,
                        "exec_batch": batches[0] if len(batches) == 1 else batches,
-                       "parallelism": (f"chunk-shard x{world} + RCCL gather to rank 0" if world > 1 else
+                       "parallelism": ((f"chunk-shard x{world}, owned ranges: per-rank input span H2D, RCCL seam "
+                                        f"exchange with neighbours, per-rank finalise + D2H" if owned else
+                                        f"chunk-shard x{world} + RCCL gather to rank 0") if world > 1 else
                                        f"1 GPU: rank 0's share of a {pworld}-rank chunk shard (rehearsal, no "
-                                       f"collective)" if sim else "1 GPU"),
+                                       f"collective; {'owned' if owned else 'gather'} form)" if sim else "1 GPU"),
                        "shard": {"world_size": dist.get_world_size() if world > 1 else 1,
                                  "backend": dist.get_backend() if world > 1 else None,
                                  "chunk_ranges": shard_ranges[0] if len(shard_ranges) == 1 else shard_ranges,
@@ -812,8 +848,10 @@ def main():
             "pcie_inclusive": None if args.no_pcie else {
                 "value": round(track_seconds * args.steps / elapsed_pcie, 3),
                 "ms_per_step": round(elapsed_pcie / args.steps * 1e3, 2),
-                "note": "same K steps from the pinned host mix (H2D) to the stems in pinned host memory (D2H on "
-                        "rank 0), transfers on the compute stream"},
+                "note": ("same K steps from the pinned host mix (H2D) to the stems in pinned host memory (D2H), "
+                         "transfers on the compute stream; " + ("owned form: each rank uploads its input span and "
+                                                               "downloads its own output range" if owned else
+                                                               "the whole mix to every rank, the stems from rank 0"))},
         }
         if sim:
             line["rehearsal"] = {

@@ -9,15 +9,17 @@
  * returns 0 on success or a negative SESA_ERR_* code with a thread-local message available
  * from sesa_last_error().
  *
- * Concurrency: the network forwards (sesa_mdx23c_forward, sesa_bsr_forward, sesa_scnet_forward,
- * sesa_htdemucs_forward) take all mutable state from the caller's workspace -- measured independent of its
- * prior contents and writing nothing outside their buffers (tools/ws_guard.py, every model / precision) -- and
- * are bit-reproducible run to run on one stream.  They are NOT re-entrant across streams of one device: with
- * forwards of one handle in flight on 2-4 streams at once, 3 of 9 runs on MI355X differed from the one-stream
- * result by up to 1.2e-3, while every configuration that device-synchronised after all launches but those of any
- * one kernel class agreed bit for bit (tools/streams_bisect.py, profiles/r05_streams_bisect.txt); the cause is not
- * found.  Callers serialise forwards on one stream per device (sesa/parallel.py refuses streams > 1); the other
- * entry points (STFT / iSTFT / gather / OLA / blend) are plain streaming kernels without shared state.
+ * Concurrency: functions are re-entrant per stream.  The network forwards (sesa_mdx23c_forward, sesa_bsr_forward,
+ * sesa_scnet_forward, sesa_htdemucs_forward) take all mutable state from the caller's workspace -- measured independent
+ * of its prior contents and writing nothing outside their buffers (tools/ws_guard.py) -- and read the handle's packed
+ * weights only, so forwards of one handle may run on several streams of one device at once, each with its own
+ * workspace, input and output; the results are bit-identical to running them one after another
+ * (tests/test_gpu_parity.py::test_side_streams_bit_identical).  Rounds 4-5 saw them differ: the FFT kernels'
+ * SLP-packed complex arithmetic (v_pk_add_f32 / v_pk_mul_f32 with a source op_sel) returned wrong values on gfx950
+ * while another wave on the same CU executed MFMAs (profiles/r06_pk_opsel_hazard.txt); libsesa is built without
+ * such instructions and tools/isa_guard.py fails the build if one appears.  The other entry points (STFT / iSTFT /
+ * gather / OLA / blend) are plain streaming kernels without shared state.  Only sesa_*_set_param / _finalize /
+ * _destroy mutate a handle and must not overlap its forwards.
  *
  * Compute is fp32 in / fp32 out.  The MDX23C network runs its contractions on MFMA in one of
  * two precisions (sesa_mdx23c_config.precision):

@@ -2215,7 +2215,9 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     // FeatureConversion
     void* tok = profile_begin(st);
     const float scale = (float)(1.0 / std::sqrt((double)T));
-    if (scn_dft_mfma()) {
+    // (the MFMA form stages a whole sequence's columns in LDS: past ~1270 frames even the one-block stage exceeds the
+    // 160 KiB, so such long chunks keep the VALU DFTs)
+    if (scn_dft_mfma() && dft_lds_bytes(1, m->dft_ks[i % 2]) <= 160 * 1024) {
       const int dir = i % 2, Ch = d / 2;
       DftArgs a{};
       a.in = X;

@@ -18,6 +18,12 @@ Chunks of the chunker/OLA are independent given the mix, so:
   chunk order as the single-GPU path (``sesa_ola_accumulate_f32`` with no result rows), so it is
   bit-identical to it and is not exchanged; then ``result / counter`` is finalised.
 
+The OWNED form (``demix_owned``, round 6; bench.py's multi-GPU line): no rank assembles the track.  Each rank
+uploads only the mix samples its chunks read (``input_span``), sends the seam of its span buffer -- the C - step
+samples its last chunks share with the next rank's first -- to that neighbour (``exchange_halos``: one RCCL
+point-to-point message per neighbour pair, ~C x rows x 4 B), and finalises the output range its chunks start in
+(``owned_ranges``), which it can copy to the host on its own PCIe link: the ranks' ranges tile the track.
+
 Summation order at the seams differs from the reference's sequential chunk order only by the
 grouping of fp32 additions (rank partial sums), ~1e-7 relative.
 """
@@ -79,7 +85,6 @@ def _runs(group):
 
 
 _SIDE_STREAMS = {}
-_ALLOW_STREAMS = False   # diagnostics only (tools/streams_bisect.py): lift the streams > 1 refusal below
 
 
 def side_streams(device, n):
@@ -97,16 +102,12 @@ def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, 
     ``streams`` > 1: consecutive forwards alternate between the current stream and side streams (each
     with its own input buffer and model workspace) so that one forward's memory-bound phases can overlap
     another's MFMA-bound ones; the OLA of every forward stays on the current stream, in chunk order,
-    after an event on its forward's stream (the result equals streams = 1 up to the order of the norm
-    statistics' fp64 atomic adds, which concurrent forwards interleave)."""
+    after an event on its forward's stream, so the result is bit-identical to streams = 1
+    (tests/test_gpu_parity.py::test_side_streams_bit_identical).  (Rounds 4-5 refused streams > 1: the FFT
+    kernels' SLP-packed complex arithmetic -- v_pk_*_f32 with a source op_sel -- computed wrong values while
+    another stream's MFMA kernel shared their CUs; libsesa is now built without those instructions,
+    tools/isa_guard.py)"""
     from . import ops
-    if int(streams) > 1 and not _ALLOW_STREAMS:
-        # measured on MI355X (tools/streams_debug2.py, profiles/r04_streams_debug.txt): streams = 2 changed 415
-        # samples of the first group's span by up to 9e-4 while streams = 3 and every single-stream run agreed
-        # bit for bit, and a forward on a side stream alone is bit-identical -- an unresolved ordering hazard, so
-        # the overlapped form is refused rather than shipped
-        raise NotImplementedError("local_accumulate_device: streams > 1 is disabled (not bit-consistent with "
-                                  "streams = 1 on MI355X; see DESIGN.md §6)")
     C = plan["chunk"]
     n_ch = mix_d.shape[0]
     device = mix_d.device
@@ -195,6 +196,112 @@ def exchange_and_assemble(local, plan, rank, world, group=None, gather_to=0, sim
         if e > s and (not simulate or r == rank):
             full[:, s:e] += gathered[r][:, :e - s]
     return full
+
+
+def owned_ranges(plan):
+    """Padded-coordinate range [a_r, b_r) of the output each rank finalises in the owned form: consecutive non-empty
+    ranks own from their first chunk's start to the next non-empty rank's (the first from 0, the last to L_pad);
+    empty ranks own nothing.  None when some rank's span reaches past the next rank's owned range (a rank with fewer
+    than overlap - 1 chunks): then only the gather form assembles the seams."""
+    ne = [r for r, (lo, hi) in enumerate(plan["ranges"]) if hi > lo]
+    own = [(0, 0)] * len(plan["ranges"])
+    for i, r in enumerate(ne):
+        a = 0 if i == 0 else plan["spans"][r][0]
+        b = plan["L_pad"] if i + 1 == len(ne) else plan["spans"][ne[i + 1]][0]
+        own[r] = (a, b)
+    for i in range(len(ne) - 1):
+        if plan["spans"][ne[i]][1] > own[ne[i + 1]][1]:
+            return None
+    return own
+
+
+def input_span(plan, rank, L):
+    """Unpadded sample range [lo, hi) of the mix rank ``rank``'s chunks read (the reflect border of the track's ends
+    included): the part of a host-resident track that rank has to upload.  (0, 0) for an empty rank."""
+    lo_c, hi_c = plan["ranges"][rank]
+    if lo_c >= hi_c:
+        return 0, 0
+    s, e = plan["spans"][rank]
+    b = plan["border"]
+    lo = max(0, s - b - 1)
+    hi = L if e - b > L else e - b + 1
+    if s - b < 0:       # reflect pad of the track's start reads samples 1 .. b
+        hi = max(hi, min(L, b + 1))
+    if e - b > L:       # ... and of its end L - 2 .. L - 1 - b
+        lo = min(lo, max(0, L - b - 2))
+    return lo, min(hi, L)
+
+
+def exchange_halos(local, plan, rank, group=None):
+    """Owned form's only exchange: every non-empty rank sends the tail of its span buffer that overlaps the next
+    non-empty rank's span (C - step samples, the seam) to that rank, which adds it in -- RCCL point-to-point
+    (gloo on CPU), one message per neighbour pair."""
+    ne = [r for r, (lo, hi) in enumerate(plan["ranges"]) if hi > lo]
+    if rank not in ne:
+        return local
+    i = ne.index(rank)
+    ops_ = []
+    recv = None
+    if i + 1 < len(ne):
+        nx = ne[i + 1]
+        s, e = plan["spans"][rank]
+        t0 = plan["spans"][nx][0] - s
+        if e - s > t0:
+            tail = local[:, t0:e - s].contiguous()
+            ops_.append(dist.P2POp(dist.isend, tail, nx if group is None else dist.get_global_rank(group, nx), group))
+    if i > 0:
+        pv = ne[i - 1]
+        n = plan["spans"][pv][1] - plan["spans"][rank][0]
+        if n > 0:
+            recv = torch.empty(local.shape[0], n, device=local.device, dtype=local.dtype)
+            ops_.append(dist.P2POp(dist.irecv, recv, pv if group is None else dist.get_global_rank(group, pv), group))
+    for w in (dist.batch_isend_irecv(ops_) if ops_ else []):
+        w.wait()
+    if recv is not None:
+        local[:, :recv.shape[1]] += recv
+    return local
+
+
+def demix_owned(config, model, mix_d, device=None, rank=None, world=None, exec_batch=8, group=None, local_fn=None,
+                finalize_fn=None, counter_fn=None, mode="generic", streams=1, simulate=False):
+    """The owned form of the chunk shard: each rank finalises only the part of the output its chunks start in
+    (``owned_ranges``) after one halo exchange with its neighbours, so no rank gathers the track: returns
+    (est [n_instr, 2, hi - lo], lo, hi) -- the unpadded sample range [lo, hi) of the stems this rank holds; the
+    ranks' ranges tile [0, L).  The mix need only be resident over ``input_span`` (the rest of ``mix_d`` is not
+    read).  Falls back to None when the plan has a rank too short for a single seam (``owned_ranges``); callers
+    then use ``demix_sharded``."""
+    rank = dist.get_rank(group) if rank is None else rank
+    world = dist.get_world_size(group) if world is None else world
+    instruments = list(config.training.instruments) if mode == "demucs" else prefer_target_instrument(config)
+    ni = len(instruments)
+    n_ch, L = mix_d.shape
+    rows = ni * n_ch
+    if L == 0:
+        return torch.zeros(ni, n_ch, 0, device=mix_d.device, dtype=torch.float32), 0, 0
+    plan = shard_plan(config, L, world, mode)
+    own = owned_ranges(plan)
+    if own is None:
+        return None
+    if local_fn is None:
+        local = local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, streams)
+    else:
+        local = local_fn(config, model, mix_d, plan, rank, rows)
+    if world > 1 and not simulate:
+        local = exchange_halos(local, plan, rank, group)
+    a, b = own[rank]
+    bd = plan["border"]
+    lo, hi = max(a, bd), min(b, plan["L_pad"] - bd)        # padded range that survives the border crop
+    if hi <= lo:
+        return torch.zeros(ni, n_ch, 0, device=mix_d.device, dtype=torch.float32), 0, 0
+    s0 = plan["spans"][rank][0]
+    counter = counter_device(plan, mix_d.device) if counter_fn is None else counter_fn(plan)
+    seg = local[:, lo - s0:hi - s0].contiguous()
+    if finalize_fn is None:
+        from . import ops
+        est = ops.ola_finalize(seg, counter[lo:hi].contiguous(), 0)
+    else:
+        est = finalize_fn(seg, counter[lo:hi].contiguous(), 0)
+    return est.reshape(ni, n_ch, hi - lo), lo - bd, hi - bd
 
 
 def demix_sharded(config, model, mix_d, device=None, rank=None, world=None, exec_batch=8, group=None,

@@ -120,6 +120,28 @@ __global__ void __launch_bounds__(256) vic_pkst(float* out, int iters, int mode)
   out[t] = __uint_as_float(bad);
 }
 
+// one packed form of the compiler's FFT code per mode, in a dependent chain (tools/victim_stress.py form<k>)
+template <int MODE>
+__global__ void __launch_bounds__(256) vic_form(float* out, int iters, float sv0, float sv1) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  f32x2 x = {1.0f + 1e-3f * (t & 1023), 1.0f - 1e-3f * (t & 511)}, y = {1.0001f, 0.9999f}, z = {1e-5f, -2e-5f};
+  const f32x2 sp = {sv0, sv1};   // kernel-argument values: SGPR pair
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (MODE == 0) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(x) : "v"(z));
+    if constexpr (MODE == 1) asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(x) : "v"(z));
+    if constexpr (MODE == 2) asm volatile("v_pk_add_f32 %0, %0, %1 op_sel:[0,1] op_sel_hi:[0,1]" : "+v"(x) : "v"(z));
+    if constexpr (MODE == 3) asm volatile("v_pk_mul_f32 %0, %0, %1 op_sel:[0,1] op_sel_hi:[1,0]" : "+v"(x) : "v"(y));
+    if constexpr (MODE == 4) asm volatile("v_pk_fma_f32 %0, %0, %1, %2 neg_lo:[0,0,1] neg_hi:[0,0,1]" : "+v"(x) : "v"(y), "v"(z));
+    if constexpr (MODE == 5) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(x) : "s"(sp));
+    if constexpr (MODE == 6) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(x) : "s"(sp), "v"(z));
+    if constexpr (MODE == 7) asm volatile("v_pk_mov_b32 %0, %0, %1 op_sel:[1,0]" : "+v"(x) : "v"(y));
+    if constexpr (MODE == 8) asm volatile("v_pk_fma_f32 %0, %0, 0.5, %1 op_sel_hi:[1,0,1]" : "+v"(x) : "v"(y));
+    if constexpr (MODE == 7) x = x * 1.0001f;
+  }
+  out[2 * t] = x[0];
+  out[2 * t + 1] = x[1];
+}
+
 // scalar f32 FMA chain (v_fma_f32), registers only
 __global__ void __launch_bounds__(256) vic_fma(float* out, int iters) {
   const int t = blockIdx.x * 256 + threadIdx.x;
@@ -154,6 +176,9 @@ extern "C" int vic_launch(int which, int blocks, int iters, void* out, void* str
     case 1: hipLaunchKernelGGL(vic_fma, dim3(blocks), dim3(256), 0, st, (float*)out, iters); break;
     case 2: hipLaunchKernelGGL(vic_lds, dim3(blocks), dim3(256), 0, st, (float*)out, iters); break;
     case 3: hipLaunchKernelGGL(vic_pkmix, dim3(blocks), dim3(256), 0, st, (float*)out, iters); break;
+#define VF(K) case 20 + K: hipLaunchKernelGGL(vic_form<K>, dim3(blocks), dim3(256), 0, st, (float*)out, iters, 1.0001f, 0.9999f); break;
+    VF(0) VF(1) VF(2) VF(3) VF(4) VF(5) VF(6) VF(7) VF(8)
+#undef VF
     case 10: case 11: case 12: case 13: case 14: case 15:
       hipLaunchKernelGGL(vic_pkst, dim3(blocks), dim3(256), 0, st, (float*)out, iters, which - 10); break;
     default: return -1;

@@ -21,7 +21,7 @@ def main():
     lib.agg_launch.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     lib.vic_launch.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
     names = ["pk", "fma", "lds", "pkmix"] + [""] * 6 + ["st_pkmul", "st_pkadd", "st_pkfma", "st_scalar", "st_pkmul_nop",
-                                                       "st_pkmul_global"]
+                                                       "st_pkmul_global"] + [""] * 4 + [f"form{k}" for k in range(9)]
     vi = names.index(vic)
     blocks, vit = 512, {"pk": 4000, "fma": 4000, "lds": 200, "pkmix": 2000}.get(vic, 2000)
     main_s = torch.cuda.current_stream(dev)
