@@ -1348,6 +1348,11 @@ struct Level {
   BandConv sd[3], su[3];
   int64_t sd_w[3], sd_b[3], gc_w, gc_b, fu_w, fu_b, su_w[3], su_b[3];
   Gemm gc_gm, fu_gm;                  // globalconv / FusionLayer as implicit-GEMM convs (MFMA, bf16x3)
+  // SD / SU band convs as implicit GEMMs in tok_gemm's sub-range conv form (sd_mm / su_mm: the band's geometry
+  // has that form -- SU needs kern == stride (one tap, `stride` output phases) or stride 1 (flipped taps))
+  bool sd_mm[3], su_mm[3];
+  ConvGeo sd_geo[3], su_geo[3];
+  Gemm sd_gm[3], su_gm[3];
   std::vector<CmLayer> cm[3];
 };
 
@@ -1422,6 +1427,13 @@ bool scn_conv3_mfma() {
 
 // FeatureConversion DFTs on MFMA (scn_dft_mfma_kernel, bf16x3); SESA_SCN_DFT=0 keeps the fp32 VALU direct DFTs
 // (scn_rfft_kernel / scn_irfft_kernel) for A/B.
+// SESA_SCN_BAND_VALU=1: the SD / SU band convs on the fp32 VALU kernels (scn_sdconv_kernel / scn_convtr_kernel)
+// instead of tok_gemm's conv mode (A/B runs)
+bool scn_band_mfma() {
+  static const bool v = !(getenv("SESA_SCN_BAND_VALU") && std::string(getenv("SESA_SCN_BAND_VALU")) == "1");
+  return v;
+}
+
 bool scn_dft_mfma() {
   static const bool v = !(getenv("SESA_SCN_DFT") && std::string(getenv("SESA_SCN_DFT")) == "0");
   return v;
@@ -1562,6 +1574,39 @@ extern "C" int sesa_scnet_create(const sesa_scnet_config* cfg, sesa_scnet** out)
       su.out_off = bc.in_off;
     }
     L.Fout = fo;
+    // band conv geometry on the (F, T) grid, taps along F; input / output bands are row sub-ranges of the level
+    // tensors [B][F][T][C] (scnet.py:114-148 SD, :171-196 SU)
+    for (int b = 0; b < 3; ++b) {
+      const BandConv& bc = L.sd[b];
+      ConvGeo& g = L.sd_geo[b];
+      g = ConvGeo{};
+      g.P1 = bc.n_out; g.P2 = m->T; g.Q1 = bc.n_in; g.Q2 = m->T; g.s1 = bc.stride; g.s2 = 1;
+      g.Cin = L.Cin;
+      g.n_taps = bc.kern;
+      for (int kk = 0; kk < std::min(bc.kern, kMaxTaps); ++kk) g.d1[kk] = kk - bc.pad_left;
+      g.phases = 1; g.O1 = bc.n_out;
+      g.xq1 = L.Fin; g.x_row0 = bc.in_off; g.oq1 = L.Fout; g.o_row0 = bc.out_off;
+      L.sd_mm[b] = bc.kern <= kMaxTaps && L.Cin % 4 == 0;
+      const BandConv& su = L.su[b];
+      ConvGeo& u = L.su_geo[b];
+      u = ConvGeo{};
+      u.P2 = m->T; u.Q1 = su.n_in; u.Q2 = m->T; u.s1 = 1; u.s2 = 1;
+      u.Cin = L.Cout;
+      u.O1 = su.n_out;
+      u.xq1 = L.Fout; u.x_row0 = su.in_off; u.oq1 = L.Fin; u.o_row0 = su.out_off;
+      if (su.kern == su.stride) {  // input row fi -> output rows fi s + r - dist, r < s: one tap, s phases
+        u.P1 = su.n_in;
+        u.n_taps = 1;
+        u.phases = su.stride;
+        u.opad = su.dist;
+      } else {                     // stride 1: output row fo <- input rows fo + dist - kk (flipped taps)
+        u.P1 = su.n_out;
+        u.n_taps = su.kern;
+        for (int kk = 0; kk < std::min(su.kern, kMaxTaps); ++kk) u.d1[kk] = su.dist - kk;
+        u.phases = 1;
+      }
+      L.su_mm[b] = (su.kern == su.stride || (su.stride == 1 && su.kern <= kMaxTaps)) && L.Cout % 4 == 0;
+    }
     if (L.h < 1) return fail("ConvolutionModule hidden size must be >= 1", L.h);
     if (L.Cout % 16 || L.Cdec % 4) return fail("dims must be multiples of 16 (decoder output channels of 4)", L.Cout);
     // the row-resident kernels where they fit (base / small configs), else the wide-level kernels
@@ -1785,6 +1830,36 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
         true, [&](int n) { return Bf[(n & 1) ? C + (n >> 1) : (n >> 1)]; }, blob, bias, f16w);
     g.x_off = g.o_off = 0;
     L.fu_gm.groups = {g};
+    // band convs: SD K = kern x Cin (tap-major); SU one tap with `stride` phases (column r Cdec + co = kernel row
+    // r, output channel co), or stride 1 with K = kern x Cin
+    for (int b = 0; b < 3; ++b) {
+      const std::string sp = "encoder." + S(i) + ".SDlayer.convs." + S(b);
+      const auto& Ws = P(m, sp + ".weight");  // [Cout][Cin][k][1]
+      const auto& Bs = P(m, sp + ".bias");
+      const int k = L.sd[b].kern, Ci = L.Cin;
+      if (L.sd_mm[b]) {
+        g = pack_group(
+            L.Cout, k * Ci, [&](int n, int kx) { const int kk = kx / Ci, ci = kx - kk * Ci; return Ws[((size_t)n * Ci + ci) * k + kk]; },
+            true, [&](int n) { return Bs[n]; }, blob, bias, f16w);
+        g.x_off = g.o_off = 0;
+        L.sd_gm[b].groups = {g};
+      }
+      const std::string up = dpfx + ".1.convtrs." + S(b);
+      const auto& Wu = P(m, up + ".weight");  // [Cout][Cdec][k][1]
+      const auto& Bu = P(m, up + ".bias");
+      const int ku = L.su[b].kern, s = L.su[b].stride, Cu = L.Cout, Cd = L.Cdec;
+      if (!L.su_mm[b]) continue;
+      if (ku == s)
+        g = pack_group(
+            s * Cd, Cu, [&](int n, int ci) { const int r = n / Cd, co = n - r * Cd; return Wu[((size_t)ci * Cd + co) * ku + r]; },
+            true, [&](int n) { return Bu[n % Cd]; }, blob, bias, f16w);
+      else
+        g = pack_group(
+            Cd, ku * Cu, [&](int n, int kx) { const int kk = kx / Cu, ci = kx - kk * Cu; return Wu[((size_t)ci * Cd + n) * ku + kk]; },
+            true, [&](int n) { return Bu[n]; }, blob, bias, f16w);
+      g.x_off = g.o_off = 0;
+      L.su_gm[b].groups = {g};
+    }
   }
   for (int i = 0; i < (int)m->dp.size(); ++i) {
     DpLayer& L = m->dp[i];
@@ -1918,6 +1993,10 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
   for (auto& L : m->lv) {
     int rc = upload_groups(L.gc_gm);
     if (!rc) rc = upload_groups(L.fu_gm);
+    for (int b = 0; b < 3 && !rc; ++b) {
+      if (L.sd_mm[b]) rc = upload_groups(L.sd_gm[b]);
+      if (!rc && L.su_mm[b]) rc = upload_groups(L.su_gm[b]);
+    }
     if (rc) return rc;
   }
   for (auto& L : m->dp)
@@ -2005,6 +2084,30 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     conv3_bytes = tok_gemm_bytes(a, gm, gx);
     return launch_tok_gemm(a, gx, st);
   };
+  // one SD / SU band conv (sub-range conv form, geometry from create): x [B][xq1][T][Cin] -> o [B][oq1][T][o_ld];
+  // adds its algorithmic flops / bytes to *fl / *by
+  auto band_gemm = [&](const Gemm& gm, const ConvGeo& geo, const float* xin, float* o, int o_ld, double* fl,
+                       double* by) {
+    TokGemmArgs a{};
+    a.x = xin;
+    a.x_ld = geo.Cin;
+    a.out = o;
+    a.o_ld = o_ld;
+    a.w = m->d_w;
+    a.bias = m->d_bias;
+    a.groups = gm.d_groups;
+    a.n_groups = 1;
+    a.M = B * geo.P1 * geo.P2;
+    a.act = TOK_ACT_NONE;
+    a.conv = 1;
+    a.geo = geo;
+    const int N = gm.groups[0].N;
+    a.bn64 = N <= 64 || N % 128 == 64;   // narrow bands: 64-column tiles
+    a.n_tiles_n = a.bn64 ? (N + 63) / 64 : gm.n_tiles_n;
+    *fl += 2.0 * a.M * N * gm.groups[0].K;
+    *by += tok_gemm_bytes(a, gm, gx);
+    return launch_tok_gemm(a, gx, st);
+  };
 
   // 1. STFT (scnet.py:335-348)
   float* spec = F32(pl.spec);
@@ -2029,7 +2132,16 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     // algorithmic bytes of the simt group: the level input read once and the band outputs written once, then
     // every ConvolutionModule layer reads and writes its rows once
     double by = 4.0 * B * T * ((double)L.Fin * L.Cin + (double)L.Fout * L.Cout);
-    for (int b = 0; b < 3; ++b) {
+    const bool sd_mfma = scn_band_mfma() && L.sd_mm[0] && L.sd_mm[1] && L.sd_mm[2];
+    if (sd_mfma) {  // the three bands on MFMA, profiled as their own record
+      double gfl = 0, gby = 0;
+      for (int b = 0; b < 3 && !rc; ++b) rc = band_gemm(L.sd_gm[b], L.sd_geo[b], cur, skip, L.Cout, &gfl, &gby);
+      if (rc) return rc;
+      profile_end(tok, st, SESA_KCLASS_TOKGEMM, gfl, gby);
+      tok = profile_begin(st);
+      by = 0;
+    }
+    for (int b = 0; b < 3 && !sd_mfma; ++b) {
       const BandConv& bc = L.sd[b];
       const int64_t total = (int64_t)B * bc.n_out * T * (L.Cout / 4);
       hipLaunchKernelGGL(scn_sdconv_kernel, blocks(total), dim3(kST), 0, st, cur, L.Fin, T, L.Cin, Wb + L.sd_w[b],
@@ -2297,6 +2409,17 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     fl = 2.0 * B * L.Fout * T * 2.0 * L.Cout * 2.0 * L.Cout * 9;
     by += 12.0 * B * L.Fout * T * L.Cout;
     }
+    if (scn_band_mfma() && L.su_mm[0] && L.su_mm[1] && L.su_mm[2]) {  // the band transposed convs on MFMA
+      if (!scn_conv3_mfma()) {
+        profile_end(tok, st, SESA_KCLASS_SIMT, fl, by - 4.0 * B * T * ((double)L.Fout * L.Cout + (double)L.Fin * L.Cdec));
+        tok = profile_begin(st);
+      }
+      double gfl = 0, gby = 0;
+      for (int b = 0; b < 3 && !rc; ++b) rc = band_gemm(L.su_gm[b], L.su_geo[b], Y, X, L.Cdec, &gfl, &gby);
+      if (rc) return rc;
+      profile_end(tok, st, SESA_KCLASS_TOKGEMM, gfl, gby);
+      continue;
+    }
     for (int b = 0; b < 3; ++b) {
       const BandConv& bc = L.su[b];
       const int64_t total = (int64_t)B * bc.n_out * T * (L.Cdec / 4);
@@ -2331,9 +2454,13 @@ extern "C" int sesa_scnet_destroy(sesa_scnet* m) {
       if (L.ih[l].d_groups) (void)hipFree(L.ih[l].d_groups);
       if (L.lin[l].d_groups) (void)hipFree(L.lin[l].d_groups);
     }
-  for (auto& L : m->lv)
+  for (auto& L : m->lv) {
     for (Gemm* g : {&L.gc_gm, &L.fu_gm})
       if (g->d_groups) (void)hipFree(g->d_groups);
+    for (int b = 0; b < 3; ++b)
+      for (Gemm* g : {&L.sd_gm[b], &L.su_gm[b]})
+        if (g->d_groups) (void)hipFree(g->d_groups);
+  }
   delete m;
   return SESA_OK;
 }

@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
       const int mm = rok[i] ? m : 0;
       const int i2 = mm % a.geo.P2, t = mm / a.geo.P2;
       const int i1 = t % a.geo.P1, b = t / a.geo.P1;
-      rb1[i] = b * a.geo.Q1;
+      rb1[i] = a.geo.xq1 ? b * a.geo.xq1 + a.geo.x_row0 : b * a.geo.Q1;
       ri1[i] = i1 * a.geo.s1;
       ri2[i] = i2 * a.geo.s2;
       rpos0[i] = (rb1[i] + ri1[i]) * a.geo.Q2 + ri2[i];   // input position of tap offset (0, 0)
@@ -364,15 +364,16 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
     __syncthreads();
   }
 
-  const bool tconv = CONV && a.geo.phases > 1;
+  // output rows through the table: transposed conv, or the sub-range form (phases == 1: n_ph = N, ph = 0)
+  const bool tconv = CONV && (a.geo.phases > 1 || a.geo.oq1 > 0);
   if constexpr (CONV) {
-    if (a.geo.phases > 1) {
+    if (tconv) {
       for (int r = tid; r < BM; r += NT) {
         const int m = min(m0 + r, a.M - 1);
         const int i2 = m % a.geo.P2, t = m / a.geo.P2;
         const int i1 = t % a.geo.P1, b = t / a.geo.P1;
         orow_i1[r] = i1 * a.geo.phases - a.geo.opad;
-        orow_base[r] = (b * a.geo.O1 + orow_i1[r]) * a.geo.P2 + i2;
+        orow_base[r] = ((a.geo.oq1 ? b * a.geo.oq1 + a.geo.o_row0 : b * a.geo.O1) + orow_i1[r]) * a.geo.P2 + i2;
       }
       __syncthreads();
     }
@@ -1696,6 +1697,11 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
                      a.x_ld % 4 == 0 && c.P1 > 0 && c.P2 > 0 && c.Q1 > 0 && c.Q2 > 0 && c.phases >= 1 && !a.rope &&
                      !a.rownorm && (int64_t)c.P1 * c.P2 > 0 && (c.phases == 1 || !a.glu),
                  SESA_ERR_INVALID, "tok_gemm conv: bad geometry");
+    SESA_REQUIRE((c.phases == 1 && c.oq1 == 0) || c.O1 > 0, SESA_ERR_INVALID, "tok_gemm conv: output rows need O1");
+    SESA_REQUIRE(c.xq1 == 0 || (c.x_row0 >= 0 && c.x_row0 + c.Q1 <= c.xq1), SESA_ERR_INVALID,
+                 "tok_gemm conv: input sub-range [%d, %d) outside %d rows", c.x_row0, c.x_row0 + c.Q1, c.xq1);
+    SESA_REQUIRE(c.oq1 == 0 || (c.o_row0 >= 0 && c.o_row0 + c.O1 <= c.oq1), SESA_ERR_INVALID,
+                 "tok_gemm conv: output sub-range [%d, %d) outside %d rows", c.o_row0, c.o_row0 + c.O1, c.oq1);
     SESA_REQUIRE(!a.a_hi, SESA_ERR_INVALID, "tok_gemm conv: pre-split A is for token rows");
     // SESA_HCONV_VARIANT=1: the double-buffered 512-thread 256 x 128 tile for the implicit-GEMM convs (A/B)
     static const int hv = getenv("SESA_HCONV_VARIANT") ? atoi(getenv("SESA_HCONV_VARIANT")) : 0;

@@ -31,13 +31,18 @@ struct TokGroup {
 // tap t reads input position (i1 s1 + d1[t], i2 s2 + d2[t]) (zero outside the grid: conv padding).
 // phases > 1: transposed-conv epilogue -- column n = r * (N / phases) + co is written to output row
 // (b O1 + i1 phases + r - opad) P2 + i2 when 0 <= i1 phases + r - opad < O1 (1-D along axis 1).
-constexpr int kMaxTaps = 9;
+// Sub-range form (SCNet's band convs, sesa_scnet.hip): xq1 > 0 -- the item's input grid is rows
+// [x_row0, x_row0 + Q1) of a larger per-item grid of xq1 rows (base (b xq1 + x_row0) instead of b Q1; validity
+// still against Q1); oq1 > 0 -- output row i1' (i1 itself, or the transposed row above) of item b lands at
+// (b oq1 + o_row0 + i1') P2 + i2 (validity against O1, = P1 when phases == 1).
+constexpr int kMaxTaps = 16;
 struct ConvGeo {
   int P1, P2, Q1, Q2, s1, s2;
   int Cin, n_taps;
   int d1[kMaxTaps], d2[kMaxTaps];
   const float* x2;            // nullable: A = x + x2 (same layout; the decoder's x + skip)
   int phases, O1, opad;
+  int xq1, x_row0, oq1, o_row0;
 };
 
 struct TokGemmArgs {
