@@ -857,9 +857,12 @@ def main():
             line["rehearsal"] = {
                 "world": pworld, "rank0_chunks": shard_ranges[0][0][1] - shard_ranges[0][0][0] if len(names) == 1
                 else [r[0][1] - r[0][0] for r in shard_ranges],
-                "note": f"value = track seconds / rank 0's wall time for its share (gather -> forwards -> local OLA -> "
-                        f"assemble + finalise, no collective): the compute ceiling of a {pworld}-GPU run, which "
-                        f"adds the RCCL gather of the other ranks' spans to rank 0"}
+                "note": (f"value = track seconds / rank 0's wall time for its share (its input span -> forwards -> local "
+                         f"OLA -> finalise of its own output range, no collective): the compute ceiling of a "
+                         f"{pworld}-GPU run, which adds one RCCL seam exchange with each neighbour" if owned else
+                         f"value = track seconds / rank 0's wall time for its share (gather -> forwards -> local OLA -> "
+                         f"assemble + finalise, no collective): the compute ceiling of a {pworld}-GPU run, which "
+                         f"adds the RCCL gather of the other ranks' spans to rank 0")}
         # north_star evidence: HBM GB/s of the streaming kernels (STFT / iSTFT / chunk gather + OLA),
         # algorithmic bytes / event-timed kernel time, against the 8 TB/s HBM3E peak
         hbm = {}

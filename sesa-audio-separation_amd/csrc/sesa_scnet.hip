@@ -221,6 +221,8 @@ struct CmArgs {
   const float* W3;         // [h][C]
   const float* b3;         // [C]
   int gelu;                // SDblock F.gelu after the module's last layer (:229-234)
+  const uint16_t* W1h;     // scn_cm_mfma_kernel: W1 as fp16 16x16x32 B fragments [3C / 32][h / 8][64][8]
+  const uint16_t* W3h;     //   and W3 as [hp / 32][C / 16][64][8] (hp = h rounded up to 32, zero rows past h)
 };
 
 __device__ __forceinline__ void block_sum2(double& s, double& ss, double* red) {
@@ -429,6 +431,231 @@ __global__ void __launch_bounds__(kST) scn_cm_out_kernel(CmArgs a) {
     float v = xr[i] + acc;
     if (a.gelu) v = gelu_erf(v);
     xr[i] = v;
+  }
+}
+
+// ---- ConvolutionModule layer on MFMA (fp16mix), one workgroup per (b, f) row: both convolutions of
+// scnet.py:35-43 as fp16 GEMMs (v_mfma_f32_16x16x32_f16, fp32 accumulation), the norms / GLU / depthwise / Swish /
+// residual in fp32 around them, in ONE launch per layer (scn_cm_in_rb_kernel + scn_cm_out_kernel are two, and spend
+// their time on LDS-bound VALU FMAs: 9-14 TF/s).
+//   A: GroupNorm(1, C) statistics of the row (fp64 sums, as scn_cm_in_kernel); W1's fragments into LDS.
+//   B: per slab of kCmTT positions, the normalised rows t0 - 1 .. t0 + kCmTT as fp16 in LDS (row stride C + 8).  The
+//      k3 conv is a GEMM whose A row t is the three input rows t - 1, t, t + 1 (k = dt C + c); each wave takes 16
+//      positions and every column tile.  Packed column tile i holds the GLU value columns 8i .. 8i + 7 (lanes 0-7)
+//      and their gates (lanes 8-15), so the GLU is a lane swap in the epilogue; U [T + 2][h] fp32 stays in LDS
+//      (zero end rows: the depthwise conv's padding).
+//   C: depthwise k3 + GroupNorm(1, h) statistics (fp64), then Swish of the normalised values as fp16 V [T16][h]
+//      into the dead phase-B region (zero rows past T; phase D zeroes the k past h).
+//   D: the 1x1 conv h -> C as a GEMM over V (K = hp), + b3 + the residual x (+ the SDblock gelu), stored in place
+//      (each element is read and written by the same lane).
+constexpr int kCmTT = 64;
+__host__ __device__ constexpr int cm_hp(int h) { return (h + 31) / 32 * 32; }
+struct CmMfmaLds {
+  int xs, w1, vh, w3, u, red, total;   // byte offsets of the regions, total bytes
+};
+__host__ __device__ inline CmMfmaLds cm_mfma_layout(int T, int C, int h) {
+  CmMfmaLds l{};
+  const int T16 = (T + 15) / 16 * 16, hp = cm_hp(h);
+  const int xs_b = (kCmTT + 2) * (C + 8) * 2, w1_b = 3 * C * 2 * h * 2;
+  const int vh_b = T16 * (h + 8) * 2, w3_b = hp * C * 2;
+  const int r1 = max(xs_b + w1_b, vh_b + w3_b);
+  l.xs = 0;
+  l.w1 = xs_b;
+  l.vh = 0;
+  l.w3 = vh_b;
+  l.u = (r1 + 15) / 16 * 16;
+  l.red = l.u + ((T + 2) * h * 4 + 15) / 16 * 16;
+  l.total = l.red + 16 * 8;
+  return l;
+}
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+
+template <int NT1>   // h / 8: column tiles of the k3 conv (GLU pairs)
+__global__ void __launch_bounds__(kST) scn_cm_mfma_kernel(CmArgs a) {
+  extern __shared__ __align__(16) char smc[];
+  const int C = a.C, h = a.h, T = a.T;
+  const int hp = cm_hp(h), T16 = (T + 15) / 16 * 16;
+  const CmMfmaLds L = cm_mfma_layout(T, C, h);
+  _Float16* xs = reinterpret_cast<_Float16*>(smc + L.xs);
+  const u32x4* w1s = reinterpret_cast<const u32x4*>(smc + L.w1);
+  _Float16* vh = reinterpret_cast<_Float16*>(smc + L.vh);
+  const u32x4* w3s = reinterpret_cast<const u32x4*>(smc + L.w3);
+  float* U = reinterpret_cast<float*>(smc + L.u);
+  double* red = reinterpret_cast<double*>(smc + L.red);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int row = blockIdx.x;
+  const int64_t b = row / a.n_f;
+  const int f = a.f_off + row % a.n_f;
+  float* xr = a.X + ((b * a.F_all + f) * T) * C;
+  const f32x4* xr4 = reinterpret_cast<const f32x4*>(xr);
+  const int SX = C + 8, SV = h + 8, C4 = C / 4;   // (h % 8 == 0: 16-B aligned V rows)
+  const int K1 = 3 * C;
+
+  // ---- A: GroupNorm(1, C) statistics; W1 fragments -> LDS; U's zero end rows ----
+  {
+    u32x4* d = reinterpret_cast<u32x4*>(smc + L.w1);
+    const u32x4* s = reinterpret_cast<const u32x4*>(a.W1h);
+    for (int i = tid; i < K1 * 2 * h / 8; i += kST) d[i] = s[i];
+    for (int i = tid; i < h; i += kST) {
+      U[i] = 0.f;
+      U[(T + 1) * h + i] = 0.f;
+    }
+  }
+  double s = 0, ss = 0;
+#pragma unroll 4
+  for (int i = tid; i < T * C4; i += kST) {
+    const f32x4 v = xr4[i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s += v[q];
+      ss += (double)v[q] * v[q];
+    }
+  }
+  block_sum2(s, ss, red);
+  float mean, rstd;
+  {
+    const double n = (double)T * C;
+    const double mu = s / n;
+    const double var = fmax(ss / n - mu * mu, 0.0);
+    mean = (float)mu;
+    rstd = (float)(1.0 / sqrt(var + 1e-5));
+  }
+  // this thread's channel quad when staging (kST % C4 == 0: host check)
+  const int cq = tid % C4, c0 = cq * 4;
+  float gs[4], gb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    gs[q] = rstd * a.g1[c0 + q];
+    gb[q] = a.be1[c0 + q];
+  }
+  // this lane's packed k3-conv columns: bias of the value column and of its gate
+  const int col = lane & 15;
+  float bias1[NT1];
+#pragma unroll
+  for (int nt = 0; nt < NT1; ++nt) bias1[nt] = a.b1[col < 8 ? 8 * nt + col : h + 8 * nt + col - 8];
+
+  // ---- B: k3 conv C -> 2h + GLU, slab by slab ----
+  for (int t0 = 0; t0 < T; t0 += kCmTT) {
+    __syncthreads();   // (the previous slab's fragment reads are done; first slab: W1 and the stats are in place)
+    for (int i = tid; i < (kCmTT + 2) * C4; i += kST) {
+      const int rl = i / C4;
+      const int t = t0 - 1 + rl;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (t >= 0 && t < T) {
+        v = xr4[(int64_t)t * C4 + cq];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = (v[q] - mean) * gs[q] + gb[q];
+      }
+      h16x4 hv;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hv[q] = (_Float16)v[q];
+      *reinterpret_cast<h16x4*>(xs + rl * SX + c0) = hv;
+    }
+    __syncthreads();
+    const int tl0 = 16 * w;
+    if (t0 + tl0 < T) {   // (wave-uniform)
+      f32x4 acc[NT1];
+#pragma unroll
+      for (int nt = 0; nt < NT1; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int arow = tl0 + (lane & 15);
+      for (int ks = 0; ks < K1 / 32; ++ks) {
+        const int kb = 32 * ks + 8 * (lane >> 4);
+        const int dt = kb / C, c = kb - dt * C;   // (C % 32 == 0: a lane's 8 k lie in one tap)
+        const h16x8 av = *reinterpret_cast<const h16x8*>(xs + (arow + dt) * SX + c);
+#pragma unroll
+        for (int nt = 0; nt < NT1; ++nt) {
+          const h16x8 bv = __builtin_bit_cast(h16x8, w1s[(ks * NT1 + nt) * 64 + lane]);
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc[nt], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT1; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[nt][r] + bias1[nt];
+          const float g = __shfl_xor(v, 8);
+          const int t = t0 + tl0 + (lane >> 4) * 4 + r;
+          if (col < 8 && t < T) U[(t + 1) * h + 8 * nt + col] = v * sigm(g);
+        }
+    }
+  }
+  __syncthreads();   // U complete; the slab buffer and W1 are dead
+
+  // ---- C: depthwise k3 + GroupNorm(1, h) statistics, then Swish(norm) as fp16 V; W3 fragments -> LDS ----
+  {
+    u32x4* d = reinterpret_cast<u32x4*>(smc + L.w3);
+    const u32x4* s3 = reinterpret_cast<const u32x4*>(a.W3h);
+    for (int i = tid; i < hp * C / 8; i += kST) d[i] = s3[i];
+  }
+  const int j = tid % h;              // (kST % h == 0: host check) this thread's hidden unit
+  const float wd0 = a.wdw[3 * j], wd1 = a.wdw[3 * j + 1], wd2 = a.wdw[3 * j + 2], bd = a.bdw[j];
+  s = 0;
+  ss = 0;
+  for (int t = tid / h; t < T; t += kST / h) {
+    float v = bd;
+    v = fmaf(wd0, U[t * h + j], v);
+    v = fmaf(wd1, U[(t + 1) * h + j], v);
+    v = fmaf(wd2, U[(t + 2) * h + j], v);
+    s += v;
+    ss += (double)v * v;
+  }
+  block_sum2(s, ss, red);
+  {
+    const double n = (double)T * h;
+    const double mu = s / n;
+    const double var = fmax(ss / n - mu * mu, 0.0);
+    mean = (float)mu;
+    rstd = (float)(1.0 / sqrt(var + 1e-5));
+  }
+  const float g2 = rstd * a.g2[j], be2 = a.be2[j];
+  for (int t = tid / h; t < T16; t += kST / h) {
+    float o = 0.f;
+    if (t < T) {
+      float v = bd;
+      v = fmaf(wd0, U[t * h + j], v);
+      v = fmaf(wd1, U[(t + 1) * h + j], v);
+      v = fmaf(wd2, U[(t + 2) * h + j], v);
+      v = (v - mean) * g2 + be2;
+      o = v * sigm(v);
+    }
+    vh[t * SV + j] = (_Float16)o;
+  }
+  __syncthreads();
+
+  // ---- D: 1x1 conv h -> C + b3 + residual (+ gelu), in place ----
+  const int KS2 = hp / 32, NT2 = C / 16;
+  for (int mt = w; mt < T16 / 16; mt += kST / 64) {
+    h16x8 av[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      if (ks < KS2) {   // k past h: zero (V holds h columns; W3's rows past h are zero too)
+        const int kb = 32 * ks + 8 * (lane >> 4);
+        av[ks] = kb < h ? *reinterpret_cast<const h16x8*>(vh + (16 * mt + (lane & 15)) * SV + kb) : h16x8{};
+      }
+    for (int nt = 0; nt < NT2; ++nt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        if (ks < KS2)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[ks], __builtin_bit_cast(h16x8, w3s[(ks * NT2 + nt) * 64 + lane]),
+                                                       acc, 0, 0, 0);
+      const int c = 16 * nt + col;
+      const float bias = a.b3[c];
+      float res[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * mt + (lane >> 4) * 4 + r;
+        res[r] = t < T ? xr[(int64_t)t * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * mt + (lane >> 4) * 4 + r;
+        float v = res[r] + (acc[r] + bias);
+        if (a.gelu) v = gelu_erf(v);
+        if (t < T) xr[(int64_t)t * C + c] = v;
+      }
+    }
   }
 }
 
@@ -1340,6 +1567,7 @@ struct Param {
 
 struct CmLayer {  // float offsets into the packed fp32 blob
   int64_t g1, be1, w1, b1, wdw, bdw, g2, be2, w3, b3;
+  int64_t w1h = -1, w3h = -1;   // uint16 offsets of scn_cm_mfma_kernel's fp16 fragments in the d_w blob (-1: none)
 };
 
 struct Level {
@@ -1432,6 +1660,29 @@ bool scn_conv3_mfma() {
 bool scn_band_mfma() {
   static const bool v = !(getenv("SESA_SCN_BAND_VALU") && std::string(getenv("SESA_SCN_BAND_VALU")) == "1");
   return v;
+}
+
+// the fused MFMA ConvolutionModule layer (scn_cm_mfma_kernel) takes this geometry; SESA_SCN_CM_VALU=1: the VALU
+// kernels in fp16mix too (A/B runs)
+bool scn_cm_mfma_ok(int T, int C, int h) {
+  return C % 32 == 0 && h % 8 == 0 && h <= 64 && kST % (C / 4) == 0 && kST % h == 0 &&
+         cm_mfma_layout(T, C, h).total <= 160 * 1024;
+}
+bool scn_cm_mfma_env() {
+  static const bool v = !(getenv("SESA_SCN_CM_VALU") && std::string(getenv("SESA_SCN_CM_VALU")) == "1");
+  return v;
+}
+int launch_cm_mfma(const CmArgs& a, int rows, hipStream_t st) {
+  const size_t lds = cm_mfma_layout(a.T, a.C, a.h).total;
+  switch (a.h / 8) {
+    case 1: hipLaunchKernelGGL(scn_cm_mfma_kernel<1>, dim3(rows), dim3(kST), lds, st, a); break;
+    case 2: hipLaunchKernelGGL(scn_cm_mfma_kernel<2>, dim3(rows), dim3(kST), lds, st, a); break;
+    case 4: hipLaunchKernelGGL(scn_cm_mfma_kernel<4>, dim3(rows), dim3(kST), lds, st, a); break;
+    case 8: hipLaunchKernelGGL(scn_cm_mfma_kernel<8>, dim3(rows), dim3(kST), lds, st, a); break;
+    default: SESA_REQUIRE(false, SESA_ERR_INVALID, "scnet: ConvolutionModule MFMA hidden size %d", a.h);
+  }
+  SESA_CHECK_LAUNCH();
+  return SESA_OK;
 }
 
 bool scn_dft_mfma() {
@@ -1860,6 +2111,38 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
       g.x_off = g.o_off = 0;
       L.su_gm[b].groups = {g};
     }
+    // ConvolutionModule layers as fp16 MFMA fragments (scn_cm_mfma_kernel): W1 [2h][C][3] -> [3C / 32][h / 8][64][8]
+    // with k = dt C + c and column tile nt = value columns 8 nt .. 8 nt + 7, then their gates; W3 [C][h][1] ->
+    // [hp / 32][C / 16][64][8], zero past h
+    if (f16w && scn_cm_mfma_ok(m->T, L.Cout, L.h)) {
+      const int h = L.h, NT1 = h / 8, hp = cm_hp(h);
+      auto f16 = [](float v) { return __builtin_bit_cast(uint16_t, (_Float16)v); };
+      for (int b = 0; b < 3; ++b)
+        for (size_t l = 0; l < L.cm[b].size(); ++l) {
+          const std::string q = "encoder." + S(i) + ".conv_modules." + S(b) + ".layers." + S((int)l);
+          const auto& W1 = P(m, q + ".1.weight");
+          const auto& W3 = P(m, q + ".6.weight");
+          while (blob.size() % 8) blob.push_back(0);
+          CmLayer& cl = L.cm[b][l];
+          cl.w1h = (int64_t)blob.size();
+          for (int ks = 0; ks < 3 * C / 32; ++ks)
+            for (int nt = 0; nt < NT1; ++nt)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int k = 32 * ks + 8 * (ln >> 4) + e, dt = k / C, c = k - dt * C, qc = ln & 15;
+                  const int o = qc < 8 ? 8 * nt + qc : h + 8 * nt + qc - 8;
+                  blob.push_back(f16(W1[((size_t)o * C + c) * 3 + dt]));
+                }
+          cl.w3h = (int64_t)blob.size();
+          for (int ks = 0; ks < hp / 32; ++ks)
+            for (int nt = 0; nt < C / 16; ++nt)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int k = 32 * ks + 8 * (ln >> 4) + e, n = 16 * nt + (ln & 15);
+                  blob.push_back(k < h ? f16(W3[(size_t)n * h + k]) : 0);
+                }
+        }
+    }
   }
   for (int i = 0; i < (int)m->dp.size(); ++i) {
     DpLayer& L = m->dp[i];
@@ -2019,6 +2302,9 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
                                      160 * 1024));
   SESA_CHECK_HIP(hipFuncSetAttribute((const void*)scn_dft_mfma_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024));
+  for (const void* k : {(const void*)scn_cm_mfma_kernel<1>, (const void*)scn_cm_mfma_kernel<2>,
+                        (const void*)scn_cm_mfma_kernel<4>, (const void*)scn_cm_mfma_kernel<8>})
+    SESA_CHECK_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   m->finalized = true;
   return SESA_OK;
 }
@@ -2180,7 +2466,12 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         a.W3 = Wb + cl.w3;
         a.b3 = Wb + cl.b3;
         a.gelu = l + 1 == L.cm[b].size();
-        if (L.cm_gen) {
+        if (cl.w1h >= 0 && scn_cm_mfma_env()) {
+          a.W1h = m->d_w + cl.w1h;
+          a.W3h = m->d_w + cl.w3h;
+          rc = launch_cm_mfma(a, rows, st);
+          if (rc) return rc;
+        } else if (L.cm_gen) {
           hipLaunchKernelGGL(scn_cm_in_gen_kernel, dim3(rows), dim3(kST), cm_in_gen_lds(L.h), st, a);
           SESA_CHECK_LAUNCH();
           hipLaunchKernelGGL(scn_cm_out_gen_kernel, dim3(rows), dim3(kST), cm_out_gen_lds(L.Cout, L.h), st, a);
