@@ -85,14 +85,16 @@ FP32_VECTOR_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table (fp32 vector)
 KDESC = {"conv3x3": "conv3x3_db_kernel (TFC conv3x3, implicit GEMM, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "tokgemm": "tok_gemm_glds_kernel + tok_gemm_kernel (token-major Linear layers, bf16x3 "
                     "v_mfma_f32_32x32x16_bf16 / v_mfma_f32_16x16x32_bf16)",
-         "lstm": "scn_lstm_mfma_kernel (bi-LSTM recurrence, bf16x3 v_mfma_f32_32x32x16_bf16)",
+         "lstm": "scn_lstm_mfma_kernel / _wide_kernel (bi-LSTM recurrence: v_mfma_f32_32x32x16_f16, one fp16 pass in "
+                 "SCNet fp16mix; bf16x3 v_mfma_f32_32x32x16_bf16 otherwise)",
          "dft": "scn_dft_mfma_kernel (SCNet feature conversion: rfft / irfft over T as a GEMM against the packed "
                 "DFT matrix, bf16x3 v_mfma_f32_32x32x16_bf16)",
          "hconv": "tok_gemm_kernel<conv> (HTDemucs implicit-GEMM convolutions, v_mfma_f32_32x32x16_bf16)",
          "attn": "attn_kernel (flash attention, S^T = K Q^T, bf16x3 v_mfma_f32_32x32x16_bf16)",
-         "simt": "fp32 VALU kernels (SCNet: scn_cm_in / scn_cm_out ConvolutionModule, scn_sdconv / scn_convtr band "
-                 "convs; HTDemucs: htd_dc_conv_valu / htd_dc_gram / htd_dc_apply "
-                 "DConv, norms)"}
+         "simt": "norm / elementwise kernels priced at the fp32 VALU peak (SCNet: the ConvolutionModule layers -- "
+                 "scn_cm_mfma_kernel in fp16mix, fp16 MFMA convs inside fp32 norms, else the VALU scn_cm_in / "
+                 "scn_cm_out --, the dual-path GroupNorms, FeatureConversion fallbacks, the VALU band-conv fallback; "
+                 "HTDemucs: htd_dc_conv_valu / htd_dc_gram / htd_dc_apply DConv, norms)"}
 
 
 def kdesc(kclass, precision, model):
@@ -197,7 +199,8 @@ def class_precision(kclass, precision, model="mdx23c", members=None):
     with (default: member_precision).  MDX23C classes follow MDX23C's mode; token GEMMs run one fp16 pass for a
     BS-Roformer fp16, SCNet fp16mix or HTDemucs fp16mix member (HTDemucs: unless SESA_HTD_PRESPLIT=0 keeps its
     Linears bf16x3), else that member's mode (bf16 / bf16x3); attention fp16 for BS-Roformer fp16 / HTDemucs
-    fp16mix; HTDemucs' implicit-GEMM convs fp16 in fp16mix; the LSTM recurrence bf16x3 (bf16 in the bf16 mode);
+    fp16mix; HTDemucs' implicit-GEMM convs fp16 in fp16mix; the LSTM recurrence one fp16 pass in SCNet fp16mix
+    (SESA_SCN_LSTM_PASSES), bf16 in the bf16 mode, else bf16x3;
     SCNet's feature-conversion DFTs bf16x3; simt is fp32 VALU."""
     if members is None:
         names = ("mdx23c", "bs_roformer", "scnet") if model == "ensemble" else (model,)
@@ -222,7 +225,10 @@ def class_precision(kclass, precision, model="mdx23c", members=None):
     if kclass == "simt":
         return "fp32"
     if kclass == "lstm":
-        return "bf16" if members.get("scnet") == "bf16" else "bf16x3"
+        p = members.get("scnet")
+        if p == "fp16mix":   # the fp16mix recurrence (H <= 256): SESA_SCN_LSTM_PASSES 1 (default) / 2 / 3
+            return {"2": "fp16w2", "3": "bf16x3"}.get(os.environ.get("SESA_SCN_LSTM_PASSES", "1"), "fp16")
+        return "bf16" if p == "bf16" else "bf16x3"
     if kclass == "dft":
         return "bf16x3"
     f16 = {"bs_roformer": "fp16", "scnet": "fp16mix", "htdemucs": "fp16mix"}

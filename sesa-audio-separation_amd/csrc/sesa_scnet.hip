@@ -94,17 +94,25 @@ __global__ void __launch_bounds__(kST) scn_stft_kernel(const float* __restrict__
   }
 }
 
-// spec [B][F0][T][2*nsig] -> frames [B*nsig][T][4096] (c2r with scale, window = ones; scnet.py:364-368)
+// spec -> frames [B*nsig][T][4096] (c2r with scale, window = ones; scnet.py:364-368).  spec is frame-major
+// [B][T][F0][2 nsig] (fmajor: the MFMA band convs' output) or band-major [B][F0][T][2 nsig] (the VALU fallback).
+// One workgroup per (item, frame, signal), signals fastest and the workgroups of one frame on one XCD (blockIdx
+// remapped like tok_gemm's xcd_tile): a frame's signals share its 64-B bin lines in that XCD's L2.
 __global__ void __launch_bounds__(kST) scn_istft_frames_kernel(const float* __restrict__ spec, int nsig, int T,
-                                                               float scale, ScnTables tb, float* __restrict__ fw) {
+                                                               int fmajor, float scale, ScnTables tb,
+                                                               float* __restrict__ fw) {
   __shared__ float2 bufA[kSH];
   __shared__ float2 bufB[kSH + 1];
-  const int t = blockIdx.x;
-  const int sg = blockIdx.y;
-  const int b = sg / nsig, m = sg - b * nsig;
+  const int nb = gridDim.x, q8 = nb >> 3, r8 = nb & 7, x8 = blockIdx.x & 7;
+  const int id = x8 * q8 + min(x8, r8) + (blockIdx.x >> 3);
+  const int m = id % nsig, bt = id / nsig;
+  const int b = bt / T, t = bt - b * T;
+  const int sg = b * nsig + m;
   const int C = 2 * nsig;
+  const int64_t ks = fmajor ? C : (int64_t)T * C;
+  const float* sp = spec + (int64_t)b * (kSH + 1) * T * C + (fmajor ? (int64_t)t * (kSH + 1) * C : (int64_t)t * C) + 2 * m;
   for (int k = threadIdx.x; k <= kSH; k += kST) {
-    float2 X = *reinterpret_cast<const float2*>(spec + (((int64_t)b * (kSH + 1) + k) * T + t) * C + 2 * m);
+    float2 X = *reinterpret_cast<const float2*>(sp + k * ks);
     if (k == 0 || k == kSH) X.y = 0.f;  // C2R ignores the imaginary parts of DC and Nyquist
     bufB[k] = X;
   }
@@ -1034,8 +1042,39 @@ __device__ __forceinline__ float tanh_f(float v) {
 __device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x16 mfma_f16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b), c, 0, 0, 0);
+}
+// PS: MFMA passes of the recurrence product.  3: h and W_hh as bf16 hi + lo, three bf16 products (bf16x3).
+// 2: h as one fp16 plane x W_hh as fp16 hi + lo (two fp16 products).  1: fp16 h x fp16 W_hh.  PS < 3 reads the
+// fp16 fragment image (same layout, fp16 values) and keeps only the hi plane of h in LDS.
+template <int PS>
+__device__ __forceinline__ void lstm_mfma_step(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
+                                               f32x16& acc) {
+  if constexpr (PS == 3) {
+    acc = mfma_bf16(al, bh, acc);
+    acc = mfma_bf16(ah, bl, acc);
+    acc = mfma_bf16(ah, bh, acc);
+  } else if constexpr (PS == 2) {
+    acc = mfma_f16(ah, bl, acc);
+    acc = mfma_f16(ah, bh, acc);
+  } else {
+    acc = mfma_f16(ah, bh, acc);
+  }
+}
+template <int PS>
+__device__ __forceinline__ void lstm_store_h(float hv, uint16_t* hi, uint16_t* lo) {
+  if constexpr (PS == 3) {
+    __bf16 h, l;
+    split_bf16(hv, h, l);
+    *hi = __builtin_bit_cast(uint16_t, h);
+    *lo = __builtin_bit_cast(uint16_t, l);
+  } else {
+    *hi = __builtin_bit_cast(uint16_t, (_Float16)hv);
+  }
+}
 
-template <int NW, int PF>
+template <int NW, int PF, int PS = 3>
 __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, const uint16_t* __restrict__ Wf) {
   constexpr int H = 32 * NW, H4 = 4 * H, KS = H / 16, RS = H + 8;
   extern __shared__ __align__(16) uint16_t lsa[];
@@ -1088,25 +1127,22 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, cons
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         bh[p][q] = wb[((p * 4 + q) * 2 + 0) * 64];
-        bl[p][q] = wb[((p * 4 + q) * 2 + 1) * 64];
+        if constexpr (PS >= 2) bl[p][q] = wb[((p * 4 + q) * 2 + 1) * 64];
       }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int slot = ks % PF;
       const int ao = l32 * RS + 16 * ks + 8 * hh;
       const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ahi + ao);
-      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Alo + ao);
+      bf16x8 al{};
+      if constexpr (PS == 3) al = *reinterpret_cast<const bf16x8*>(Alo + ao);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc[q] = mfma_bf16(al, bh[slot][q], acc[q]);
-        acc[q] = mfma_bf16(ah, bl[slot][q], acc[q]);
-        acc[q] = mfma_bf16(ah, bh[slot][q], acc[q]);
-      }
+      for (int q = 0; q < 4; ++q) lstm_mfma_step<PS>(ah, al, bh[slot][q], bl[slot][q], acc[q]);
       if (ks + PF < KS) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           bh[slot][q] = wb[(((ks + PF) * 4 + q) * 2 + 0) * 64];
-          bl[slot][q] = wb[(((ks + PF) * 4 + q) * 2 + 1) * 64];
+          if constexpr (PS >= 2) bl[slot][q] = wb[(((ks + PF) * 4 + q) * 2 + 1) * 64];
         }
       }
       if constexpr (STREAM) asm volatile("" ::: "memory");  // keep the prefetch depth at PF k-steps
@@ -1120,10 +1156,7 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, cons
       const float gg = tanh_f(acc[2][r] + gv[2][r]), og = sigm_f(acc[3][r] + gv[3][r]);
       c[r] = fg * c[r] + ig * gg;
       const float hv = og * tanh_f(c[r]);
-      __bf16 hi, lo;
-      split_bf16(hv, hi, lo);
-      Ahi[sl * RS + j] = __builtin_bit_cast(uint16_t, hi);
-      Alo[sl * RS + j] = __builtin_bit_cast(uint16_t, lo);
+      lstm_store_h<PS>(hv, Ahi + sl * RS + j, Alo + sl * RS + j);
       const int64_t rb = rowb[sl];
       if (rb >= 0) a.HO[(rb + (int64_t)pos * a.pstride) * a.ho_ld + dir * H + j] = hv;
     }
@@ -1137,7 +1170,7 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, cons
 // input-projection gates (no separate gate registers) and streaming W_hh's B fragments through a
 // one-k-step ring (4 gates x hi / lo = 32 registers): gate q of k-step ks + 1 is requested as soon as
 // gate q of k-step ks has been consumed.
-template <int NW>
+template <int NW, int PS = 3>
 __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_wide_kernel(LstmArgs a, const uint16_t* __restrict__ Wf) {
   constexpr int H = 32 * NW, H4 = 4 * H, KS = H / 16, RS = H + 8;
   extern __shared__ __align__(16) uint16_t lsa[];
@@ -1175,21 +1208,20 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_wide_kernel(LstmArgs a,
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       bh[q] = wb[(q * 2 + 0) * 64];
-      bl[q] = wb[(q * 2 + 1) * 64];
+      if constexpr (PS >= 2) bl[q] = wb[(q * 2 + 1) * 64];
     }
 #pragma unroll 1
     for (int ks = 0; ks < KS; ++ks) {
       const int ao = l32 * RS + 16 * ks + 8 * hh;
       const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ahi + ao);
-      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Alo + ao);
+      bf16x8 al{};
+      if constexpr (PS == 3) al = *reinterpret_cast<const bf16x8*>(Alo + ao);
       const int kn = ks + 1 < KS ? ks + 1 : ks;  // (the last k-step re-reads its own fragments: harmless)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        acc[q] = mfma_bf16(al, bh[q], acc[q]);
-        acc[q] = mfma_bf16(ah, bl[q], acc[q]);
-        acc[q] = mfma_bf16(ah, bh[q], acc[q]);
+        lstm_mfma_step<PS>(ah, al, bh[q], bl[q], acc[q]);
         bh[q] = wb[((kn * 4 + q) * 2 + 0) * 64];
-        bl[q] = wb[((kn * 4 + q) * 2 + 1) * 64];
+        if constexpr (PS >= 2) bl[q] = wb[((kn * 4 + q) * 2 + 1) * 64];
       }
     }
     __syncthreads();  // every wave has read h_{t-1}
@@ -1200,10 +1232,7 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_wide_kernel(LstmArgs a,
       const float gg = tanh_f(acc[2][r]), og = sigm_f(acc[3][r]);
       c[r] = fg * c[r] + ig * gg;
       const float hv = og * tanh_f(c[r]);
-      __bf16 hi, lo;
-      split_bf16(hv, hi, lo);
-      Ahi[sl * RS + j] = __builtin_bit_cast(uint16_t, hi);
-      Alo[sl * RS + j] = __builtin_bit_cast(uint16_t, lo);
+      lstm_store_h<PS>(hv, Ahi + sl * RS + j, Alo + sl * RS + j);
       const int64_t rb = rowb[sl];
       if (rb >= 0) a.HO[(rb + (int64_t)pos * a.pstride) * a.ho_ld + dir * H + j] = hv;
     }
@@ -1222,18 +1251,33 @@ int lstm_wide_min_nw() {
 
 size_t lstm_mfma_lds(int H) { return (size_t)64 * (H + 8) * 2 + 32 * 8; }
 
-template <int NW>
+template <int NW, int PS = 3>
 void launch_lstm_mfma_t(const LstmArgs& a, const uint16_t* Wf, hipStream_t st) {
   constexpr int PF = 2;
   const size_t lds = lstm_mfma_lds(32 * NW);
   dim3 grid((unsigned)((a.n_seq + 31) / 32), 2);
   if constexpr (NW <= 8) {
     if (NW < lstm_wide_min_nw()) {
-      hipLaunchKernelGGL((scn_lstm_mfma_kernel<NW, PF>), grid, dim3(64 * NW), lds, st, a, Wf);
+      hipLaunchKernelGGL((scn_lstm_mfma_kernel<NW, PF, PS>), grid, dim3(64 * NW), lds, st, a, Wf);
       return;
     }
   }
-  hipLaunchKernelGGL((scn_lstm_mfma_wide_kernel<NW>), grid, dim3(64 * NW), lds, st, a, Wf);
+  hipLaunchKernelGGL((scn_lstm_mfma_wide_kernel<NW, PS>), grid, dim3(64 * NW), lds, st, a, Wf);
+}
+// the fp16 recurrence forms (PS 1 / 2) exist for H <= 256 (the musdb18 / base widths); wider layers run bf16x3
+template <int PS>
+bool launch_lstm_mfma_f16(const LstmArgs& a, const uint16_t* Wf, hipStream_t st) {
+  switch (a.H / 32) {
+    case 1: launch_lstm_mfma_t<1, PS>(a, Wf, st); return true;
+    case 2: launch_lstm_mfma_t<2, PS>(a, Wf, st); return true;
+    case 3: launch_lstm_mfma_t<3, PS>(a, Wf, st); return true;
+    case 4: launch_lstm_mfma_t<4, PS>(a, Wf, st); return true;
+    case 5: launch_lstm_mfma_t<5, PS>(a, Wf, st); return true;
+    case 6: launch_lstm_mfma_t<6, PS>(a, Wf, st); return true;
+    case 7: launch_lstm_mfma_t<7, PS>(a, Wf, st); return true;
+    case 8: launch_lstm_mfma_t<8, PS>(a, Wf, st); return true;
+    default: return false;
+  }
 }
 
 // Raise the dynamic-LDS limit of the wide recurrence instances (> 64 KiB at H = 512); finalize time.
@@ -1251,7 +1295,10 @@ int lstm_mfma_prepare(int H) {
   return SESA_OK;
 }
 
-void launch_lstm_mfma(const LstmArgs& a, const uint16_t* Wf, hipStream_t st) {
+// ps: 3 bf16x3 (Wf = the bf16 hi / lo image); 2 / 1: the fp16 forms (Wf = the fp16 hi / lo image), H <= 256
+void launch_lstm_mfma(const LstmArgs& a, const uint16_t* Wf, int ps, hipStream_t st) {
+  if (ps == 2 && launch_lstm_mfma_f16<2>(a, Wf, st)) return;
+  if (ps == 1 && launch_lstm_mfma_f16<1>(a, Wf, st)) return;
   switch (a.H / 32) {
     case 1: launch_lstm_mfma_t<1>(a, Wf, st); break;
     case 2: launch_lstm_mfma_t<2>(a, Wf, st); break;
@@ -1589,6 +1636,7 @@ struct DpLayer {
   Gemm ih[2], lin[2];
   int64_t whh[2], gn_g[2], gn_b[2];
   int64_t whh_frag[2];  // uint16 offset of the MFMA B fragments (d_w blob)
+  int64_t whh_frag16[2] = {-1, -1};  // the same as fp16 hi / lo (fp16mix, H <= 256: the PS < 3 recurrences)
 };
 
 }  // namespace
@@ -1683,6 +1731,18 @@ int launch_cm_mfma(const CmArgs& a, int rows, hipStream_t st) {
   }
   SESA_CHECK_LAUNCH();
   return SESA_OK;
+}
+
+// fp16mix LSTM recurrence passes (lstm_mfma_step): SESA_SCN_LSTM_PASSES = 1 (default: fp16 h x fp16 W_hh) | 2 | 3
+// (bf16x3).  Same box, musdb18 4-min track: lstm class 121.6 / 114.6 / 59.6 ms per step at 3 / 2 / 1 passes, the
+// full-chunk fixture's rms 1.6558e-5 / 1.6560e-5 / 1.6556e-5 (profiles/r06_scnet_lstm_ps*.json): the wide kernel
+// streams W_hh's fragments from L2 every step, and one pass reads half of them (the hi image only)
+int scn_lstm_passes() {
+  static const int v = [] {
+    const int p = getenv("SESA_SCN_LSTM_PASSES") ? atoi(getenv("SESA_SCN_LSTM_PASSES")) : 1;
+    return p == 1 || p == 2 ? p : 3;
+  }();
+  return v;
 }
 
 bool scn_dft_mfma() {
@@ -1845,6 +1905,7 @@ extern "C" int sesa_scnet_create(const sesa_scnet_config* cfg, sesa_scnet** out)
       u.Cin = L.Cout;
       u.O1 = su.n_out;
       u.xq1 = L.Fout; u.x_row0 = su.in_off; u.oq1 = L.Fin; u.o_row0 = su.out_off;
+      u.o_fmajor = i == 0;   // the last decoder layer writes the iSTFT's frame-major spectrum [B][T][F0][2 nsig]
       if (su.kern == su.stride) {  // input row fi -> output rows fi s + r - dist, r < s: one tap, s phases
         u.P1 = su.n_in;
         u.n_taps = 1;
@@ -2197,6 +2258,27 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
                   }
         }
       }
+      if (f16w && H <= 256) {  // the same fragments as fp16 hi / lo (lstm_mfma_step PS 1 / 2)
+        const int NW = H / 32, KS = H / 16;
+        while (blob.size() % 8) blob.push_back(0);
+        L.whh_frag16[l] = (int64_t)blob.size();
+        blob.resize(blob.size() + (size_t)2 * NW * KS * 4 * 2 * 64 * 8, 0);
+        uint16_t* f = blob.data() + L.whh_frag16[l];
+        for (int dir = 0; dir < 2; ++dir) {
+          const auto& Wh = P(m, q + (dir ? ".weight_hh_l0_reverse" : ".weight_hh_l0"));
+          for (int w = 0; w < NW; ++w)
+            for (int ks = 0; ks < KS; ++ks)
+              for (int g4 = 0; g4 < 4; ++g4)
+                for (int ln = 0; ln < 64; ++ln)
+                  for (int e = 0; e < 8; ++e) {
+                    const float v = Wh[(size_t)(g4 * H + 32 * w + (ln & 31)) * H + 16 * ks + 8 * (ln >> 5) + e];
+                    const _Float16 hh = (_Float16)v;
+                    const size_t base = ((((((size_t)dir * NW + w) * KS + ks) * 4 + g4) * 2) * 64 + ln) * 8 + e;
+                    f[base] = __builtin_bit_cast(uint16_t, hh);
+                    f[base + 64 * 8] = __builtin_bit_cast(uint16_t, (_Float16)(v - (float)hh));
+                  }
+        }
+      }
       L.gn_g[l] = putp(p + ".norm_layers." + S(l) + ".weight");
       L.gn_b[l] = putp(p + ".norm_layers." + S(l) + ".bias");
     }
@@ -2329,7 +2411,8 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
   const float* Wb = m->d_f32;
   const int T = m->T, K = m->K, F0 = m->F0, ach = c.audio_channels;
   const bool f16mix = c.precision == SESA_PREC_F16MIX;
-  const int x3 = c.precision == SESA_PREC_BF16X3 || f16mix ? 1 : 0;   // the LSTM recurrence: bf16x3 in fp16mix
+  // the VALU-recurrence fallback's / DFTs' passes: bf16x3 in fp16mix (the MFMA recurrence: scn_lstm_passes())
+  const int x3 = c.precision == SESA_PREC_BF16X3 || f16mix ? 1 : 0;
   const int gx = f16mix ? 2 : x3;   // token GEMMs (3x3 convs, input projections, Linears): fp16 single pass
   ScnTables tb;
   int rc = get_tables(&tb);
@@ -2588,7 +2671,10 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
           a.pstride = 1;
         }
         void* t0 = profile_begin(st);
-        if (lstm_mfma_on(H)) launch_lstm_mfma(a, m->d_w + L.whh_frag[path], st);
+        if (lstm_mfma_on(H)) {
+          const int ps = L.whh_frag16[path] >= 0 ? scn_lstm_passes() : 3;
+          launch_lstm_mfma(a, m->d_w + (ps < 3 ? L.whh_frag16[path] : L.whh_frag[path]), ps, st);
+        }
         else launch_lstm(a, st);
         SESA_CHECK_LAUNCH();
         // bytes: the input-projection gates read once, the hidden outputs written once (W_hh stays on chip)
@@ -2726,7 +2812,10 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
     void* tok = profile_begin(st);
     float* FR = F32(pl.frames);
     const float scale = c.normalized ? 2.0f / 64.0f : 2.0f / (float)kSN;
-    hipLaunchKernelGGL(scn_istft_frames_kernel, dim3(T, B * m->nsig), dim3(kST), 0, st, X, m->nsig, T, scale, tb, FR);
+    const Level& L0 = m->lv[0];   // frame-major when the level-0 band transposed convs ran on MFMA
+    const int fmajor = scn_band_mfma() && L0.su_mm[0] && L0.su_mm[1] && L0.su_mm[2] ? 1 : 0;
+    hipLaunchKernelGGL(scn_istft_frames_kernel, dim3((unsigned)(T * B * m->nsig)), dim3(kST), 0, st, X, m->nsig, T,
+                       fmajor, scale, tb, FR);
     SESA_CHECK_LAUNCH();
     hipLaunchKernelGGL(scn_istft_ola_kernel, dim3((c.chunk_size + kST - 1) / kST, B * m->nsig), dim3(kST), 0, st, FR, T,
                        c.hop_size, c.chunk_size, out);

@@ -373,7 +373,8 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
         const int i2 = m % a.geo.P2, t = m / a.geo.P2;
         const int i1 = t % a.geo.P1, b = t / a.geo.P1;
         orow_i1[r] = i1 * a.geo.phases - a.geo.opad;
-        orow_base[r] = ((a.geo.oq1 ? b * a.geo.oq1 + a.geo.o_row0 : b * a.geo.O1) + orow_i1[r]) * a.geo.P2 + i2;
+        orow_base[r] = a.geo.o_fmajor ? (b * a.geo.P2 + i2) * a.geo.oq1 + a.geo.o_row0 + orow_i1[r]
+                                      : ((a.geo.oq1 ? b * a.geo.oq1 + a.geo.o_row0 : b * a.geo.O1) + orow_i1[r]) * a.geo.P2 + i2;
       }
       __syncthreads();
     }
@@ -423,7 +424,7 @@ __global__ void __launch_bounds__(NT, DB ? 1 : 2) tok_gemm_kernel(TokGemmArgs a)
         const int ml = m - m0;
         const int i1 = orow_i1[ml] + ph;
         ok = ok && i1 >= 0 && i1 < a.geo.O1;
-        return (int64_t)orow_base[ml] + (int64_t)ph * a.geo.P2;
+        return (int64_t)orow_base[ml] + (int64_t)ph * (a.geo.o_fmajor ? 1 : a.geo.P2);
       };
       if (a.residual && n_ok) {
 #pragma unroll
@@ -1698,6 +1699,7 @@ int launch_tok_gemm(const TokGemmArgs& a, int x3, hipStream_t st) {
                      !a.rownorm && (int64_t)c.P1 * c.P2 > 0 && (c.phases == 1 || !a.glu),
                  SESA_ERR_INVALID, "tok_gemm conv: bad geometry");
     SESA_REQUIRE((c.phases == 1 && c.oq1 == 0) || c.O1 > 0, SESA_ERR_INVALID, "tok_gemm conv: output rows need O1");
+    SESA_REQUIRE(!c.o_fmajor || c.oq1 > 0, SESA_ERR_INVALID, "tok_gemm conv: axis-2-major output needs oq1");
     SESA_REQUIRE(c.xq1 == 0 || (c.x_row0 >= 0 && c.x_row0 + c.Q1 <= c.xq1), SESA_ERR_INVALID,
                  "tok_gemm conv: input sub-range [%d, %d) outside %d rows", c.x_row0, c.x_row0 + c.Q1, c.xq1);
     SESA_REQUIRE(c.oq1 == 0 || (c.o_row0 >= 0 && c.o_row0 + c.O1 <= c.oq1), SESA_ERR_INVALID,

@@ -34,7 +34,9 @@ struct TokGroup {
 // Sub-range form (SCNet's band convs, sesa_scnet.hip): xq1 > 0 -- the item's input grid is rows
 // [x_row0, x_row0 + Q1) of a larger per-item grid of xq1 rows (base (b xq1 + x_row0) instead of b Q1; validity
 // still against Q1); oq1 > 0 -- output row i1' (i1 itself, or the transposed row above) of item b lands at
-// (b oq1 + o_row0 + i1') P2 + i2 (validity against O1, = P1 when phases == 1).
+// (b oq1 + o_row0 + i1') P2 + i2 (validity against O1, = P1 when phases == 1); with o_fmajor the output is
+// axis-2-major instead, (b P2 + i2) oq1 + o_row0 + i1' (SCNet's last band convs write the frame-major spectrum the
+// iSTFT reads).
 constexpr int kMaxTaps = 16;
 struct ConvGeo {
   int P1, P2, Q1, Q2, s1, s2;
@@ -43,6 +45,7 @@ struct ConvGeo {
   const float* x2;            // nullable: A = x + x2 (same layout; the decoder's x + skip)
   int phases, O1, opad;
   int xq1, x_row0, oq1, o_row0;
+  int o_fmajor;
 };
 
 struct TokGemmArgs {
