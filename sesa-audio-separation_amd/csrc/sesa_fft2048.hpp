@@ -52,8 +52,17 @@ inline int get_fft2048_tables(Fft2048Tables* out) {
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// complex add / sub as explicit two-lane vectors: one v_pk_add_f32 each, both halves in place (no op_sel).  libsesa
+// is built without the SLP vectorizer (its packed complex arithmetic used half-swapping op_sel forms, which are wrong
+// beside MFMA work on gfx950: tools/isa_guard.py); these lane-parallel forms are the safe part of that packing.
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) {
+  const f32x2 r = f32x2{a.x, a.y} + f32x2{b.x, b.y};
+  return make_float2(r[0], r[1]);
+}
+__device__ __forceinline__ float2 csub(float2 a, float2 b) {
+  const f32x2 r = f32x2{a.x, a.y} - f32x2{b.x, b.y};
+  return make_float2(r[0], r[1]);
+}
 __device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
 
 // 2048-point Stockham FFT in LDS (x -> returned buffer, y is scratch); 256 threads.

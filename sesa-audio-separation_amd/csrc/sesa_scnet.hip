@@ -949,6 +949,24 @@ __global__ void scn_gn_apply_kernel(const float* __restrict__ X, int64_t n_item,
   const float mean = (float)mu, rstd = (float)(1.0 / sqrt(var + 1e-5));
   Y[i] = (X[i] - mean) * rstd * g[c] + be[c];
 }
+// the same as one fp16 plane (the fp16 input projection's A), four elements per thread (n_item % 4 == 0, C % 4 == 0)
+__global__ void scn_gn_apply_f16_kernel(const float* __restrict__ X, int64_t n_item, int C, const double* __restrict__ stats,
+                                        const float* __restrict__ g, const float* __restrict__ be, uint16_t* __restrict__ Y,
+                                        int64_t total4) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total4) return;
+  const int64_t e = 4 * i;
+  const int64_t b = e / n_item;
+  const int c = (int)(e % C);
+  const double mu = stats[2 * b] / (double)n_item;
+  const double var = fmax(stats[2 * b + 1] / (double)n_item - mu * mu, 0.0);
+  const float mean = (float)mu, rstd = (float)(1.0 / sqrt(var + 1e-5));
+  const f32x4 v = reinterpret_cast<const f32x4*>(X)[i];
+  uint16_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o[q] = __builtin_bit_cast(uint16_t, (_Float16)((v[q] - mean) * rstd * g[c + q] + be[c + q]));
+  *reinterpret_cast<uint2*>(Y + e) = make_uint2(o[0] | ((uint32_t)o[1] << 16), o[2] | ((uint32_t)o[3] << 16));
+}
 
 // ---- bi-LSTM recurrence (torch.nn.LSTM, batch_first, gate order i, f, g, o) -----------------
 // token row of (sequence s, position p) = (s / sdiv) * smul_a + (s % sdiv) * smul_b + p * pstride
@@ -960,7 +978,13 @@ struct LstmArgs {
   const float* Wt;    // [2][H][4H]  (W_hh transposed, k-major)
   int H, L, n_seq, sdiv;
   int64_t smul_a, smul_b, pstride;
+  // fp16mix chain (DpLayer::p16): the gates as the input projection's fp16 plane G16 (g_ld) with each direction's
+  // columns gate-interleaved, 4 j + q = gate q of unit j (one 8-B load per row and lane), and h written as the output
+  // Linear's fp16 A plane HO16 (ho_ld); null: G / HO in fp32, column q H + j
+  const uint16_t* G16;
+  uint16_t* HO16;
 };
+__device__ __forceinline__ float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
 
 template <int ST>
 __global__ void __launch_bounds__(kST) scn_lstm_kernel(LstmArgs a) {
@@ -1074,8 +1098,9 @@ __device__ __forceinline__ void lstm_store_h(float hv, uint16_t* hi, uint16_t* l
   }
 }
 
-template <int NW, int PF, int PS = 3>
+template <int NW, int PF, int PS = 3, bool G16 = false>
 __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, const uint16_t* __restrict__ Wf) {
+  static_assert(!G16 || PS < 3, "the fp16 gate plane feeds the fp16 recurrences");
   constexpr int H = 32 * NW, H4 = 4 * H, KS = H / 16, RS = H + 8;
   extern __shared__ __align__(16) uint16_t lsa[];
   uint16_t* Ahi = lsa;            // [32 seq][RS]
@@ -1105,14 +1130,21 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, cons
     const int pos = dir ? a.L - 1 - step : step;
     // input-projection gates: issued now, added after the MFMAs (their latency hides under them);
     // the streamed-W variant (H = 256) loads them after the MFMAs (register budget of 2 waves/SIMD)
-    float gv[4][16];
+    // G16: the fp16 gate plane stays packed (8 B per row, 32 registers) until the cell update -- converting at the
+    // load would make the MFMAs below wait for it
+    float gv[G16 ? 1 : 4][16];
+    uint2 graw[G16 ? 16 : 1];
     auto load_g = [&]() {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t rb = rowb[(r & 3) + 8 * (r >> 2) + 4 * hh];
-        const float* gp = a.G + (rb >= 0 ? (rb + (int64_t)pos * a.pstride) * a.g_ld + dir * H4 + j : 0);
+        const int64_t go = rb >= 0 ? (rb + (int64_t)pos * a.pstride) * a.g_ld + dir * H4 : 0;
+        if constexpr (G16) {
+          graw[r] = rb >= 0 ? *reinterpret_cast<const uint2*>(a.G16 + go + 4 * j) : make_uint2(0u, 0u);
+        } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) gv[q][r] = rb >= 0 ? gp[q * H] : 0.f;
+          for (int q = 0; q < 4; ++q) gv[G16 ? 0 : q][r] = rb >= 0 ? a.G[go + q * H + j] : 0.f;
+        }
       }
     };
     if constexpr (!STREAM) load_g();
@@ -1152,13 +1184,29 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, cons
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int sl = (r & 3) + 8 * (r >> 2) + 4 * hh;
-      const float ig = sigm_f(acc[0][r] + gv[0][r]), fg = sigm_f(acc[1][r] + gv[1][r]);
-      const float gg = tanh_f(acc[2][r] + gv[2][r]), og = sigm_f(acc[3][r] + gv[3][r]);
+      float g4[4];
+      if constexpr (G16) {
+        const uint2 v = graw[r];
+        g4[0] = h2f((uint16_t)v.x);
+        g4[1] = h2f((uint16_t)(v.x >> 16));
+        g4[2] = h2f((uint16_t)v.y);
+        g4[3] = h2f((uint16_t)(v.y >> 16));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g4[q] = gv[G16 ? 0 : q][r];
+      }
+      const float ig = sigm_f(acc[0][r] + g4[0]), fg = sigm_f(acc[1][r] + g4[1]);
+      const float gg = tanh_f(acc[2][r] + g4[2]), og = sigm_f(acc[3][r] + g4[3]);
       c[r] = fg * c[r] + ig * gg;
       const float hv = og * tanh_f(c[r]);
       lstm_store_h<PS>(hv, Ahi + sl * RS + j, Alo + sl * RS + j);
       const int64_t rb = rowb[sl];
-      if (rb >= 0) a.HO[(rb + (int64_t)pos * a.pstride) * a.ho_ld + dir * H + j] = hv;
+      const int64_t ho = (rb + (int64_t)pos * a.pstride) * a.ho_ld + dir * H + j;
+      if (a.HO16) {
+        if (rb >= 0) a.HO16[ho] = __builtin_bit_cast(uint16_t, (_Float16)hv);
+      } else {
+        if (rb >= 0) a.HO[ho] = hv;
+      }
     }
     __syncthreads();  // h_t visible
   }
@@ -1171,7 +1219,8 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_kernel(LstmArgs a, cons
 // one-k-step ring (4 gates x hi / lo = 32 registers): gate q of k-step ks + 1 is requested as soon as
 // gate q of k-step ks has been consumed.
 template <int NW, int PS = 3>
-__global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_wide_kernel(LstmArgs a, const uint16_t* __restrict__ Wf) {
+__global__ void __launch_bounds__(64 * NW, NW <= 8 ? 2 : 1) scn_lstm_mfma_wide_kernel(LstmArgs a,
+                                                                                      const uint16_t* __restrict__ Wf) {
   constexpr int H = 32 * NW, H4 = 4 * H, KS = H / 16, RS = H + 8;
   extern __shared__ __align__(16) uint16_t lsa[];
   uint16_t* Ahi = lsa;            // [32 seq][RS]
@@ -1197,12 +1246,23 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_wide_kernel(LstmArgs a,
     const int pos = dir ? a.L - 1 - step : step;
     asm volatile("" ::: "memory");  // re-read rowb per step (no 32 hoisted row registers)
     f32x16 acc[4];
+    // fp16 gate plane (PS < 3): one 8-B load per row, converted into the starting accumulators (no extra registers:
+    // the kernel must stay within 128 VGPRs for two workgroups per CU at H = 256)
+    const bool g16 = PS < 3 && a.G16 != nullptr;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int64_t rb = rowb[(r & 3) + 8 * (r >> 2) + 4 * hh];
-      const float* gp = a.G + (rb >= 0 ? (rb + (int64_t)pos * a.pstride) * a.g_ld + dir * H4 + j : 0);
+      const int64_t go = rb >= 0 ? (rb + (int64_t)pos * a.pstride) * a.g_ld + dir * H4 : 0;
+      if (g16) {
+        const uint2 v = rb >= 0 ? *reinterpret_cast<const uint2*>(a.G16 + go + 4 * j) : make_uint2(0u, 0u);
+        acc[0][r] = h2f((uint16_t)v.x);
+        acc[1][r] = h2f((uint16_t)(v.x >> 16));
+        acc[2][r] = h2f((uint16_t)v.y);
+        acc[3][r] = h2f((uint16_t)(v.y >> 16));
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q][r] = rb >= 0 ? gp[q * H] : 0.f;
+        for (int q = 0; q < 4; ++q) acc[q][r] = rb >= 0 ? a.G[go + q * H + j] : 0.f;
+      }
     }
     bf16x8 bh[4], bl[4];
 #pragma unroll
@@ -1234,7 +1294,12 @@ __global__ void __launch_bounds__(64 * NW) scn_lstm_mfma_wide_kernel(LstmArgs a,
       const float hv = og * tanh_f(c[r]);
       lstm_store_h<PS>(hv, Ahi + sl * RS + j, Alo + sl * RS + j);
       const int64_t rb = rowb[sl];
-      if (rb >= 0) a.HO[(rb + (int64_t)pos * a.pstride) * a.ho_ld + dir * H + j] = hv;
+      const int64_t ho = (rb + (int64_t)pos * a.pstride) * a.ho_ld + dir * H + j;
+      if (a.HO16) {
+        if (rb >= 0) a.HO16[ho] = __builtin_bit_cast(uint16_t, (_Float16)hv);
+      } else {
+        if (rb >= 0) a.HO[ho] = hv;
+      }
     }
     __syncthreads();  // h_t visible
   }
@@ -1258,6 +1323,12 @@ void launch_lstm_mfma_t(const LstmArgs& a, const uint16_t* Wf, hipStream_t st) {
   dim3 grid((unsigned)((a.n_seq + 31) / 32), 2);
   if constexpr (NW <= 8) {
     if (NW < lstm_wide_min_nw()) {
+      if constexpr (PS < 3) {
+        if (a.G16) {
+          hipLaunchKernelGGL((scn_lstm_mfma_kernel<NW, PF, PS, true>), grid, dim3(64 * NW), lds, st, a, Wf);
+          return;
+        }
+      }
       hipLaunchKernelGGL((scn_lstm_mfma_kernel<NW, PF, PS>), grid, dim3(64 * NW), lds, st, a, Wf);
       return;
     }
@@ -1637,6 +1708,7 @@ struct DpLayer {
   int64_t whh[2], gn_g[2], gn_b[2];
   int64_t whh_frag[2];  // uint16 offset of the MFMA B fragments (d_w blob)
   int64_t whh_frag16[2] = {-1, -1};  // the same as fp16 hi / lo (fp16mix, H <= 256: the PS < 3 recurrences)
+  int p16 = 0;  // fp16mix plane chain (scn_p16_mode): 0 fp32 G / HO; 1 fp16 gate-interleaved G16; 2 G16 + fp16 HO16
 };
 
 }  // namespace
@@ -1742,6 +1814,12 @@ int scn_lstm_passes() {
     const int p = getenv("SESA_SCN_LSTM_PASSES") ? atoi(getenv("SESA_SCN_LSTM_PASSES")) : 1;
     return p == 1 || p == 2 ? p : 3;
   }();
+  return v;
+}
+
+// SESA_SCN_P16 = 0 | 1 | 2 (default 2): how much of the fp16mix dual-path chain runs in fp16 planes (DpLayer::p16)
+int scn_p16_mode() {
+  static const int v = getenv("SESA_SCN_P16") ? atoi(getenv("SESA_SCN_P16")) : 2;
   return v;
 }
 
@@ -2217,10 +2295,18 @@ extern "C" int sesa_scnet_finalize(sesa_scnet* m, void* stream) {
       const auto& bhf = P(m, q + ".bias_hh_l0");
       const auto& bir = P(m, q + ".bias_ih_l0_reverse");
       const auto& bhr = P(m, q + ".bias_hh_l0_reverse");
+      // the fp16 chain's gate plane interleaves each direction's columns: packed column dir 4H + 4 j + q = gate q of
+      // unit j (source row dir 4H + q H + j)
+      L.p16 = f16w && H <= 256 && lstm_mfma_on(H) && scn_lstm_passes() < 3 ? scn_p16_mode() : 0;
+      const bool ilv = L.p16 > 0;
+      auto src_n = [&](int n) { const int dir = n / (4 * H), r = n - dir * 4 * H;
+                                return ilv ? dir * 4 * H + (r & 3) * H + (r >> 2) : n; };
       TokGroup g = pack_group(
           8 * H, d,
-          [&](int n, int k) { return n < 4 * H ? Wf[(int64_t)n * d + k] : Wr[(int64_t)(n - 4 * H) * d + k]; }, true,
-          [&](int n) { return n < 4 * H ? bif[n] + bhf[n] : bir[n - 4 * H] + bhr[n - 4 * H]; }, blob, bias, f16w);
+          [&](int n, int k) { const int sn = src_n(n);
+                              return sn < 4 * H ? Wf[(int64_t)sn * d + k] : Wr[(int64_t)(sn - 4 * H) * d + k]; }, true,
+          [&](int n) { const int sn = src_n(n); return sn < 4 * H ? bif[sn] + bhf[sn] : bir[sn - 4 * H] + bhr[sn - 4 * H]; },
+          blob, bias, f16w);
       g.x_off = g.o_off = 0;
       L.ih[l].groups = {g};
       const auto& Wl = P(m, p + ".linear_layers." + S(l) + ".weight");
@@ -2623,10 +2709,21 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
       const unsigned gb = (unsigned)std::min<int64_t>((n_item + kST * 8 - 1) / (kST * 8), 512);
       hipLaunchKernelGGL(scn_gn_stats_kernel, dim3(gb, B), dim3(kST), 0, st, X, n_item, stats);
       SESA_CHECK_LAUNCH();
-      hipLaunchKernelGGL(scn_gn_apply_kernel, blocks(B * n_item), dim3(kST), 0, st, X, n_item, d, stats,
-                         Wb + L.gn_g[path], Wb + L.gn_b[path], bufN, (int64_t)B * n_item);
+      // fp16mix with the fp16 recurrence: the dual-path chain in fp16 planes -- GroupNorm -> fp16 A plane, input
+      // projection -> fp16 gate plane (LDS-DMA kernel, split epilogue), recurrence -> fp16 h plane, Linear from it
+      const int p16m = f16mix ? L.p16 : 0;
+      const bool p16 = p16m > 0;
+      uint16_t* N16 = reinterpret_cast<uint16_t*>(bufN);
+      uint16_t* G16 = reinterpret_cast<uint16_t*>(G);
+      uint16_t* HO16 = reinterpret_cast<uint16_t*>(HO);
+      if (p16)
+        hipLaunchKernelGGL(scn_gn_apply_f16_kernel, blocks(B * n_item / 4), dim3(kST), 0, st, X, n_item, d, stats,
+                           Wb + L.gn_g[path], Wb + L.gn_b[path], N16, (int64_t)B * n_item / 4);
+      else
+        hipLaunchKernelGGL(scn_gn_apply_kernel, blocks(B * n_item), dim3(kST), 0, st, X, n_item, d, stats,
+                           Wb + L.gn_g[path], Wb + L.gn_b[path], bufN, (int64_t)B * n_item);
       SESA_CHECK_LAUNCH();
-      profile_end(tok, st, SESA_KCLASS_ACT, 12.0 * B * n_item);
+      profile_end(tok, st, SESA_KCLASS_ACT, (p16 ? 10.0 : 12.0) * B * n_item);
       // input projection, both directions: G = XN W_ih^T + (b_ih + b_hh)
       {
         TokGemmArgs a{};
@@ -2634,6 +2731,14 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         a.x_ld = d;
         a.out = G;
         a.o_ld = 8 * H;
+        if (p16) {
+          a.a_hi = N16;
+          a.a_ld = d;
+          a.out = nullptr;
+          a.out_hi = G16;
+          a.k8 = L.ih[path].k8;
+          a.n4 = L.ih[path].n4;
+        }
         a.w = m->d_w;
         a.bias = m->d_bias;
         a.groups = L.ih[path].d_groups;
@@ -2655,6 +2760,8 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         a.ho_ld = 2 * H;
         a.Wt = Wb + L.whh[path];
         a.H = H;
+        if (p16) a.G16 = G16;
+        if (p16m == 2) a.HO16 = HO16;
         if (path == 0) {
           a.L = Fn;
           a.n_seq = B * Tc;
@@ -2678,7 +2785,8 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         else launch_lstm(a, st);
         SESA_CHECK_LAUNCH();
         // bytes: the input-projection gates read once, the hidden outputs written once (W_hh stays on chip)
-        profile_end(t0, st, SESA_KCLASS_LSTM, 2.0 * rows * 2 * 4 * H * (double)H, 4.0 * rows * (8.0 * H + 2.0 * H));
+        profile_end(t0, st, SESA_KCLASS_LSTM, 2.0 * rows * 2 * 4 * H * (double)H,
+                    rows * ((p16 ? 2.0 : 4.0) * 8.0 * H + (p16m == 2 ? 2.0 : 4.0) * 2.0 * H));
       }
       // Linear(2H -> d) + residual, in place
       {
@@ -2688,6 +2796,12 @@ extern "C" int sesa_scnet_forward(sesa_scnet* m, const float* x, int B, float* o
         a.out = X;
         a.o_ld = d;
         a.residual = X;
+        if (p16m == 2) {
+          a.a_hi = HO16;
+          a.a_ld = 2 * H;
+          a.k8 = L.lin[path].k8;
+          a.n4 = L.lin[path].n4;
+        }
         a.w = m->d_w;
         a.bias = m->d_bias;
         a.groups = L.lin[path].d_groups;
