@@ -796,8 +796,14 @@ def main():
     # dominant kernel class: the model's own, or the class with the most kernel time
     kclass = MODELS[args.model][2] or max(roofs, key=lambda k: roofs[k]["ms_per_step"])
     roof = dict(roofs[kclass])
-    traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model, member_prec),
-                                       args.model, roof["launches"] / args.steps)
+    if pworld > 1:
+        # the committed PMC summaries count one step of the N = 1 workload (its exec batch, its chunk count): a rank's
+        # share has other launches and per-launch sizes, so its counter bytes are not known here
+        traffic, traffic_src = None, (f"profiles/pmc_{kclass}_{args.model}.json counts the 1-GPU workload; not applied to "
+                                      f"a {pworld}-rank share")
+    else:
+        traffic, traffic_src = pmc_traffic(kclass, class_precision(kclass, args.precision, args.model, member_prec),
+                                           args.model, roof["launches"] / args.steps)
     if isinstance(traffic_src, dict):   # one algorithmic figure: this run's (the PMC file's own is for its run)
         traffic_src.pop("algorithmic_bytes_per_launch", None)
     alg_bytes = roof["algorithmic_bytes_per_launch"]

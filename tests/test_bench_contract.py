@@ -27,7 +27,8 @@ def test_default_precision():
     assert cp("attn", "fp16mix", "htdemucs") == "fp16"
     assert cp("tokgemm", "fp16mix", "htdemucs") == "fp16"       # HTDemucs fp16mix Linears: one fp16 pass
     assert cp("tokgemm", "fp16mix", "scnet") == "fp16"
-    assert cp("lstm", "fp16mix", "scnet") == "bf16x3"
+    assert cp("lstm", "fp16mix", "scnet") == "fp16"               # one fp16 recurrence pass (SESA_SCN_LSTM_PASSES=1)
+    assert cp("lstm", "bf16x3", "scnet") == "bf16x3" and cp("lstm", "bf16", "scnet") == "bf16"
     assert cp("simt", "fp16mix", "scnet") == "fp32"              # VALU kernels
     assert cp("dft", "fp16mix", "scnet") == "bf16x3"             # feature-conversion DFTs on MFMA
     assert cp("conv3x3", "fp16") == "fp16" and cp("conv3x3", "fp16mix") == "fp16"
@@ -95,3 +96,14 @@ def test_bench_maps_fp16_to_parity_for_other_members(name, monkeypatch):
     monkeypatch.setattr(bench, "synth_weights", lambda m: {})
     bench.build_model(name, "fp16w2")
     assert seen["p"] == "bf16x3"
+
+
+def test_scnet_lstm_pass_switch(monkeypatch):
+    """SESA_SCN_LSTM_PASSES selects the fp16mix recurrence's MFMA passes (sesa_scnet.hip scn_lstm_passes); the line
+    prices the lstm class at the matching peak."""
+    cp = bench.class_precision
+    for env, want in (("1", "fp16"), ("2", "fp16w2"), ("3", "bf16x3")):
+        monkeypatch.setenv("SESA_SCN_LSTM_PASSES", env)
+        assert cp("lstm", "fp16mix", "scnet") == want
+    monkeypatch.setenv("SESA_SCN_LSTM_PASSES", "3")
+    assert cp("lstm", "bf16", "scnet") == "bf16"
