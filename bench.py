@@ -60,6 +60,11 @@ MODELS = {
     "htdemucs": ("config_musdb18_htdemucs.yaml", 4.857e11, None),
 }
 ENSEMBLE = ("mdx23c", "bs_roformer", "scnet")
+# forwards in flight per rank (sesa/parallel.py local_accumulate_device; re-entrant per stream since round 6).  Same box,
+# --streams 1 vs 2 (profiles/r06_streams_ab.txt): HTDemucs 1282 -> 1342x (the 30-min track's 11 forwards overlap their
+# low-occupancy tails); MDX23C +1.4 %, BS-Roformer +1.6 % -- inside the box spread, so they keep one stream; SCNet runs
+# one forward per step
+DEFAULT_STREAMS = {"htdemucs": 2}
 MODELS["ensemble"] = (None, sum(MODELS[m][1] for m in ENSEMBLE), None)
 METRIC = {"ensemble": "separated-audio sec/sec (RTF), ensemble mdx23c + bs_roformer + scnet (vocals, avg_wave), MI355X",
           "mdx23c": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X",
@@ -601,8 +606,9 @@ def main():
     ap.add_argument("--no-parity", action="store_true", help="skip the parity forward (PMC passes: one workload only)")
     ap.add_argument("--no-pcie", action="store_true",
                     help="skip the PCIe-inclusive timing (PMC / kernel-trace runs: the timed steps only)")
-    ap.add_argument("--streams", type=int, default=1, help="forwards in flight on separate HIP streams (bit-identical "
-                    "to 1, sesa/parallel.py)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="forwards in flight on separate HIP streams, bit-identical to 1 (sesa/parallel.py); default "
+                         "per model (DEFAULT_STREAMS)")
     ap.add_argument("--rank-share", type=int, default=0, metavar="W",
                     help="one-GPU rehearsal of rank 0's share of a W-rank run (its chunks, its exec batch, local OLA + "
                          "finalise, no collective): value = the implied W-rank ceiling (track seconds / rank-0 time)")
@@ -613,6 +619,8 @@ def main():
     args = ap.parse_args()
     if args.precision is None:
         args.precision = default_precision(args.model)
+    if args.streams is None:
+        args.streams = DEFAULT_STREAMS.get(args.model, 1)
     track_seconds = args.track_seconds or TRACK_SECONDS.get(args.model, 240.0)
 
     from sesa.launch import needs_spawn, spawn_world, world_from_env
@@ -718,7 +726,11 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    _native.profile_enable(True)
+    # libsesa's per-launch event timing (the rooflines) runs inside the timed steps on one stream; with forwards in
+    # flight on several streams an event pair would also time the other stream's kernels, so the rooflines then come
+    # from a separate single-stream pass of the same K steps below (`roofline.timing_pass`)
+    streams_timed = args.streams
+    _native.profile_enable(streams_timed == 1)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         est = step()
@@ -728,6 +740,14 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     _native.profile_enable(False)
+    if streams_timed > 1:
+        args.streams = 1
+        _native.profile_enable(True)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        _native.profile_enable(False)
+        args.streams = streams_timed
     # the same K steps with the host transfers inside (reported as pcie_inclusive, never as `value`)
     if world > 1:
         dist.barrier()
@@ -815,6 +835,9 @@ def main():
             per_fwd += b_
             l_fwd += l_
         roof["algorithmic_bytes_host_model"] = round(per_fwd / max(l_fwd, 1))
+    roof["timing_pass"] = ("the timed steps (one stream)" if args.streams == 1 else
+                           f"a separate single-stream pass of the same {args.steps} steps (the timed steps ran "
+                           f"{args.streams} streams)")
     roof.update(traffic=traffic, traffic_source=traffic_src, kernel=kdesc(kclass, args.precision, args.model),
                 traffic_over_algorithmic=round(traffic / alg_bytes, 3) if traffic and alg_bytes else None,
                 **{"class": kclass})
@@ -844,7 +867,7 @@ def main():
             "config": {"workload": f"{desc[0]}, {track_seconds:.0f} s 44.1 kHz stereo track chunked; timed: the mix "
                                    f"resident in HBM -> gather -> forwards -> OLA -> finalise -> stems in HBM "
                                    f"(pcie_inclusive adds the pinned host mix H2D and the stems D2H)",
-                       "model": args.model, "chunks": n_chunks,
+                       "model": args.model, "chunks": n_chunks, "streams": args.streams,
                        "exec_batch": batches[0] if len(batches) == 1 else batches,
                        "parallelism": ((f"chunk-shard x{world}, owned ranges: per-rank input span H2D, RCCL seam "
                                         f"exchange with neighbours, per-rank finalise + D2H" if owned else
