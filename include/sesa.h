@@ -14,7 +14,10 @@
  * of its prior contents and writing nothing outside their buffers (tools/ws_guard.py) -- and read the handle's packed
  * weights only, so forwards of one handle may run on several streams of one device at once, each with its own
  * workspace, input and output; the results are bit-identical to running them one after another
- * (tests/test_gpu_parity.py::test_side_streams_bit_identical).  Rounds 4-5 saw them differ: the FFT kernels'
+ * (tests/test_gpu_parity.py::test_side_streams_bit_identical; full-size 4-min tracks at two streams: MDX23C, SCNet and
+ * HTDemucs 0 differing samples, tools/streams_check.py).  Exception, cause open: sesa_bsr_forward at full size differs
+ * in ~1e-4 of the samples (max 3.7e-3) when two forwards overlap, so the Python layer keeps BS-Roformer /
+ * Mel-Band-Roformer on one stream (NativeModule.multi_stream_ok).  Rounds 4-5 saw them differ: the FFT kernels'
  * SLP-packed complex arithmetic (v_pk_add_f32 / v_pk_mul_f32 with a source op_sel) returned wrong values on gfx950
  * while another wave on the same CU executed MFMAs (profiles/r06_pk_opsel_hazard.txt); libsesa is built without
  * such instructions and tools/isa_guard.py fails the build if one appears.  The other entry points (STFT / iSTFT /

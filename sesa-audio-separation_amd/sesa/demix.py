@@ -11,6 +11,7 @@ The *logical* batch (``config.inference.batch_size``) still decides the window f
 in the reference (:145-155); the *execution* batch is independent of it (InstanceNorm is
 per-instance, so grouping chunks differently does not change any chunk's output).
 """
+import contextlib
 import math
 
 import numpy as np
@@ -114,10 +115,21 @@ class _Windows:
         return self.no_in if no_in else (self.no_out if no_out else self.normal)
 
 
+# forwards in flight in demix_device (consecutive execution batches alternate between the current stream and side
+# streams; the OLA stays on the current stream in chunk order, so the stems are bit-identical to one stream for the
+# models whose forwards are -- NativeModule.multi_stream_ok).  Same box, bench.py --streams 1 vs 2: HTDemucs +4.6 %,
+# MDX23C +1.4 % (profiles/r06_streams_ab.txt)
+DEMIX_STREAMS = 2
+
+
 def demix_device(config, model, mix, device, exec_batch=None, progress=True, chunk_range=None,
-                 instruments=None):
+                 instruments=None, streams=None):
     """Core device loop.  ``mix`` is a host array [2, L] or a device tensor.  Returns the
     device tensor est [n_instr, 2, L] (after nan_to_num and border crop).
+
+    ``streams`` (default DEMIX_STREAMS): execution batches in flight on separate HIP streams; the native forwards
+    are re-entrant per stream (include/sesa.h) and the OLA runs on the current stream in chunk order, so the result
+    does not depend on it.
 
     ``chunk_range`` = (first, last) restricts the work to a contiguous range of global chunk
     indices (multi-GPU chunk sharding, sesa/parallel.py); the caller then receives the raw
@@ -139,8 +151,11 @@ def demix_device(config, model, mix, device, exec_batch=None, progress=True, chu
             return (torch.zeros(ni * n_ch, 0, device=device), torch.zeros(0, device=device), (False, 0, 0))
         return torch.zeros(ni, n_ch, 0, device=device, dtype=torch.float32)
     padded, border, L_pad, batches, prog = chunk_plan(L, C, ov, bs)
+    streams = max(1, int(DEMIX_STREAMS if streams is None else streams)) if torch.device(device).type == "cuda" else 1
+    if not getattr(model, "multi_stream_ok", True):
+        streams = 1            # (models/bs_roformer.py)
     E = exec_batch or getattr(model, "exec_batch", None) or plan_exec_batch(model, len(flat_plan(batches)), C,
-                                                                            device)
+                                                                            device, streams=streams)
     win = _Windows(C, device)
     result = torch.zeros(ni * n_ch, L_pad, device=device, dtype=torch.float32)
     counter = torch.zeros(L_pad, device=device, dtype=torch.float32)
@@ -151,16 +166,33 @@ def demix_device(config, model, mix, device, exec_batch=None, progress=True, chu
             flat.append((s, n, no_in, no_out))
     lo, hi = (0, len(flat)) if chunk_range is None else chunk_range
     prog_at = dict(prog)
-    xbuf = None
-    pos = lo
+    pool, xbufs, freed = [None], [None], [None]
+    if streams > 1:
+        from .parallel import side_streams
+        main = torch.cuda.current_stream(device)
+        pool = [main] + side_streams(device, streams - 1)
+        xbufs, freed = [None] * len(pool), [None] * len(pool)
+        for st in pool[1:]:
+            st.wait_stream(main)      # the mix upload and the zeroed buffers happen-before every side stream
+    pos, gi = lo, 0
     while pos < hi:
         group = flat[pos:min(hi, pos + E)]
         starts = [g[0] for g in group]
-        if xbuf is None or xbuf.shape[0] != len(group):
-            xbuf = torch.empty(len(group), n_ch, C, device=device, dtype=torch.float32)
-        ops.chunk_gather(mix_d, border if padded else 0, starts, C, out=xbuf)
-        y = model(xbuf)
-        y = y.reshape(len(group), ni * n_ch, C)
+        si = gi % len(pool)
+        st = pool[si]
+        side = st is not None and st is not pool[0]
+        if side and freed[si] is not None:
+            st.wait_event(freed[si])  # its input buffer / workspace are free again
+        with torch.cuda.stream(st) if side else contextlib.nullcontext():
+            if xbufs[si] is None or xbufs[si].shape[0] != len(group):
+                xbufs[si] = torch.empty(len(group), n_ch, C, device=device, dtype=torch.float32)
+            xbuf = xbufs[si]
+            ops.chunk_gather(mix_d, border if padded else 0, starts, C, out=xbuf)
+            y = model(xbuf)
+            y = y.reshape(len(group), ni * n_ch, C)
+        if side:
+            pool[0].wait_stream(st)
+            y.record_stream(pool[0])
         # OLA per run of equal windows (== per logical batch), in chunk order
         j = 0
         while j < len(group):
@@ -170,11 +202,17 @@ def demix_device(config, model, mix, device, exec_batch=None, progress=True, chu
             w = win.pick(*group[j][2:])
             ops.ola_accumulate(y[j:k], [g[0] for g in group[j:k]], [g[1] for g in group[j:k]], w, result, counter)
             j = k
+        if side:
+            freed[si] = torch.cuda.Event()
+            freed[si].record(pool[0])
         if progress:
             for ci in range(pos, pos + len(group)):
                 if ci in prog_at:
                     print(f"[SESA_PROGRESS]{prog_at[ci]}", flush=True)
         pos += len(group)
+        gi += 1
+    for st in pool[1:]:
+        pool[0].wait_stream(st)
     if chunk_range is not None:
         return result, counter, (padded, border, L_pad)
     est = ops.ola_finalize(result, counter, border if padded else 0)

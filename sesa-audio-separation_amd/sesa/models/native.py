@@ -35,6 +35,11 @@ class _Node(torch.nn.Module):
 class NativeModule(torch.nn.Module):
     """Base of the native model faces.  Subclasses set ``_prefix`` (``sesa_<prefix>_*`` entry
     points) and implement ``_config(chunk)`` (the ctypes config struct) and ``_out_shape``."""
+    # forwards of one handle on several streams at once (sesa.parallel streams > 1): bit-identical to one stream for
+    # this model at full size (tools/streams_check.py, DESIGN.md §6).  A model that is not sets it False and the
+    # multi-stream loops run it on one stream.
+    multi_stream_ok = True
+
 
     _prefix = None
     _precisions = ("bf16x3", "bf16")

@@ -47,10 +47,12 @@ def zeroed_ws(self, device, h, batch):
 
 
 def build(kind, precision):
-    m, c = get_model_from_config(kind, os.path.join(CONFIGS, CFG[kind]))
+    # STREAMS_TRACE_CONFIG=<yaml under tests/configs>: another config (the full-size ones) instead of CFG's small one
+    m, c = get_model_from_config(kind, os.path.join(CONFIGS, os.environ.get("STREAMS_TRACE_CONFIG", CFG[kind])))
     m.load_state_dict(synth_state_dict(m, affine="random") if kind == "mdx23c" else
                       synth_model_state(m, affine="random"), strict=True)
     m.set_precision(precision)
+    m.multi_stream_ok = True   # trace the raw behaviour
     return m, c
 
 
