@@ -14,15 +14,17 @@
  * of its prior contents and writing nothing outside their buffers (tools/ws_guard.py) -- and read the handle's packed
  * weights only, so forwards of one handle may run on several streams of one device at once, each with its own
  * workspace, input and output; the results are bit-identical to running them one after another
- * (tests/test_gpu_parity.py::test_side_streams_bit_identical; full-size 4-min tracks at two streams: MDX23C, SCNet and
- * HTDemucs 0 differing samples, tools/streams_check.py).  Exception, cause open: sesa_bsr_forward at full size differs
- * in ~1e-4 of the samples (max 3.7e-3) when two forwards overlap, so the Python layer keeps BS-Roformer /
- * Mel-Band-Roformer on one stream (NativeModule.multi_stream_ok).  Rounds 4-5 saw them differ: the FFT kernels'
- * SLP-packed complex arithmetic (v_pk_add_f32 / v_pk_mul_f32 with a source op_sel) returned wrong values on gfx950
- * while another wave on the same CU executed MFMAs (profiles/r06_pk_opsel_hazard.txt); libsesa is built without
- * such instructions and tools/isa_guard.py fails the build if one appears.  The other entry points (STFT / iSTFT /
- * gather / OLA / blend) are plain streaming kernels without shared state.  Only sesa_*_set_param / _finalize /
- * _destroy mutate a handle and must not overlap its forwards.
+ * (tests/test_gpu_parity.py::test_side_streams_bit_identical, tests/test_bsr.py::test_full_size_4min_properties;
+ * full-size 4-min tracks at two streams: all four networks 0 differing samples, tools/streams_check.py).  Rounds 4-6
+ * saw them differ, from two gfx950 behaviours under another kernel's waves on the same CU: (1) packed-fp32 VALU ops
+ * with a source op_sel (v_pk_add_f32 / v_pk_mul_f32, SLP-emitted in the FFT kernels) returned wrong values beside
+ * MFMA work (profiles/r06_pk_opsel_hazard.txt) -- libsesa is built without them, tools/isa_guard.py fails the build
+ * otherwise; (2) an s_barrier reached with the wave's own LDS writes in flight (the compiler omits the lgkmcnt wait
+ * of __syncthreads where its fence needs no cross-address-space ordering) let other waves read the previous FFT
+ * stage -- every such barrier now waits first (sesa_sync), tools/barrier_scan.py fails the build otherwise
+ * (profiles/r06_sync_ab.txt).  The other entry points (STFT / iSTFT / gather / OLA / blend) are plain streaming
+ * kernels without shared state.  Only sesa_*_set_param / _finalize / _destroy mutate a handle and must not overlap
+ * its forwards.
  *
  * Compute is fp32 in / fp32 out.  The MDX23C network runs its contractions on MFMA in one of
  * two precisions (sesa_mdx23c_config.precision):

@@ -90,7 +90,7 @@ __device__ float2* fft1024(float2* x, float2* y, const float2* __restrict__ tw) 
 #pragma unroll 1
   for (int stage = 0; stage < 5; ++stage) {
     const int m = n >> 2;
-    __syncthreads();
+    sesa_sync();
     const int bfly = threadIdx.x;  // 256 butterflies per stage
     const int q = bfly & (s - 1);
     const int p = bfly >> __builtin_ctz(s);
@@ -107,7 +107,7 @@ __device__ float2* fft1024(float2* x, float2* y, const float2* __restrict__ tw) 
     n = m;
     s <<= 2;
   }
-  __syncthreads();
+  sesa_sync();
   return x;
 }
 
@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(kFT) bsr_istft_frames_kernel(const float* __re
     if (k == 0 || k == kH) Y.y = 0.f;  // C2R ignores the imaginary parts of DC and Nyquist
     bufB[k] = Y;
   }
-  __syncthreads();
+  sesa_sync();
   for (int k = threadIdx.x; k < kH; k += kFT) {
     const float2 xk = bufB[k];
     const float2 xm = cconj(bufB[kH - k]);
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(kFT) bsr_istft_frames_kernel(const float* __re
     const float2 O = cmul(make_float2(0.5f * D.x, 0.5f * D.y), w);
     bufA[k] = make_float2(E.x - O.y, E.y + O.x);
   }
-  __syncthreads();  // bufB is reused as the FFT ping-pong buffer
+  sesa_sync();  // bufB is reused as the FFT ping-pong buffer
   float2* z = fft1024<true>(bufA, bufB, tb.tw);
   float* fw = frame_ws + ((int64_t)sig * frames + t) * kN;
   const float scale = 1.0f / (float)kH;

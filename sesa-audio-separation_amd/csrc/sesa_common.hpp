@@ -37,6 +37,17 @@ void clear_error();
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- device helpers ----
+// Workgroup barrier that first retires this wave's own LDS operations.  __syncthreads() leaves the lgkmcnt wait to the
+// memory legalizer, which omits it where its fence needs no cross-address-space ordering (LLVM takes LDS operations of
+// all waves to execute in one global order), e.g. at the top of an LDS ping-pong FFT stage loop.  On MI355X that
+// order did not hold with another kernel's waves on the CU: the BS-Roformer iSTFT read a previous stage's values for
+// whole waves (512-sample runs of a frame) when another stream's forward ran beside it (tools/barrier_scan.py lists the
+// barriers reachable with LDS writes in flight).
+__device__ __forceinline__ void sesa_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

@@ -72,7 +72,7 @@ __device__ float2* fft2048(float2* x, float2* y, const float2* __restrict__ tw) 
 #pragma unroll 1
   for (int stage = 0; stage < 5; ++stage) {
     const int m = n >> 2;
-    __syncthreads();
+    sesa_sync();
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int bfly = threadIdx.x + r * kFftThreads;  // 512 butterflies per stage
@@ -92,7 +92,7 @@ __device__ float2* fft2048(float2* x, float2* y, const float2* __restrict__ tw) 
     n = m;
     s <<= 2;
   }
-  __syncthreads();  // n = 2, s = 1024: final radix-2 stage, unit twiddles
+  sesa_sync();  // n = 2, s = 1024: final radix-2 stage, unit twiddles
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int q = threadIdx.x + r * kFftThreads;
@@ -100,7 +100,7 @@ __device__ float2* fft2048(float2* x, float2* y, const float2* __restrict__ tw) 
     y[q] = cadd(a, b);
     y[q + 1024] = csub(a, b);
   }
-  __syncthreads();
+  sesa_sync();
   return y;
 }
 

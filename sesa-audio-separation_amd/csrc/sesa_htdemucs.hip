@@ -1787,7 +1787,7 @@ __global__ void __launch_bounds__(kT) htd_istft_fused_kernel(const float* __rest
   }
   for (int tp = tpa - 3; tp < tpb; ++tp) {
     if (real(tp)) {   // (uniform)
-      __syncthreads();   // the previous frame's ring add (reads of z) and emit are done
+      sesa_sync();   // the previous frame's ring add (reads of z) and emit are done
 #pragma unroll
       for (int u = 0; u < KPT; ++u) {
         const int k = threadIdx.x + u * kT;
@@ -1796,7 +1796,7 @@ __global__ void __launch_bounds__(kT) htd_istft_fused_kernel(const float* __rest
       int nx = tp + 1;   // the next real frame: its loads fly under this frame's FFT
       while (nx < tpb && !real(nx)) ++nx;
       if (nx < tpb) load_frame(nx - 2);
-      __syncthreads();
+      sesa_sync();
       for (int k = threadIdx.x; k < kFft2048; k += kT) bufA[k] = irfft_pack(bufB, tb.twN, k);
       const float2* z = fft2048<true>(bufA, bufB, tb.tw);   // (returns after a barrier)
       for (int k = threadIdx.x; k < kFft2048; k += kT) {
@@ -1806,7 +1806,7 @@ __global__ void __launch_bounds__(kT) htd_istft_fused_kernel(const float* __rest
         ring[pos + 1] += v.y * sc * win[2 * k + 1];
       }
     }
-    __syncthreads();
+    sesa_sync();
     // samples [tp hop, tp hop + hop) are complete: emit the segment's, then clear their slots
     for (int mm = threadIdx.x; mm < kHop; mm += kT) {
       const int n = tp * kHop + mm, idx = n & (kFft4096 - 1);

@@ -545,7 +545,7 @@ __global__ void __launch_bounds__(kST) scn_cm_mfma_kernel(CmArgs a) {
 
   // ---- B: k3 conv C -> 2h + GLU, slab by slab ----
   for (int t0 = 0; t0 < T; t0 += kCmTT) {
-    __syncthreads();   // (the previous slab's fragment reads are done; first slab: W1 and the stats are in place)
+    sesa_sync();   // (the previous slab's fragment reads are done; first slab: W1 and the stats are in place)
     for (int i = tid; i < (kCmTT + 2) * C4; i += kST) {
       const int rl = i / C4;
       const int t = t0 - 1 + rl;
@@ -560,7 +560,7 @@ __global__ void __launch_bounds__(kST) scn_cm_mfma_kernel(CmArgs a) {
       for (int q = 0; q < 4; ++q) hv[q] = (_Float16)v[q];
       *reinterpret_cast<h16x4*>(xs + rl * SX + c0) = hv;
     }
-    __syncthreads();
+    sesa_sync();
     const int tl0 = 16 * w;
     if (t0 + tl0 < T) {   // (wave-uniform)
       f32x4 acc[NT1];
@@ -588,7 +588,7 @@ __global__ void __launch_bounds__(kST) scn_cm_mfma_kernel(CmArgs a) {
         }
     }
   }
-  __syncthreads();   // U complete; the slab buffer and W1 are dead
+  sesa_sync();   // U complete; the slab buffer and W1 are dead
 
   // ---- C: depthwise k3 + GroupNorm(1, h) statistics, then Swish(norm) as fp16 V; W3 fragments -> LDS ----
   {
@@ -629,7 +629,7 @@ __global__ void __launch_bounds__(kST) scn_cm_mfma_kernel(CmArgs a) {
     }
     vh[t * SV + j] = (_Float16)o;
   }
-  __syncthreads();
+  sesa_sync();
 
   // ---- D: 1x1 conv h -> C + b3 + residual (+ gelu), in place ----
   const int KS2 = hp / 32, NT2 = C / 16;

@@ -533,7 +533,7 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
   if (PERS && blockIdx.x >= gridDim.x / 2)
     for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   for (int wgi = blockIdx.x; wgi < n_wg; wgi += (PERS ? (int)gridDim.x : n_wg)) {
-  if (PERS) __syncthreads();   // the previous tile's epilogue is done with the LDS the ring and tables reuse
+  if (PERS) sesa_sync();   // the previous tile's epilogue is done with the LDS the ring and tables reuse
   const TokGroup g = a.groups[blockIdx.y];
   const int n_tiles2 = HT ? a.n_tiles_n : (a.n_tiles_n + 1) >> 1;   // TN-column tiles
   const int tile = xcd_tile(wgi, n_wg);
@@ -673,7 +673,7 @@ __global__ void __launch_bounds__(HT ? 256 : 512, HT ? 2 : 1) tok_gemm_glds_kern
       }
   };
 
-  __syncthreads();                                         // rs / rpos visible; no DMA in flight yet
+  sesa_sync();                                         // rs / rpos visible; no DMA in flight yet
   // waves whose 64 columns all lie past the group's N (the partial last tile, e.g. BS-Roformer's
   // 8 gate columns after q / k / v) skip their MFMAs (wave-uniform); they still issue their DMA pieces
   const bool busy = n0 + wn * 64 < g.N;

@@ -153,7 +153,7 @@ def demix_device(config, model, mix, device, exec_batch=None, progress=True, chu
     padded, border, L_pad, batches, prog = chunk_plan(L, C, ov, bs)
     streams = max(1, int(DEMIX_STREAMS if streams is None else streams)) if torch.device(device).type == "cuda" else 1
     if not getattr(model, "multi_stream_ok", True):
-        streams = 1            # (models/bs_roformer.py)
+        streams = 1            # (a model whose forwards are not bit-identical across streams)
     E = exec_batch or getattr(model, "exec_batch", None) or plan_exec_batch(model, len(flat_plan(batches)), C,
                                                                             device, streams=streams)
     win = _Windows(C, device)

@@ -24,10 +24,9 @@ def _freqs(dim_head, theta=10000.0):
 
 class BSRoformer(NativeModule):
     """Reference-compatible BS-Roformer module (torch.nn.Module) backed by the native HIP forward."""
-    # round 6: with two forwards in flight the 4-min vocals track differs from the one-stream run in 500-4600 of 21 M
-    # samples (max 3.7e-3; bf16x3 and fp16 alike, workspaces zeroed or not; tools/streams_check.py) -- cause open, so
-    # BS-Roformer / Mel-Band-Roformer forwards stay on one stream
-    multi_stream_ok = False
+    # round 6: two forwards in flight differed from one stream in 500-4600 of the 4-min track's 21 M samples until the
+    # iSTFT's FFT stage barrier waited for the wave's own LDS writes (sesa_sync, DESIGN.md §6); now 0 differing
+    # (tools/streams_check.py, profiles/r06_sync_ab.txt), so the NativeModule default (multi-stream) holds
 
 
     _prefix = "bsr"

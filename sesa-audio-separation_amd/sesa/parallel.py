@@ -119,7 +119,7 @@ def local_accumulate_device(config, model, mix_d, plan, rank, rows, exec_batch, 
     win = _Windows(plan, device)
     main = torch.cuda.current_stream(device)
     if not getattr(model, "multi_stream_ok", True):
-        streams = 1            # (models/bs_roformer.py: not bit-identical across streams at full size)
+        streams = 1            # (a model whose forwards are not bit-identical across streams)
     pool = [main] + side_streams(device, max(1, int(streams)) - 1)
     xbufs = [None] * len(pool)
     freed = [None] * len(pool)    # event on main after the OLA that consumed the stream's last forward

@@ -182,7 +182,9 @@ _FULL_4MIN = {}
 def test_full_size_4min_properties(dev, precision):
     """configs[2] at full size (4-min track, BS-Roformer vocals config, 62 chunks at overlap 2), in the parity
     precision and in the one the bench line runs (fp16): the sharded path at world 1 equals demix_device
-    bit-for-bit, the vocals stem is finite, shaped [1, 2, L] and not degenerate (size-independent properties;
+    bit-for-bit, two forwards in flight on two streams equal one stream bit-for-bit (the iSTFT barrier fix, DESIGN.md
+    §6: 500-4600 samples differed before it), the vocals stem is finite, shaped [1, 2, L] and not degenerate
+    (size-independent properties;
     the oracle would need ~20 min of CPU); the fp16 stems agree with the bf16x3 ones within the 1e-4 gate (the
     bf16x3 path is itself pinned to the reference at 1e-6 on the full-chunk golden).
     Mirrors tests/test_gpu_parity.py::test_full_size_4min_properties."""
@@ -193,7 +195,9 @@ def test_full_size_4min_properties(dev, precision):
     rng = np.random.default_rng(0)
     mix = torch.from_numpy((0.1 * rng.standard_normal((2, L))).astype(np.float32)).to(dev)
     with contextlib.redirect_stdout(io.StringIO()):
-        a = demix_device(c, m, mix, dev, exec_batch=4)
+        a = demix_device(c, m, mix, dev, exec_batch=4, streams=1)
+        a2 = demix_device(c, m, mix, dev, exec_batch=4, streams=2)
+    assert torch.equal(a, a2), f"streams 2 vs 1: {int((a != a2).sum())} samples differ"
     b = demix_sharded(c, m, mix, dev, rank=0, world=1, exec_batch=4)
     assert a.shape == b.shape == (1, 2, L)
     assert torch.isfinite(a).all().item()

@@ -18,3 +18,23 @@ def test_no_packed_fp32_op_sel():
     n, hits = isa_guard.scan(LIB)
     assert n >= 8, "expected one gfx950 code object per HIP translation unit"
     assert not hits, f"{len(hits)} v_pk_*_f32 with op_sel, e.g. {hits[:3]}"
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
+                    reason="needs the built libsesa and the ROCm LLVM tools")
+def test_no_barrier_with_lds_writes_in_flight():
+    """Every s_barrier is reached with the wave's own LDS writes retired (tools/barrier_scan.py; sesa_sync): the
+    compiler-omitted lgkmcnt wait at the FFT stage barrier was the BS-Roformer cross-stream discrepancy."""
+    import barrier_scan
+    import isa_guard
+    import subprocess
+    import tempfile
+    bad = []
+    with tempfile.TemporaryDirectory() as td:
+        for n, img in enumerate(isa_guard.device_images(LIB)):
+            f = os.path.join(td, f"co{n}.o")
+            open(f, "wb").write(img)
+            asm = subprocess.run([os.path.join(isa_guard.LLVM, "llvm-objdump"), "-d", "--mcpu=gfx950",
+                                  "--no-show-raw-insn", f], capture_output=True, text=True, check=True).stdout
+            bad += [fn for fn, body in barrier_scan.functions(asm) if barrier_scan.scan_fn(body, {"w"})]
+    assert not bad, f"{len(bad)} kernels reach an s_barrier with LDS writes in flight, e.g. {bad[:3]}"
