@@ -30,6 +30,10 @@ if [[ $PART == *p* ]]; then
     local m=$1; shift
     step pmc $m
     timeout -k 10 800 bash tools/pmc_refresh.sh $m "$@" > $O/pmc_$m.log 2>&1
+    if [ $m = mdx23c ]; then   # the streaming classes (STFT / iSTFT / gather + OLA) from the same two passes
+      timeout -k 10 120 python3 tools/pmc_stream.py gpurun_out/pmc_mdx23c_f gpurun_out/pmc_mdx23c_w mdx23c \
+        "$(python3 -c 'import bench; print(bench.default_precision("mdx23c"))')" gpurun_out > $O/pmc_stream.log 2>&1
+    fi
     rm -rf gpurun_out/pmc_*_f gpurun_out/pmc_*_w
   }
   pmc mdx23c "conv3x3=conv3x3_db_kernel<true, true, 0, false, 1, true|conv3x3_db_kernel<true, false, 0, false, 1, true" \
@@ -40,7 +44,8 @@ if [[ $PART == *p* ]]; then
     "simt=htd_dc_|htd_item_stats|htd_gn_apply|htd_norm_freq|htd_norm_time" "attn=attn_kernel|attn_f16_kernel"
   pmc ensemble "conv3x3=conv3x3_db_kernel|tap_gemm_kernel<3, 3" "tokgemm=tok_gemm_glds_kernel|tok_gemm_kernel"
   mkdir -p $O/pmc
-  cp gpurun_out/pmc_*_*.json $O/pmc/ 2>/dev/null || true
+  cp gpurun_out/pmc_*_*.json gpurun_out/pmc_stft.json gpurun_out/pmc_istft.json gpurun_out/pmc_ola.json $O/pmc/ \
+    2>/dev/null || true
   ls $O/pmc
 fi
 if [[ $PART == *b* ]]; then
