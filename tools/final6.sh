@@ -50,8 +50,9 @@ if [[ $PART == *p* ]]; then
 fi
 if [[ $PART == *b* ]]; then
   [ -d $O/pmc ] && cp $O/pmc/pmc_*.json profiles/ 2>/dev/null || true
-  line() {  # NAME SECONDS ARGS...
+  line() {  # NAME SECONDS ARGS...   (LINES="a b ..." runs only those)
     local n=$1 s=$2; shift 2
+    [ -z "$LINES" ] || [[ " $LINES " == *" $n "* ]] || return 0
     step bench $n
     timeout -k 10 $s python bench.py "$@" > $O/bench_$n.json 2> $O/bench_$n.err
     python3 -c "
