@@ -63,8 +63,9 @@ ENSEMBLE = ("mdx23c", "bs_roformer", "scnet")
 # forwards in flight per rank (sesa/parallel.py local_accumulate_device; re-entrant per stream since round 6).  Same box,
 # --streams 1 vs 2 (profiles/r06_streams_ab.txt): HTDemucs 1282 -> 1342x (the 30-min track's 11 forwards overlap their
 # low-occupancy tails), MDX23C 270.4 -> 274.2x, BS-Roformer 216.2 -> 219.8x (bit-identical to one stream since the
-# iSTFT barrier fix); SCNet runs one forward per step and the ensemble's members run one after another
-DEFAULT_STREAMS = {"htdemucs": 2, "mdx23c": 2, "bs_roformer": 2}
+# iSTFT barrier fix); SCNet runs one forward per step.  The ensemble's members run one after another, each
+# with two forwards in flight (ensemble_separate streams=)
+DEFAULT_STREAMS = {"htdemucs": 2, "mdx23c": 2, "bs_roformer": 2, "ensemble": 2}
 MODELS["ensemble"] = (None, sum(MODELS[m][1] for m in ENSEMBLE), None)
 METRIC = {"ensemble": "separated-audio sec/sec (RTF), ensemble mdx23c + bs_roformer + scnet (vocals, avg_wave), MI355X",
           "mdx23c": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X",
@@ -703,7 +704,7 @@ def main():
             mix_d = mix_host.to(dev, non_blocking=True) if pcie else mix_dev
         if args.model == "ensemble":
             est = ensemble_separate([(cfg, m) for m, cfg, _ in members], mix_d, "vocals", args.blend, rank=rank,
-                                    world=pworld, exec_batch=batches, simulate=sim)[0]
+                                    world=pworld, exec_batch=batches, simulate=sim, streams=args.streams)[0]
         elif owned:
             m, cfg, _ = members[0]
             est = demix_owned(cfg, m, mix_d, dev, rank=rank, world=pworld, exec_batch=batches[0], mode=modes[0],

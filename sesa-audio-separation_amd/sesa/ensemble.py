@@ -57,7 +57,7 @@ def blend_device(waves, method, weights=None, buffer=32768):
 
 def ensemble_separate(members, mix_d, stem="vocals", method="avg_wave", weights=None, buffer=32768, rank=None,
                       world=None, exec_batch=None, group=None, demix_hooks=None, blend_fn=None, gather_to=0,
-                      simulate=False):
+                      simulate=False, streams=1):
     """Multi-model ensemble of one track, all on the device (BASELINE configs[4]).
 
     The GUI's ensemble flow (processing.py:266-363 runs inference.py once per model, then
@@ -67,7 +67,8 @@ def ensemble_separate(members, mix_d, stem="vocals", method="avg_wave", weights=
     ``gather_to``), the members' ``stem`` outputs are stacked and blended with ``sesa_blend_f32``
     (ensemble.py:258-407 semantics, float64) on that rank.  Returns (blend [2, L] float64, {member index:
     stem [2, L] float32}) there and (None, {}) on the other ranks (``gather_to=None``: every rank blends).
-    ``exec_batch``: chunks per forward, a list (one per member) or an int.  ``demix_hooks`` (local_fn /
+    ``exec_batch``: chunks per forward, a list (one per member) or an int.  ``streams``: forwards of each member in
+    flight on side streams (bit-identical to 1, include/sesa.h).  ``demix_hooks`` (local_fn /
     counter_fn / finalize_fn of demix_sharded) and ``blend_fn`` exist so the CPU test-suite can drive the
     sharding, the collectives and the member loop over gloo ranks with the oracle's OLA and blend."""
     from .config import prefer_target_instrument
@@ -81,7 +82,7 @@ def ensemble_separate(members, mix_d, stem="vocals", method="avg_wave", weights=
                 raise ValueError(f"ensemble member {i} has no '{stem}' stem (instruments: {names})")
             eb = exec_batch[i] if isinstance(exec_batch, (list, tuple)) else (exec_batch or 8)
             est = demix_sharded(cfg, model, mix_d, mix_d.device, rank=rank, world=world, exec_batch=eb, group=group,
-                                gather_to=gather_to, simulate=simulate, **(demix_hooks or {}))
+                                gather_to=gather_to, simulate=simulate, streams=streams, **(demix_hooks or {}))
             if est is not None:
                 stems.append(est[names.index(stem)])
     finally:
