@@ -63,9 +63,10 @@ ENSEMBLE = ("mdx23c", "bs_roformer", "scnet")
 # forwards in flight per rank (sesa/parallel.py local_accumulate_device; re-entrant per stream since round 6).  Same box,
 # --streams 1 vs 2 (profiles/r06_streams_ab.txt): HTDemucs 1282 -> 1342x (the 30-min track's 11 forwards overlap their
 # low-occupancy tails), MDX23C 270.4 -> 274.2x, BS-Roformer 216.2 -> 219.8x (bit-identical to one stream since the
-# iSTFT barrier fix); SCNet runs one forward per step.  The ensemble's members run one after another, each
-# with two forwards in flight (ensemble_separate streams=)
-DEFAULT_STREAMS = {"htdemucs": 2, "mdx23c": 2, "bs_roformer": 2, "ensemble": 2}
+# iSTFT barrier fix); SCNet runs one forward per step.  The ensemble's members run one after another
+# (--streams 2 gives each member two forwards in flight, ensemble_separate streams=; each member then plans its
+# execution batch against the same free HBM, so it stays opt-in)
+DEFAULT_STREAMS = {"htdemucs": 2, "mdx23c": 2, "bs_roformer": 2}
 MODELS["ensemble"] = (None, sum(MODELS[m][1] for m in ENSEMBLE), None)
 METRIC = {"ensemble": "separated-audio sec/sec (RTF), ensemble mdx23c + bs_roformer + scnet (vocals, avg_wave), MI355X",
           "mdx23c": "separated-audio sec/sec (RTF), MDX23C 44.1kHz stereo, 1/2/4/8 MI355X",

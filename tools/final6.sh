@@ -68,7 +68,7 @@ print(sys.argv[2], d['value'], d['ms_per_step'], r['class'], r['frac'], r.get('t
   line htdemucs 700 --model htdemucs --steps 2 --warmup 1 --cpu-sample-chunks 8
   line htdemucs_share8 300 --model htdemucs --rank-share 8 --steps 3 --warmup 1 --no-cpu-baseline --no-parity
   line ensemble 900 --model ensemble --steps 2 --warmup 1
-  line ensemble_streams1 600 --model ensemble --steps 2 --warmup 1 --streams 1 --no-cpu-baseline --no-parity
+  line ensemble_streams2 600 --model ensemble --steps 2 --warmup 1 --streams 2 --no-cpu-baseline --no-parity
 fi
 if [[ $PART == *c* ]]; then
   prof() {  # NAME ARGS...
