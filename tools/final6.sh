@@ -26,8 +26,9 @@ if [[ $PART == *t* ]]; then
   tail -2 $O/smoke.log
 fi
 if [[ $PART == *p* ]]; then
-  pmc() {  # MODEL SPEC...
+  pmc() {  # MODEL SPEC...   (PMC_MODELS="a b ..." runs only those)
     local m=$1; shift
+    [ -z "$PMC_MODELS" ] || [[ " $PMC_MODELS " == *" $m "* ]] || return 0
     step pmc $m
     timeout -k 10 800 bash tools/pmc_refresh.sh $m "$@" > $O/pmc_$m.log 2>&1
     if [ $m = mdx23c ]; then   # the streaming classes (STFT / iSTFT / gather + OLA) from the same two passes
