@@ -11,7 +11,9 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 # the precision the default bench line of this model runs in (bench.py default_precision), stamped into the
 # summaries (bench.py reports traffic only for a run in the same mode)
 P=$(python3 -c "import bench; print(bench.default_precision('$M'))")
-B="python3 bench.py --model $M --steps 1 --warmup 0 --no-cpu-baseline --no-parity --no-pcie --precision $P"
+# --streams 1: one step, every launch in it a libsesa profile record (with several streams bench.py adds a single-stream
+# roofline pass, and the counters would see both passes against one pass of records)
+B="python3 bench.py --model $M --steps 1 --warmup 0 --streams 1 --no-cpu-baseline --no-parity --no-pcie --precision $P"
 O=gpurun_out
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_${M}_f -o run -- $B > $O/pmc_${M}_f.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_${M}_w -o run -- $B > $O/pmc_${M}_w.log 2>&1
