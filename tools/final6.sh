@@ -75,7 +75,8 @@ if [[ $PART == *c* ]]; then
   prof() {  # NAME ARGS...
     local n=$1; shift
     step rocprof $n
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$n -o run -- python3 bench.py "$@" --no-cpu-baseline \
+    # --streams 1: the kernel averages then match the single-stream pass the bench line's roofline is timed on
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$n -o run -- python3 bench.py "$@" --streams 1 --no-cpu-baseline \
       --no-parity --no-pcie > $O/prof_$n.json 2> $O/prof_$n.err
     python3 tools/rocprof_summary.py $O/prof_$n $O/kernel_stats_$n.txt > /dev/null
     rm -rf $O/prof_$n
